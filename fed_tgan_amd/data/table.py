@@ -1,0 +1,171 @@
+"""Local table preprocessing, meta generation and label encoding.
+
+Behavioural parity with the reference ``FileGenerator`` (`Server/dtds/data/utils/
+file_generator.py:59-265`) and ``prepare_data`` / ``encode_data_with_meta_labelencoder``
+(`Server/dtds/data/load.py:51-90`):
+
+* integer columns are detected on the raw frame (int dtype, or float whose non-null
+  values are whole numbers) (`file_generator.py:104-110`);
+* blank cells become NaN then the literal ``"empty"`` (`:115-116`);
+* every non-categorical, non-date column listed as non-negative is mapped by
+  ``log(x + 1)`` (`:118-126`);
+* date columns are split into categorical parts (`:129-133`, see :mod:`.date`);
+* ``local_meta()`` returns the reference meta dict, with per-category value counts in
+  ``i2s`` (`:191-231`), the ``"continous"`` spelling and ``"column no"``;
+* ``encode(vocabs)`` label-encodes categoricals with the *global* vocabularies
+  (``astype(str)`` first, `:163-167`) and returns the numeric training matrix.
+
+The reference round-trips the encoded matrix through ``dtds/saved_models/.../*.npz`` on
+disk before reading it back (`load.py:38-48, 72-90`); we keep that artefact optional
+(``write_artifacts``) and hand the matrix over in memory.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import os
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import pandas as pd
+
+from .constants import CATEGORICAL, EMPTY, META_CONTINUOUS
+from .date import split_dates
+from .vocab import CategoryVocab
+
+
+class NumpyJSONEncoder(json.JSONEncoder):
+    """JSON encoder for numpy scalars/arrays (meta files contain numpy ints/floats)."""
+
+    def default(self, o):  # noqa: D401
+        if isinstance(o, np.integer):
+            return int(o)
+        if isinstance(o, np.floating):
+            return float(o)
+        if isinstance(o, np.bool_):
+            return bool(o)
+        if isinstance(o, np.ndarray):
+            return o.tolist()
+        if isinstance(o, complex):
+            return {"real": o.real, "imag": o.imag}
+        return super().default(o)
+
+
+def dump_meta_json(meta: dict, path: str) -> None:
+    with open(path, "w") as f:
+        json.dump(meta, f, sort_keys=True, indent=4, separators=(",", ": "), cls=NumpyJSONEncoder)
+
+
+def timestamp_token() -> str:
+    """The reference's folder/file timestamp token (`file_generator.py:97`)."""
+    return str(datetime.datetime.now().timestamp()).replace(".", "")
+
+
+def detect_integer_columns(df: pd.DataFrame) -> List[str]:
+    out = []
+    for c in df.columns:
+        s = df[c].dropna()
+        kind = s.dtype.kind
+        if kind in "iu":
+            out.append(c)
+        elif kind == "f":
+            v = s.to_numpy()
+            if np.all(np.isfinite(v)) and np.array_equal(v, np.trunc(v)):
+                out.append(c)
+    return out
+
+
+class TablePreprocessor:
+    """One client's view of its local CSV (the reference ``FileGenerator``)."""
+
+    def __init__(self, frame: pd.DataFrame, file_name: str, problem_type: str, target_col: str,
+                 categorical_list: Sequence[str], non_negative_columns: Sequence[str],
+                 date_columns: Optional[Dict[str, str]] = None, synthesizer_used: str = "CTGANSynthesizer"):
+        self.file_name = file_name.strip()
+        self.problem_type = problem_type.strip()
+        self.target_col = target_col.strip()
+        self.non_negative_columns = list(non_negative_columns)
+        self.date_columns = dict(date_columns or {})
+        self.synthesizer_used = synthesizer_used.strip()
+        self.output_name = f"{self.file_name}_{self.synthesizer_used}-{timestamp_token()}"
+
+        self.integer_columns = detect_integer_columns(frame)
+        df = frame.replace(r" ", np.nan).fillna(EMPTY)
+        categorical = list(categorical_list) + [d for d in self.date_columns if d not in categorical_list]
+        untouched = set(categorical) | set(self.date_columns)
+        for c in df.columns:
+            if c not in untouched and c in self.non_negative_columns:
+                df[c] = np.log(df[c].astype(np.float64) + 1.0)
+        if self.date_columns:
+            df, categorical = split_dates(df, self.date_columns, categorical)
+        self.categorical_list = categorical
+        self.df = df
+
+    # ------------------------------------------------------------------ meta
+    def local_meta(self) -> dict:
+        cols = []
+        for pos, c in enumerate(self.df.columns):
+            entry: dict = {"column_name": c}
+            if c in self.categorical_list:
+                counts = self.df[c].astype(str).value_counts()
+                entry["type"] = CATEGORICAL
+                entry["size"] = int(len(counts))
+                entry["i2s"] = {str(k): int(v) for k, v in counts.items()}
+            else:
+                entry["type"] = META_CONTINUOUS
+                entry["min"] = self.df[c].min()
+                entry["max"] = self.df[c].max()
+            entry["column no"] = pos
+            cols.append(entry)
+        meta = {
+            "columns": cols,
+            "problem_type": self.problem_type,
+            "name": self.output_name,
+            "date_info": self.date_columns,
+            "integer_info": self.integer_columns,
+            "non_negative_cols": self.non_negative_columns,
+        }
+        if self.target_col:
+            meta["target"] = self.target_col
+        return meta
+
+    # ------------------------------------------------------------------ encode
+    def encode(self, vocabs: Sequence[CategoryVocab]) -> np.ndarray:
+        """Label-encode with the global vocabularies; returns float64 [rows, cols]."""
+        out = np.empty((len(self.df), self.df.shape[1]), dtype=np.float64)
+        cursor = 0
+        for j, c in enumerate(self.df.columns):
+            if c in self.categorical_list:
+                out[:, j] = vocabs[cursor].transform(self.df[c].astype(str).to_numpy())
+                cursor += 1
+            else:
+                out[:, j] = pd.to_numeric(self.df[c]).to_numpy(dtype=np.float64)
+        return out
+
+    def categorical_indices(self) -> List[int]:
+        return [j for j, c in enumerate(self.df.columns) if c in self.categorical_list]
+
+    def write_artifacts(self, meta: dict, encoded: np.ndarray, timestamp: str,
+                        root: str = "dtds/saved_models") -> str:
+        """Reference-compatible on-disk dump (`file_generator.py:156-188`)."""
+        name = f"{self.file_name}_{self.synthesizer_used}-{timestamp}"
+        path = os.path.join(root, name)
+        os.makedirs(path, mode=0o760, exist_ok=True)
+        dump_meta_json(meta, os.path.join(path, name + ".json"))
+        np.savez(os.path.join(path, name + ".npz"), train=encoded, test=encoded[:0])
+        frame = pd.DataFrame(encoded, columns=self.df.columns)
+        frame.to_csv(os.path.join(path, name + ".csv"), index=False)
+        return path
+
+
+def categorical_columns_of(meta: dict) -> List[int]:
+    """Indices of categorical columns in a meta dict (`load.py:26-35`)."""
+    return [i for i, c in enumerate(meta["columns"]) if c["type"] == CATEGORICAL]
+
+
+def load_table(path: str, spec) -> TablePreprocessor:
+    frame = pd.read_csv(path)
+    stem = os.path.splitext(os.path.basename(path))[0]
+    return TablePreprocessor(frame[spec.selected_variables], stem, spec.problem_type,
+                             "" if spec.target_column == "none" else spec.target_column,
+                             spec.categorical_list, spec.nonnegative_list, spec.date_dic)

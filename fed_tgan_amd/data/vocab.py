@@ -1,0 +1,57 @@
+"""Label vocabularies (sklearn ``LabelEncoder`` semantics without the sklearn object).
+
+The reference fits one sklearn ``LabelEncoder`` per categorical column on the
+frequency-sorted global vocabulary (`Server/dtds/distributed.py:621-624`): codes are the
+positions in the *lexicographically* sorted unique string list.  ``CategoryVocab`` keeps
+exactly that mapping as a plain sorted ``numpy`` string array so it can be broadcast
+as a list over the control plane and used inside native decode kernels; it converts
+to / from sklearn ``LabelEncoder`` objects for the ``label_encoders_{name}.pickle`` artefact.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Sequence
+
+import numpy as np
+
+
+class CategoryVocab:
+    __slots__ = ("column_name", "classes_")
+
+    def __init__(self, classes: Iterable[str], column_name: str = ""):
+        arr = np.asarray([str(c) for c in classes], dtype=object)
+        self.classes_ = np.asarray(sorted(set(arr.tolist())), dtype=object)
+        self.column_name = column_name
+
+    # --- LabelEncoder-compatible surface -------------------------------------------------
+    def transform(self, values: Sequence) -> np.ndarray:
+        vals = np.asarray([str(v) for v in values], dtype=object)
+        # object arrays of python str sort consistently with sorted()
+        idx = np.searchsorted(self.classes_, vals)
+        idx = np.clip(idx, 0, len(self.classes_) - 1)
+        bad = self.classes_[idx] != vals
+        if np.any(bad):
+            raise ValueError(f"y contains previously unseen labels: {sorted(set(vals[bad].tolist()))[:5]}")
+        return idx.astype(np.int64)
+
+    def inverse_transform(self, codes: Sequence) -> np.ndarray:
+        codes = np.asarray(codes, dtype=np.int64)
+        return self.classes_[codes]
+
+    def __len__(self) -> int:
+        return len(self.classes_)
+
+    def tolist(self) -> List[str]:
+        return self.classes_.tolist()
+
+    def to_sklearn(self):
+        from sklearn.preprocessing import LabelEncoder
+        le = LabelEncoder()
+        le.classes_ = np.asarray(self.classes_.tolist())
+        return le
+
+    @classmethod
+    def from_sklearn(cls, le, column_name: str = "") -> "CategoryVocab":
+        return cls(le.classes_.tolist(), column_name)
+
+    def __repr__(self) -> str:
+        return f"CategoryVocab({self.column_name!r}, n={len(self)})"

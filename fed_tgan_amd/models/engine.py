@@ -1,0 +1,492 @@
+"""CTGANEngine — the production WGAN-GP training/generation path on flat buffers.
+
+Where the reference runs ``nn.Module`` forward passes plus autograd's double backward
+with ~3.8k ATen dispatches per step and host-side NumPy samplers
+(`Client/.../dtds/distributed.py:179-269`, `Server/dtds/synthesizers/ctgan.py:231-258`),
+this engine:
+
+* keeps every trainable tensor of G and D plus the BN running statistics in ONE flat fp32
+  buffer (``self.flat``: ``[theta_G | theta_D | BN buffers]``) so federated aggregation is a
+  single pre-scaled all-reduce and Adam is one fused multi-tensor kernel per network;
+* lays out activations concat-free: the generator's residual stack writes every layer's
+  ``ReLU(BN(.))`` into a column slice of one ``[B, E+n_opt+sum(gen_dims)]`` buffer, so
+  ``cat([out, input])`` (`ctgan.py:44`) is free; the discriminator's fake / real /
+  interpolated batches share one ``[3B, data_dim+n_opt]`` buffer whose packed view is the
+  PacGAN input (`ctgan.py:28-30`);
+* runs an **explicit** backward, including the hand-derived gradient-penalty double
+  backward (see ``_d_step``), as a short chain of GEMMs with fused epilogues;
+* draws conditional vectors, real rows, noise, Gumbel noise, dropout masks and slerp
+  weights on the device, so a whole step is a static sequence of kernel launches that is
+  captured once into a hipGraph and replayed.
+
+Step semantics follow the reference client exactly (`Client/.../distributed.py:185-265`):
+D step on ``loss_d = mean D(fake) - mean D(real) + GP`` then G step on
+``-mean D(fake) + cond_loss``; G's BN layers run in training mode in both phases; the
+gradients that the reference computes and then discards (G grads from the D phase, D
+grads from the G phase) are not computed.
+
+Gradient-penalty backward (D with hidden layers l = 0..L-1, weights V_l, dropout-masked
+LeakyReLU slopes MS_l = lrelu'(u_l) * mask_l, head vector v):
+    q_{L-1} = v * MS_{L-1};  q_{l-1} = (q_l V_l) * MS_{l-1};  g = q_0 V_0   (= dD/dx)
+    pen = lam * mean_p (|g_p| - 1)^2;   R_{-1} = dpen/dg
+    R_l = (R_{l-1} V_l^T) * MS_l;   dpen/dV_l = q_l^T R_{l-1};   dpen/dv = sum_p R_{L-1,p}
+Bias gradients of the penalty are exactly zero.  The same A-chain serves the WGAN terms
+of the fake/real rows (seed coefficient +-1/n_packs), so every weight gradient of the D
+step is ONE GEMM over the stacked [fake; real; interp] rows.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..features.transformer import SpanLayout
+from .ctgan import Discriminator, Generator
+from .samplers import CondTables, RowIndex
+
+EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU = 0, 1, 2, 3
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    embedding_dim: int = 128
+    gen_dims: Tuple[int, ...] = (256, 256)
+    dis_dims: Tuple[int, ...] = (256, 256)
+    batch_size: int = 500
+    pack: int = 10
+    lr: float = 2e-4
+    betas: Tuple[float, float] = (0.5, 0.9)
+    adam_eps: float = 1e-8
+    l2scale: float = 1e-6
+    tau: float = 0.2
+    gp_lambda: float = 10.0
+    lrelu_slope: float = 0.2
+    dropout_p: float = 0.5
+    bn_momentum: float = 0.1
+    bn_eps: float = 1e-5
+    gen_chunk: int = 8192
+
+
+def get_ops(backend: str, device: torch.device):
+    if backend == "auto":
+        backend = "hip" if device.type == "cuda" else "torch"
+    if backend == "torch":
+        from ..ops.ref import TorchOps
+        return TorchOps()
+    if backend == "hip":
+        from ..ops.hip import HipOps
+        return HipOps()
+    raise ValueError(backend)
+
+
+class CTGANEngine:
+    def __init__(self, layout: SpanLayout, cfg: EngineConfig | None = None, device="cpu", backend: str = "auto",
+                 seed: int | None = None):
+        self.cfg = cfg = cfg or EngineConfig()
+        self.layout = layout
+        self.device = torch.device(device)
+        self.ops = get_ops(backend, self.device)
+        self.seed = int(seed if seed is not None else torch.initial_seed() % (2 ** 31))
+        B, P = cfg.batch_size, cfg.pack
+        if B % P:
+            raise ValueError("batch_size must be a multiple of pack")
+        self.B, self.P, self.nP = B, P, B // P
+        self.E = cfg.embedding_dim
+        self.C = layout.n_opt
+        self.Dd = layout.data_dim
+        self.Din = self.Dd + self.C
+        self.K1 = P * self.Din
+        self.gdims = list(cfg.gen_dims)
+        self.ddims = list(cfg.dis_dims)
+        self.d0 = self.E + self.C
+        self.Hw = self.d0 + sum(self.gdims)
+        # column offsets in H: layer l (0-based) reads H[:, off[l]:], writes H[:, off[l+1]:off[l]]
+        off = [sum(self.gdims)]
+        for g in self.gdims:
+            off.append(off[-1] - g)
+        self.off = off            # off[0] = start of z, off[L] = 0
+        self.z_cols = (off[0], off[0] + self.E)
+        self.c_cols = (off[0] + self.E, self.Hw)
+        self.spans = [(int(s), int(w), int(k)) for s, w, k in zip(layout.start, layout.width, layout.kind)]
+        self.cond_spans = [(int(s), int(w)) for s, w in zip(layout.cond_start, layout.cond_width)]
+        self._build_params()
+        self._build_buffers()
+        self.tables: Dict[str, torch.Tensor] = {}
+        self.gen_tables = None
+        self._gen_bufs = None
+        self.graph = None
+        self.graph_steps = 0
+        self.bn_batches = 0       # num_batches_tracked of every BN layer
+
+    # ================================================================= parameters
+    def _build_params(self):
+        E, C, Dd = self.E, self.C, self.Dd
+        spec: List[Tuple[str, Tuple[int, ...], str]] = []
+        dim = E + C
+        for i, g in enumerate(self.gdims):
+            spec += [(f"G.{i}.W", (g, dim), "G"), (f"G.{i}.b", (g,), "G"),
+                     (f"G.{i}.gamma", (g,), "G"), (f"G.{i}.beta", (g,), "G")]
+            dim += g
+        spec += [("G.out.W", (Dd, dim), "G"), ("G.out.b", (Dd,), "G")]
+        dim = self.K1
+        for i, h in enumerate(self.ddims):
+            spec += [(f"D.{i}.W", (h, dim), "D"), (f"D.{i}.b", (h,), "D")]
+            dim = h
+        spec += [("D.out.W", (1, dim), "D"), ("D.out.b", (1,), "D")]
+        for i, g in enumerate(self.gdims):
+            spec += [(f"G.{i}.rm", (g,), "S"), (f"G.{i}.rv", (g,), "S")]
+        order = {"G": 0, "D": 1, "S": 2}
+        spec.sort(key=lambda t: order[t[2]])
+        self.param_spec = spec
+        sizes = [int(np.prod(s)) for _, s, _ in spec]
+        total = sum(sizes)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.p: Dict[str, torch.Tensor] = {}
+        pos = 0
+        self.group_range = {}
+        for (name, shape, grp), n in zip(spec, sizes):
+            self.p[name] = self.flat[pos:pos + n].view(shape)
+            a, _ = self.group_range.get(grp, (pos, pos))
+            self.group_range[grp] = (a, pos + n)
+            pos += n
+        gA, gB = self.group_range["G"]
+        dA, dB = self.group_range["D"]
+        self.nG, self.nD = gB - gA, dB - dA
+        self.flatG = self.flat[gA:gB]
+        self.flatD = self.flat[dA:dB]
+        self.gradG = torch.zeros(self.nG, dtype=torch.float32, device=self.device)
+        self.gradD = torch.zeros(self.nD, dtype=torch.float32, device=self.device)
+        self.g: Dict[str, torch.Tensor] = {}
+        for (name, shape, grp), n in zip(spec, sizes):
+            if grp == "S":
+                continue
+            base = self.p[name].data_ptr() - (self.flatG if grp == "G" else self.flatD).data_ptr()
+            buf = self.gradG if grp == "G" else self.gradD
+            o = base // 4
+            self.g[name] = buf[o:o + n].view(shape)
+        self.mG = torch.zeros_like(self.gradG)
+        self.vG = torch.zeros_like(self.gradG)
+        self.mD = torch.zeros_like(self.gradD)
+        self.vD = torch.zeros_like(self.gradD)
+        self.stepG = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.stepD = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        """PyTorch default init of the reference modules (Linear kaiming-uniform, BN 1/0)."""
+        G = Generator(self.E + self.C, self.gdims, self.Dd)
+        D = Discriminator(self.Din, self.ddims, self.P)
+        self.load_modules(G, D)
+        self.mG.zero_(); self.vG.zero_(); self.mD.zero_(); self.vD.zero_()
+        self.stepG.zero_(); self.stepD.zero_()
+
+    # --- reference-compatible state dicts ------------------------------------
+    def g_key_map(self) -> List[Tuple[str, str]]:
+        m = []
+        for i in range(len(self.gdims)):
+            m += [(f"seq.{i}.fc.weight", f"G.{i}.W"), (f"seq.{i}.fc.bias", f"G.{i}.b"),
+                  (f"seq.{i}.bn.weight", f"G.{i}.gamma"), (f"seq.{i}.bn.bias", f"G.{i}.beta"),
+                  (f"seq.{i}.bn.running_mean", f"G.{i}.rm"), (f"seq.{i}.bn.running_var", f"G.{i}.rv")]
+        L = len(self.gdims)
+        m += [(f"seq.{L}.weight", "G.out.W"), (f"seq.{L}.bias", "G.out.b")]
+        return m
+
+    def d_key_map(self) -> List[Tuple[str, str]]:
+        m = []
+        for i in range(len(self.ddims)):
+            m += [(f"seq.{3 * i}.weight", f"D.{i}.W"), (f"seq.{3 * i}.bias", f"D.{i}.b")]
+        L = len(self.ddims)
+        m += [(f"seq.{3 * L}.weight", "D.out.W"), (f"seq.{3 * L}.bias", "D.out.b")]
+        return m
+
+    def g_state_dict(self) -> Dict[str, torch.Tensor]:
+        sd = {k: self.p[n].detach().cpu().clone() for k, n in self.g_key_map()}
+        for i in range(len(self.gdims)):
+            sd[f"seq.{i}.bn.num_batches_tracked"] = torch.tensor(self.bn_batches, dtype=torch.int64)
+        return sd
+
+    def d_state_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: self.p[n].detach().cpu().clone() for k, n in self.d_key_map()}
+
+    def load_g_state_dict(self, sd):
+        with torch.no_grad():
+            for k, n in self.g_key_map():
+                self.p[n].copy_(sd[k].reshape(self.p[n].shape))
+        key = "seq.0.bn.num_batches_tracked"
+        if key in sd:
+            self.bn_batches = int(sd[key])
+
+    def load_d_state_dict(self, sd):
+        with torch.no_grad():
+            for k, n in self.d_key_map():
+                self.p[n].copy_(sd[k].reshape(self.p[n].shape))
+
+    def load_modules(self, G: Generator, D: Discriminator):
+        self.load_g_state_dict(G.state_dict())
+        self.load_d_state_dict(D.state_dict())
+
+    def to_modules(self) -> Tuple[Generator, Discriminator]:
+        G = Generator(self.E + self.C, self.gdims, self.Dd)
+        D = Discriminator(self.Din, self.ddims, self.P)
+        G.load_state_dict(self.g_state_dict())
+        D.load_state_dict(self.d_state_dict())
+        return G, D
+
+    # ================================================================= buffers
+    def _build_buffers(self):
+        dev, f32 = self.device, torch.float32
+        B, nP = self.B, self.nP
+        z = lambda *s: torch.zeros(*s, dtype=f32, device=dev)  # noqa: E731
+        self.H = z(B, self.Hw)
+        self.abuf = [z(B, g) for g in self.gdims]
+        self.nhat = [z(B, g) for g in self.gdims]
+        self.bn_mean = [z(g) for g in self.gdims]
+        self.bn_invstd = [z(g) for g in self.gdims]
+        self.da = [z(B, g) for g in self.gdims]
+        self.logits = z(B, self.Dd)
+        self.dlogits = z(B, self.Dd)
+        self.dH = z(B, self.Hw)
+        self.Xd = z(3 * B, self.Din)
+        self.X = self.Xd.view(3 * nP, self.K1)
+        self.dact = None
+        self.dl = [z(3 * nP, h) for h in self.ddims]
+        self.ms = [z(3 * nP, h) for h in self.ddims]
+        self.A = [z(3 * nP, h) for h in self.ddims]
+        self.y = z(3 * nP)
+        self.gbuf = z(nP, self.K1)
+        inv = 1.0 / nP
+        self.coef3 = torch.cat([torch.full((nP,), inv), torch.full((nP,), -inv), torch.ones(nP)]).to(dev, f32)
+        self.wloss3 = torch.cat([torch.full((nP,), inv), torch.full((nP,), -inv), torch.zeros(nP)]).to(dev, f32)
+        self.coefg = torch.full((nP,), -inv, dtype=f32, device=dev)
+        self.col = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.opt = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
+
+    # ================================================================= data
+    def set_training_data(self, encoded: np.ndarray, rows: RowIndex | None = None, cond: CondTables | None = None):
+        lay = self.layout
+        rows = rows or RowIndex(encoded, lay)
+        cond = cond or CondTables.from_encoded(encoded, lay)
+        dev = self.device
+        t = {
+            "data": torch.as_tensor(np.ascontiguousarray(encoded, dtype=np.float32), device=dev),
+            "cdf_log": torch.as_tensor(cond.cdf_log, dtype=torch.float32, device=dev),
+            "cdf_emp": torch.as_tensor(cond.cdf_emp, dtype=torch.float32, device=dev),
+            "cond_offset": torch.as_tensor(lay.cond_offset, dtype=torch.int32, device=dev),
+            "cond_width": torch.as_tensor(lay.cond_width, dtype=torch.int32, device=dev),
+            "cond_start": torch.as_tensor(lay.cond_start, dtype=torch.int32, device=dev),
+            "row_offset": torch.as_tensor(rows.offset, dtype=torch.int64, device=dev),
+            "row_count": torch.as_tensor(rows.count, dtype=torch.int64, device=dev),
+            "rows": torch.as_tensor(rows.rows, dtype=torch.int64, device=dev),
+        }
+        self.n_rows = len(encoded)
+        self.tables = t
+        self.steps_per_epoch = len(encoded) // self.B
+        self.graph = None
+
+    def set_generation_tables(self, cond: CondTables, transformer):
+        """Tables for sample_zero + fused decode (transformer: a fitted VGMTransformer)."""
+        dev = self.device
+        self.gen_cond = {
+            "cdf_emp": torch.as_tensor(cond.cdf_emp, dtype=torch.float32, device=dev),
+            "cond_offset": torch.as_tensor(self.layout.cond_offset, dtype=torch.int32, device=dev),
+            "cond_width": torch.as_tensor(self.layout.cond_width, dtype=torch.int32, device=dev),
+        }
+        mu, sd = transformer.decode_tables()
+        cols = []
+        pos = 0
+        c = 0
+        for j, m in enumerate(transformer.meta):
+            if m["type"] == "continuous":
+                nv = int(transformer.components[c].sum())
+                cols.append((0, pos, nv, c, None))
+                pos += 1 + nv
+                c += 1
+            else:
+                w = int(m["size"])
+                codes = torch.as_tensor(np.asarray(m["i2s"], dtype=np.float64), device=dev)
+                cols.append((1, pos, w, -1, codes))
+                pos += w
+        self.gen_tables = {"cols": cols, "mu": torch.as_tensor(mu, dtype=torch.float64, device=dev),
+                           "sd": torch.as_tensor(sd, dtype=torch.float64, device=dev)}
+        self._gen_bufs = None
+
+    # ================================================================= forward pieces
+    def _g_forward(self, H, logits, training: bool, nhat=True):
+        o = self.ops
+        for i, g in enumerate(self.gdims):
+            a, b_ = self.off[i], self.off[i + 1]
+            o.linear_bn_relu(H[:, a:], self.p[f"G.{i}.W"], self.p[f"G.{i}.b"], self.p[f"G.{i}.gamma"],
+                             self.p[f"G.{i}.beta"], H[:, b_:a],
+                             self.abuf[i] if nhat else None, self.nhat[i] if nhat else None,
+                             self.bn_mean[i], self.bn_invstd[i], self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
+                             training, self.cfg.bn_momentum, self.cfg.bn_eps)
+        o.gemm(H, self.p["G.out.W"], logits, tb=True, bias=self.p["G.out.b"])
+
+    def _d_forward(self, rows: slice, stream_base: int):
+        o = self.ops
+        inp = self.X[rows]
+        for i in range(len(self.ddims)):
+            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][rows], tb=True, bias=self.p[f"D.{i}.b"], epi=EPI_LRELU_DROPOUT,
+                   ms=self.ms[i][rows], slope=self.cfg.lrelu_slope, p_drop=self.cfg.dropout_p,
+                   stream_id=stream_base + i)
+            inp = self.dl[i][rows]
+
+    def _a_chain(self, rows: slice):
+        o = self.ops
+        for i in range(len(self.ddims) - 1, 0, -1):
+            o.gemm(self.A[i][rows], self.p[f"D.{i}.W"], self.A[i - 1][rows], epi=EPI_MASK, ms=self.ms[i - 1][rows])
+
+    # ================================================================= steps
+    def _d_step(self):
+        o, B, nP = self.ops, self.B, self.nP
+        L = len(self.ddims)
+        o.sample_train(self.tables, B, self.H, self.c_cols, self.z_cols, self.Xd[0:B, self.Dd:], self.Xd[B:2 * B],
+                       self.col, self.opt, stream_id=1)
+        self._g_forward(self.H, self.logits, training=True)
+        o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=2)
+        o.slerp(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], stream_id=3)
+        allr = slice(0, 3 * nP)
+        I = slice(2 * nP, 3 * nP)
+        self._d_forward(allr, stream_base=4)
+        o.d_head(self.dl[L - 1], self.ms[L - 1], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coef3,
+                 self.wloss3, self.y, self.A[L - 1], self.metrics[0:1])
+        self._a_chain(allr)
+        # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
+        o.gemm(self.A[0][I], self.p["D.0.W"], self.gbuf)
+        o.gp_scale(self.gbuf, self.X[I], self.cfg.gp_lambda, self.metrics[1:2])
+        inp = self.X[I]
+        for i in range(L):
+            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I])
+            inp = self.dl[i][I]
+        # weight gradients: one GEMM per layer over the stacked rows
+        fr = slice(0, 2 * nP)
+        prev = self.X
+        for i in range(L):
+            o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True)
+            o.colsum(self.A[i][fr], self.g[f"D.{i}.b"])
+            prev = self.dl[i]
+        o.gemm(self.dl[L - 1], self.coef3.view(-1, 1), self.g["D.out.W"].view(-1, 1), ta=True)
+        self.g["D.out.b"].zero_()
+        b1, b2 = self.cfg.betas
+        o.adam(self.flatD, self.gradD, self.mD, self.vD, self.stepD, self.cfg.lr, b1, b2, self.cfg.adam_eps, 0.0)
+
+    def _g_step(self):
+        o, B, nP = self.ops, self.B, self.nP
+        L = len(self.ddims)
+        o.sample_train(self.tables, B, self.H, self.c_cols, self.z_cols, self.Xd[0:B, self.Dd:], None,
+                       self.col, self.opt, stream_id=11)
+        self._g_forward(self.H, self.logits, training=True)
+        o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=12)
+        fk = slice(0, nP)
+        self._d_forward(fk, stream_base=14)
+        o.d_head(self.dl[L - 1][fk], self.ms[L - 1][fk], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coefg,
+                 self.coefg, self.y[fk], self.A[L - 1][fk], self.metrics[2:3])
+        self._a_chain(fk)
+        o.gemm(self.A[0][fk], self.p["D.0.W"], self.gbuf)            # d(-mean D)/dX, packed
+        dx = self.gbuf.view(B, self.Din)
+        o.act_bwd_ce(dx[:, :self.Dd], self.Xd[0:B, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
+                     self.opt, self.dlogits, self.metrics[3:4], self.cfg.tau)
+        # generator backward
+        Lg = len(self.gdims)
+        o.gemm(self.dlogits, self.H, self.g["G.out.W"], ta=True)
+        o.colsum(self.dlogits, self.g["G.out.b"])
+        top = self.off[0]
+        if Lg:
+            o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
+        for i in range(Lg - 1, -1, -1):
+            a, b_ = self.off[i], self.off[i + 1]
+            o.bn_relu_bwd(self.dH[:, b_:a], self.H[:, b_:a], self.nhat[i], self.p[f"G.{i}.gamma"],
+                          self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"])
+            o.gemm(self.da[i], self.H[:, a:], self.g[f"G.{i}.W"], ta=True)
+            o.colsum(self.da[i], self.g[f"G.{i}.b"])
+            if i > 0:
+                o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0)
+        b1, b2 = self.cfg.betas
+        o.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
+               self.cfg.l2scale)
+
+    def _one_step(self):
+        if hasattr(self.ops, "begin_step"):
+            self.ops.begin_step(self)
+        self._d_step()
+        self._g_step()
+        if hasattr(self.ops, "end_step"):
+            self.ops.end_step(self)
+
+    def train_steps(self, n: int, use_graph: bool | None = None):
+        if not self.tables:
+            raise RuntimeError("set_training_data() first")
+        if use_graph is None:
+            use_graph = self.device.type == "cuda"
+        if use_graph:
+            if self.graph is None:
+                self._capture()
+            for _ in range(n):
+                self.graph.replay()
+        else:
+            for _ in range(n):
+                self._one_step()
+        self.bn_batches += 2 * n
+
+    def train_epoch(self, use_graph: bool | None = None):
+        self.train_steps(self.steps_per_epoch, use_graph)
+
+    def _capture(self):
+        # warm up on a side stream (allocator / lazy init), then capture one step
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        snap = self.flat.clone(), self.mG.clone(), self.vG.clone(), self.mD.clone(), self.vD.clone(), \
+            self.stepG.clone(), self.stepD.clone()
+        with torch.cuda.stream(s):
+            self._one_step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        # restore state so the warm-up step does not count
+        for dst, src in zip((self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD), snap):
+            dst.copy_(src)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._one_step()
+        self.graph = g
+
+    def losses(self) -> Tuple[float, float]:
+        m = self.metrics.detach().cpu().numpy()
+        return float(m[0] + m[1]), float(m[2] + m[3])
+
+    # ================================================================= generation
+    @torch.no_grad()
+    def generate_encoded(self, n: int) -> torch.Tensor:
+        """Activated generator output for n rows (eval BN): [n, data_dim]."""
+        out = torch.empty(n, self.Dd, device=self.device)
+        for a in range(0, n, self.cfg.gen_chunk):
+            b = min(n, a + self.cfg.gen_chunk)
+            H, logits = self._gen_buffers(b - a)
+            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, stream_id=21)
+            self._g_forward(H, logits, training=False, nhat=False)
+            self.ops.activate(logits, out[a:b], self.spans, self.cfg.tau, stream_id=22)
+        return out
+
+    @torch.no_grad()
+    def generate_decoded(self, n: int) -> torch.Tensor:
+        """Fused sample -> G(eval) -> Gumbel-argmax/tanh decode: [n, n_cols] float64 on device."""
+        if self.gen_tables is None:
+            raise RuntimeError("set_generation_tables() first")
+        out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
+        for a in range(0, n, self.cfg.gen_chunk):
+            b = min(n, a + self.cfg.gen_chunk)
+            H, logits = self._gen_buffers(b - a)
+            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, stream_id=21)
+            self._g_forward(H, logits, training=False, nhat=False)
+            self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23)
+        return out
+
+    def _gen_buffers(self, n: int):
+        if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n:
+            m = max(n, min(self.cfg.gen_chunk, n))
+            self._gen_bufs = (torch.zeros(m, self.Hw, device=self.device),
+                              torch.zeros(m, self.Dd, device=self.device))
+        H, lg = self._gen_bufs
+        return H[:n], lg[:n]

@@ -1,0 +1,245 @@
+"""Eager-PyTorch reference implementations of every fused op the engine uses.
+
+Each method here states the math of one fused HIP kernel in ``csrc/kernels`` with plain
+PyTorch ops.  It is (a) the CPU execution path (gloo demos, CI without a GPU) and
+(b) the numerics oracle the HIP kernels are tested against.  Signatures are shared with
+:class:`fed_tgan_amd.ops.hip.HipOps`; outputs are written in place into (possibly
+strided, column-sliced) views so that the engine's concat-free buffer layout works on
+both paths.
+
+Randomness comes from the global torch generator of the tensor's device (the HIP path
+uses counter-based Philox streams instead, so the two paths agree in distribution, not
+bitwise).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+EPI_NONE = 0
+EPI_LRELU_DROPOUT = 1   # out = lrelu(acc + bias, slope) * M, M in {0, 1/(1-p)}; ms = lrelu'(.) * M
+EPI_MASK = 2            # out = acc * ms
+EPI_RELU = 3
+
+
+class TorchOps:
+    name = "torch"
+
+    # ------------------------------------------------------------------ GEMM
+    def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
+             slope=0.2, p_drop=0.5, stream_id=0):
+        """c = epi(alpha * op(a) @ op(b) + beta * c + bias)."""
+        A = a.t() if ta else a
+        B = b.t() if tb else b
+        acc = torch.matmul(A, B)
+        if alpha != 1.0:
+            acc = acc * alpha
+        if beta != 0.0:
+            acc = acc + beta * c
+        if bias is not None:
+            acc = acc + bias
+        if epi == EPI_LRELU_DROPOUT:
+            keep = (torch.rand(acc.shape, device=acc.device) >= p_drop).to(acc.dtype) / (1.0 - p_drop)
+            s = torch.where(acc > 0, torch.ones_like(acc), torch.full_like(acc, slope))
+            ms.copy_(s * keep)
+            acc = acc * ms
+        elif epi == EPI_MASK:
+            acc = acc * ms
+        elif epi == EPI_RELU:
+            acc = torch.relu(acc)
+        c.copy_(acc)
+
+    # ------------------------------------------------------------------ samplers
+    def sample_train(self, t, B, h, c_cols, z_cols, x_fake_c, x_real, col_out, opt_out, stream_id=0):
+        """Draw the training conditional batch, noise, permutation and real rows.
+
+        h[:, z_cols] <- N(0,1); h[:, c_cols] <- c1; x_fake_c <- c1; x_real <- [data[row], c1[perm]].
+        t: dict of device tables (cdf_log, cond_offset, cond_width, row_offset, row_count, rows, data).
+        """
+        dev = h.device
+        n_col = t["cond_width"].numel()
+        h[:, z_cols[0]:z_cols[1]].normal_()
+        c1 = h[:, c_cols[0]:c_cols[1]]
+        c1.zero_()
+        if n_col == 0:
+            if x_real is not None:
+                idx = torch.randint(0, t["data"].shape[0], (B,), device=dev)
+                x_real.copy_(t["data"][idx])
+            return
+        col = torch.randint(0, n_col, (B,), device=dev)
+        u = torch.rand(B, 1, device=dev, dtype=t["cdf_log"].dtype)
+        opt = (t["cdf_log"][col] > u).to(torch.int32).argmax(1)
+        opt = torch.minimum(opt, t["cond_width"][col].long() - 1)
+        c1.scatter_(1, (t["cond_offset"][col].long() + opt).view(-1, 1), 1.0)
+        x_fake_c.copy_(c1)
+        col_out.copy_(col.to(col_out.dtype))
+        opt_out.copy_(opt.to(opt_out.dtype))
+        if x_real is None:
+            return
+        perm = torch.argsort(torch.rand(B, device=dev))
+        cp, op_ = col[perm], opt[perm]
+        cnt = t["row_count"][cp, op_]
+        pick = torch.floor(torch.rand(B, device=dev, dtype=torch.float64) * cnt.clamp_min(1)).long()
+        pick = torch.minimum(pick, (cnt - 1).clamp_min(0))
+        row = t["rows"][t["row_offset"][cp, op_] + pick]
+        dd = t["data"].shape[1]
+        x_real[:, :dd].copy_(t["data"][row])
+        x_real[:, dd:].copy_(c1[perm])
+
+    def sample_gen(self, t, h, c_cols, z_cols, col_out=None, opt_out=None, stream_id=0):
+        """Generation draw (``sample_zero``): noise + c from the empirical option CDF."""
+        dev = h.device
+        B = h.shape[0]
+        h[:, z_cols[0]:z_cols[1]].normal_()
+        c = h[:, c_cols[0]:c_cols[1]]
+        c.zero_()
+        n_col = t["cond_width"].numel()
+        if n_col == 0:
+            return
+        col = torch.randint(0, n_col, (B,), device=dev)
+        u = torch.rand(B, 1, device=dev, dtype=t["cdf_emp"].dtype)
+        opt = (t["cdf_emp"][col] > u).to(torch.int32).argmax(1)
+        opt = torch.minimum(opt, t["cond_width"][col].long() - 1)
+        c.scatter_(1, (t["cond_offset"][col].long() + opt).view(-1, 1), 1.0)
+
+    # ------------------------------------------------------------------ batch norm + relu
+    def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
+                    eps=1e-5):
+        if training:
+            mu = a.mean(0)
+            var = a.var(0, unbiased=False)
+            n = a.shape[0]
+            with torch.no_grad():
+                rmean.mul_(1 - momentum).add_(momentum * mu)
+                rvar.mul_(1 - momentum).add_(momentum * var * n / max(n - 1, 1))
+        else:
+            mu, var = rmean, rvar
+        istd = torch.rsqrt(var + eps)
+        nh = (a - mu) * istd
+        if nhat is not None:
+            nhat.copy_(nh)
+            mean.copy_(mu)
+            invstd.copy_(istd)
+        out.copy_(torch.relu(nh * gamma + beta))
+
+    def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
+                       momentum=0.1, eps=1e-5):
+        """out = relu(BN(x @ W^T + b)); training mode uses batch statistics and updates running ones."""
+        a = torch.addmm(b, x, W.t())
+        self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps)
+
+    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta):
+        dy = dr * (r > 0).to(dr.dtype)
+        dg = (dy * nhat).sum(0)
+        db = dy.sum(0)
+        dgamma.copy_(dg)
+        dbeta.copy_(db)
+        n = dr.shape[0]
+        da.copy_(gamma * invstd * (dy - db / n - nhat * (dg / n)))
+
+    # ------------------------------------------------------------------ activations
+    def activate(self, logits, out, spans, tau=0.2, stream_id=0):
+        """spans: list of (start, width, kind) host tuples (kind 0 tanh, 1 gumbel-softmax)."""
+        for s, w, k in spans:
+            x = logits[:, s:s + w]
+            if k == 0:
+                out[:, s:s + w].copy_(torch.tanh(x))
+            else:
+                u = torch.rand(x.shape, device=x.device, dtype=x.dtype).clamp_(1e-20, 1.0 - 1e-7)
+                g = -torch.log(-torch.log(u))
+                out[:, s:s + w].copy_(torch.softmax((x + g) / tau, dim=1))
+
+    def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
+        """dlogits = d(act)/d(logits)^T dact + d(cond_loss)/d(logits); loss_out[0] <- cond_loss."""
+        for s, w, k in spans:
+            g = dact[:, s:s + w]
+            y = act[:, s:s + w]
+            if k == 0:
+                dlogits[:, s:s + w].copy_(g * (1 - y * y))
+            else:
+                dlogits[:, s:s + w].copy_(y * (g - (g * y).sum(1, keepdim=True)) / tau)
+        B = logits.shape[0]
+        loss = torch.zeros((), device=logits.device, dtype=logits.dtype)
+        colL = col.long()
+        optL = opt.long()
+        for c, (s, w) in enumerate(cond_spans):
+            sel = (colL == c).to(logits.dtype)
+            x = logits[:, s:s + w]
+            tgt = torch.clamp(optL, max=w - 1).view(-1, 1)
+            lse = torch.logsumexp(x, dim=1)
+            loss = loss + (sel * (lse - x.gather(1, tgt).view(-1))).sum()
+            sm = torch.softmax(x, dim=1)
+            sm = sm - torch.zeros_like(sm).scatter_(1, tgt, 1.0)
+            dlogits[:, s:s + w] += sm * (sel / B).view(-1, 1)
+        loss_out[0] = loss / B
+
+    # ------------------------------------------------------------------ gradient penalty pieces
+    def slerp(self, real, fake, out, stream_id=0):
+        alpha = torch.rand(real.shape[0], 1, device=real.device, dtype=real.dtype)
+        rn = real.norm(dim=1, keepdim=True)
+        fn = fake.norm(dim=1, keepdim=True)
+        cos = ((real / rn) * (fake / fn)).sum(1, keepdim=True).clamp(-1.0, 1.0)
+        om = torch.acos(cos)
+        so = torch.sin(om)
+        lin = so < 1e-6
+        wr = torch.where(lin, 1 - alpha, torch.sin((1 - alpha) * om) / torch.where(lin, torch.ones_like(so), so))
+        wf = torch.where(lin, alpha, torch.sin(alpha * om) / torch.where(lin, torch.ones_like(so), so))
+        out.copy_(wr * real + wf * fake)
+
+    def gp_scale(self, g, out, lam, loss_out):
+        n = g.norm(dim=1, keepdim=True)
+        P = g.shape[0]
+        loss_out[0] = lam * ((n - 1) ** 2).mean()
+        out.copy_(g * (lam * 2.0 * (n - 1) / (n.clamp_min(1e-30) * P)))
+
+    # ------------------------------------------------------------------ discriminator head
+    def d_head(self, d_last, ms_last, v, e, coef, wloss, y, a_last, loss_out):
+        """y = d_last @ v + e;  a_last = coef[:,None] * v[None,:] * ms_last;  loss_out[0] = sum(wloss * y)."""
+        y.copy_(d_last @ v + e)
+        a_last.copy_(coef.view(-1, 1) * v.view(1, -1) * ms_last)
+        loss_out[0] = (wloss * y).sum()
+
+    def colsum(self, a, out, beta=0.0):
+        if beta == 0.0:
+            out.copy_(a.sum(0))
+        else:
+            out.mul_(beta).add_(a.sum(0))
+
+    # ------------------------------------------------------------------ optimizer
+    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd):
+        """torch.optim.Adam (L2 weight decay added to the gradient, not AdamW); step is a device counter."""
+        step.add_(1)
+        if wd != 0.0:
+            g = g + wd * p
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        t = step.to(torch.float64)
+        bc1 = 1 - torch.pow(torch.full_like(t, b1), t)
+        bc2 = 1 - torch.pow(torch.full_like(t, b2), t)
+        denom = (v.sqrt() / torch.sqrt(bc2).to(v.dtype)).add_(eps)
+        p.sub_((lr / bc1).to(p.dtype) * (m / denom))
+
+    # ------------------------------------------------------------------ generation decode
+    def sample_decode(self, logits, out, tabs, stream_id=0):
+        """Fused activate + VGM/categorical decode of generated rows.
+
+        out: [N, n_cols] float64 (continuous columns: value; categorical: label code).
+        tabs: dict with host lists 'cols' of (kind, data_start, width, j_cont, i2s_codes).
+        """
+        N = logits.shape[0]
+        for j, (kind, s, w, c, codes) in enumerate(tabs["cols"]):
+            if kind == 0:  # continuous: alpha = tanh(logit); mode = argmax(logits + gumbel)
+                alpha = torch.tanh(logits[:, s]).clamp(-1, 1)
+                x = logits[:, s + 1:s + 1 + w]
+                u = torch.rand(x.shape, device=x.device, dtype=x.dtype).clamp_(1e-20, 1.0 - 1e-7)
+                k = (x - torch.log(-torch.log(u))).argmax(1)
+                mu = tabs["mu"][c][k]
+                sd = tabs["sd"][c][k]
+                out[:, j] = (alpha.double() * 4 * sd + mu)
+            else:
+                x = logits[:, s:s + w]
+                u = torch.rand(x.shape, device=x.device, dtype=x.dtype).clamp_(1e-20, 1.0 - 1e-7)
+                k = (x - torch.log(-torch.log(u))).argmax(1)
+                out[:, j] = codes[k].double()
+        return out
