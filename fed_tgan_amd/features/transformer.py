@@ -111,7 +111,10 @@ def metadata_from_data(data: np.ndarray, categorical_columns=(), ordinal_columns
 def metadata_from_global(data: np.ndarray, global_meta: dict, vocabs, categorical_columns=(), ordinal_columns=()):
     """``Transformer.get_metadata_refit`` (`transformers.py:41-71`): i2s = global codes by frequency."""
     meta = []
-    df = pd.DataFrame(data)
+    if data is None:   # a dataless federator: only the schema is known
+        df = pd.DataFrame(np.zeros((0, len(global_meta["columns"]))))
+    else:
+        df = pd.DataFrame(data)
     cursor = 0
     for j in df.columns:
         col = df[j]
@@ -125,7 +128,8 @@ def metadata_from_global(data: np.ndarray, global_meta: dict, vocabs, categorica
             vals = [k for k, _ in vc]
             meta.append({"name": j, "type": ORDINAL, "size": len(vals), "i2s": vals})
         else:
-            meta.append({"name": j, "type": CONTINUOUS, "min": col.min(), "max": col.max()})
+            meta.append({"name": j, "type": CONTINUOUS, "min": col.min() if len(col) else None,
+                         "max": col.max() if len(col) else None})
     return meta
 
 

@@ -1,0 +1,340 @@
+"""The federated runtime: initialisation protocol, training rounds, aggregation, sampling.
+
+Roles (one process per rank):
+
+* **client** — owns a local table shard and a :class:`CTGANEngine` on its GPU
+  (``cuda:LOCAL_RANK``) or the CPU; trains one local epoch per round
+  (`Client/.../dtds/distributed.py:179-269`).
+* **federator** — rank 0.  In *dedicated* mode (the reference topology, ``world_size = K+1``,
+  `R/README.md:7-25`) it holds no data, like ``MDGANServer`` (`Server/dtds/distributed.py:543-835`).
+  In *co-located* mode (one process per GPU, every rank a client — the MI355X layout) rank 0
+  is a client *and* the federator.
+
+Initialisation (`Server/dtds/distributed.py:865-873`), now as collectives:
+    A. meta all-gather -> vocabulary merge + JSD client distances (federator) -> broadcast
+    B. local VGM fits -> all-gather of GMM parameters -> pooled resampling, W1 distances and
+       global VGM fit (federator) -> broadcast
+    C. every rank refits its transformer with the global GMMs and encodes its rows
+    D. aggregation weights (federator) -> broadcast
+    E. global span counts (all-reduce) -> the generation-time conditional sampler.  The
+       reference reads the raw training table at the server for this (`:565-580`); here no
+       raw row ever leaves a client.
+    F. initial weights broadcast from the first client.
+
+Each round (`Server/dtds/distributed.py:794-825`): local epoch on every client; ONE
+weighted all-reduce of the flat parameter buffer (every client now holds the aggregate,
+so there is no push-back); sampling of ``n_sample`` rows (sharded over the client GPUs in
+co-located mode) with eval-mode BN; decode; CSV dump; per-round wall time.  After the
+last round ``timestamp_experiment.csv`` is written (`:827-829`).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+import pickle
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..data.constants import CATEGORICAL
+from ..data.decode import csv_columns, decode_frame, meta_column_names
+from ..data.schema import DatasetSpec
+from ..data.synthetic import generate, shard
+from ..data.table import TablePreprocessor, dump_meta_json, load_table
+from ..data.vocab import CategoryVocab
+from ..features.gmm import VGMBank, fit_vgm
+from ..features.transformer import VGMTransformer
+from ..models.engine import CTGANEngine, EngineConfig
+from ..models.samplers import CondTables
+from ..parallel.comm import Comm
+from ..utils.metrics import MetricsLog, PhaseTimer
+from .stats import (aggregation_weights, continuous_client_distances, merge_categorical_metas,
+                    normalise_over_clients, uniform_weights, wasserstein_1d)
+
+
+@dataclasses.dataclass
+class FedConfig:
+    spec: DatasetSpec
+    epochs: int = 10
+    datapath: Optional[str] = None          # CSV per client ('{client}' / '{rank}' are substituted)
+    synthetic_rows: int = 40000             # rows per client when no CSV is given
+    shard_mode: str = "independent"         # independent | iid | dirichlet | skew
+    dirichlet_alpha: float = 0.5
+    out_dir: str = "."
+    n_sample: Optional[int] = None          # rows per epoch CSV (default spec.n_sample)
+    aggregation: str = "weighted"           # weighted | uniform
+    gmm_backend: str = "torch"              # torch | sklearn
+    gmm_pool_cap: int = 0                   # cap on pooled GMM re-fit sample size (0 = reference: N)
+    backend: str = "auto"                   # engine ops: auto | hip | torch
+    write_csv: bool = True
+    csv_writer: str = "auto"                # auto | native | pandas
+    seed: int = 0
+    engine: EngineConfig = dataclasses.field(default_factory=EngineConfig)
+    ckpt_every: int = 0
+    resume: bool = False
+    use_graph: Optional[bool] = None
+    verbose: bool = True
+    metrics_log: Optional[str] = None
+
+
+def _log(cfg: FedConfig, rank: int, *msg):
+    if cfg.verbose and rank == 0:
+        print(*msg, flush=True)
+
+
+class FedRuntime:
+    def __init__(self, cfg: FedConfig, comm: Comm, device: torch.device, federator: int = 0):
+        self.cfg = cfg
+        self.comm = comm
+        self.device = device
+        self.federator = federator
+        self.rank = comm.rank
+        self.is_fed = self.rank == federator
+        self.is_client = comm.is_client
+        self.name = cfg.spec.name
+        self.n_sample = cfg.n_sample or cfg.spec.n_sample
+        self.timer = PhaseTimer()
+        self.round_times: List[float] = []
+        self.start_epoch = 0
+        self.metrics = MetricsLog(cfg.metrics_log) if (cfg.metrics_log and self.is_fed) else None
+        self.dump_csv = None
+
+    # ================================================================= data
+    def _local_frame(self) -> pd.DataFrame:
+        cfg, c = self.cfg, self.comm
+        k, idx = c.n_clients, c.client_index
+        if cfg.datapath and os.path.exists(cfg.datapath.format(client=idx, rank=self.rank)):
+            return pd.read_csv(cfg.datapath.format(client=idx, rank=self.rank))
+        if cfg.shard_mode == "independent":
+            return generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx)
+        full = generate(cfg.spec, cfg.synthetic_rows * k, seed=cfg.seed)
+        parts = shard(full, k, cfg.shard_mode, seed=cfg.seed, target=cfg.spec.target_column,
+                      alpha=cfg.dirichlet_alpha)
+        return parts[idx]
+
+    # ================================================================= init protocol
+    def initialize(self):
+        cfg, c = self.cfg, self.comm
+        spec = cfg.spec
+        t0 = time.time()
+        # ---- A. categorical meta
+        self.table = None
+        if self.is_client:
+            df = self._local_frame()
+            self.table = TablePreprocessor(df[spec.selected_variables], f"{self.name}_train", spec.problem_type,
+                                           "" if spec.target_column == "none" else spec.target_column,
+                                           spec.categorical_list, spec.nonnegative_list, spec.date_dic)
+        metas = c.all_gather_object(self.table.local_meta() if self.is_client else None)
+        client_metas = [metas[r] for r in c.client_ranks]
+        payload = None
+        if self.is_fed:
+            merged, vocabs, d_hat = merge_categorical_metas(client_metas)
+            payload = (merged, [(v.column_name, v.tolist()) for v in vocabs], d_hat)
+        merged, vocab_lists, d_hat = c.broadcast_object(payload, src=self.federator)
+        self.global_meta = merged
+        self.vocabs = [CategoryVocab(lst, name) for name, lst in vocab_lists]
+        self.d_hat = np.asarray(d_hat)
+        cat_idx = [j for j, col in enumerate(merged["columns"]) if col["type"] == CATEGORICAL]
+        self.cat_idx = cat_idx
+        if self.is_fed:
+            self._write_meta_artifacts()
+        _log(cfg, self.rank, f"[init] categorical merge done ({time.time() - t0:.2f}s)")
+        # ---- B. local VGMs -> global VGM
+        info = None
+        self.encoded = None
+        if self.is_client:
+            self.encoded = self.table.encode(self.vocabs)
+            local = VGMTransformer().fit(self.encoded, cat_idx, (), backend=cfg.gmm_backend,
+                                         seed=cfg.seed + 7 * c.client_index, device=self.device)
+            info = (local.bank.to_dict(), len(self.encoded))
+        infos = c.all_gather_object(info)
+        client_infos = [infos[r] for r in c.client_ranks]
+        self.rows = [n for _, n in client_infos]
+        payload = None
+        if self.is_fed:
+            payload = self._global_gmm([VGMBank.from_dict(b) for b, _ in client_infos], self.rows)
+        gbank, comps, e_hat = c.broadcast_object(payload, src=self.federator)
+        self.bank = VGMBank.from_dict(gbank)
+        self.components = np.asarray(comps, dtype=bool)
+        self.e_hat = np.asarray(e_hat)
+        _log(cfg, self.rank, f"[init] global VGM fitted ({time.time() - t0:.2f}s)")
+        # ---- C. refit + encode
+        self.transformer = VGMTransformer().refit(self.encoded, merged, self.vocabs, cat_idx, (), self.bank,
+                                                  self.components)
+        lay = self.transformer.layout
+        if self.is_client:
+            self.train_matrix = self.transformer.transform(self.encoded, np.random.default_rng(cfg.seed + self.rank))
+        # ---- D. weights
+        if cfg.aggregation == "uniform":
+            self.weights = uniform_weights(c.n_clients)
+        else:
+            self.weights = aggregation_weights(self.d_hat, self.e_hat, self.rows)
+        _log(cfg, self.rank, f"final aggregation weights {self.weights}")
+        # ---- E. global span counts for generation
+        maxw = int(lay.cond_width.max()) if lay.n_col else 0
+        cnt = torch.zeros(lay.n_col, maxw, dtype=torch.float64)
+        if self.is_client:
+            cnt += torch.as_tensor(CondTables.span_counts(self.train_matrix, lay))
+        c.all_reduce_cpu(cnt)
+        self.gen_cond = CondTables(lay, cnt.numpy())
+        # ---- engine + F. initial weights
+        torch.manual_seed(cfg.seed + self.rank)
+        self.engine = CTGANEngine(lay, cfg.engine, self.device, backend=cfg.backend, seed=cfg.seed * 7919 + self.rank)
+        if self.is_client:
+            self.engine.set_training_data(self.train_matrix)
+        self.engine.set_generation_tables(self.gen_cond, self.transformer)
+        first = c.client_ranks[0]
+        if c.world_size > 1:
+            host = self.engine.flat.detach().cpu()
+            torch.distributed.broadcast(host, src=first, group=c.ctrl)
+            self.engine.flat.copy_(host)
+        self.steps = [n // cfg.engine.batch_size for n in self.rows]
+        if cfg.resume:
+            self.load_checkpoint()
+        self.csv_cols = csv_columns(merged, self.vocabs) if not spec.date_dic else None
+        _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
+                             f"steps/epoch={self.steps}")
+
+    def _global_gmm(self, banks: List[VGMBank], rows: List[int]):
+        cfg = self.cfg
+        rng = np.random.default_rng(cfg.seed + 12345)
+        n_total = int(np.sum(rows))
+        if cfg.gmm_pool_cap and n_total > cfg.gmm_pool_cap:
+            n_total = cfg.gmm_pool_cap
+        share = [float(r) / float(np.sum(rows)) for r in rows]
+        n_cont = banks[0].n
+        pooled, per_client = [], [[] for _ in banks]
+        for j in range(n_cont):
+            parts = [b.sample_column(j, int(n_total * share[i]), rng) for i, b in enumerate(banks)]
+            for i, p in enumerate(parts):
+                per_client[i].append(p)
+            pooled.append(np.concatenate(parts))
+        e_hat = continuous_client_distances(pooled, per_client) if n_cont else np.zeros((len(banks), 0))
+        gb = fit_vgm(pooled, backend=cfg.gmm_backend, seed=cfg.seed, device=self.device)
+        comps = gb.components()
+        return gb.to_dict(), comps.tolist(), e_hat
+
+    def _write_meta_artifacts(self):
+        mdir = os.path.join(self.cfg.out_dir, "models")
+        os.makedirs(mdir, exist_ok=True)
+        dump_meta_json(self.global_meta, os.path.join(mdir, f"{self.name}.json"))
+        les = [{"column_name": v.column_name, "label_encoder": v.to_sklearn()} for v in self.vocabs]
+        with open(os.path.join(mdir, f"label_encoders_{self.name}.pickle"), "wb") as f:
+            pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
+
+    # ================================================================= rounds
+    def aggregate(self):
+        c = self.comm
+        w = float(self.weights[c.client_index]) if self.is_client else 0.0
+        c.weighted_all_reduce(self.engine.flat, w)
+        c.share_with_federator(self.engine.flat, self.federator)
+        # num_batches_tracked: weighted average of every client's counter, truncated (reference cast)
+        ep = self.engine
+        counts = np.asarray([2 * s for s in self.steps], dtype=np.float64) * (self._epoch_done)
+        ep.bn_batches = int(np.sum(self.weights * counts))
+
+    def sample_round(self, epoch: int):
+        """Generate n_sample rows, decode, and (federator) write the epoch CSV."""
+        c = self.comm
+        colocated = self.federator in c.client_ranks
+        samplers = c.client_ranks if colocated else [self.federator]
+        share = None
+        if self.rank in samplers:
+            k = samplers.index(self.rank)
+            per = [self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0)
+                   for i in range(len(samplers))]
+            vals = self.engine.generate_decoded(per[k]).cpu().numpy()
+            share = vals
+        if len(samplers) > 1:
+            parts = c.gather_bytes(share, dst=self.federator)
+            if self.is_fed:
+                share = np.concatenate([parts[r] for r in samplers], axis=0)
+        if self.is_fed and self.cfg.write_csv:
+            self.write_epoch_csv(share, epoch)
+        return share if self.is_fed else None
+
+    def result_dir(self) -> str:
+        d = os.path.join(self.cfg.out_dir, f"{self.name}_result")
+        os.makedirs(d, exist_ok=True)
+        return d
+
+    def write_epoch_csv(self, values: np.ndarray, epoch: int):
+        path = os.path.join(self.result_dir(), f"{self.name}_synthesis_epoch_{epoch}.csv")
+        use_native = self.cfg.csv_writer in ("auto", "native") and self.csv_cols is not None
+        if use_native:
+            from ..utils import csvio
+            if csvio.available() or self.cfg.csv_writer == "native":
+                names, kinds, vocab_lists = self.csv_cols
+                csvio.write_table(path, values, names, kinds, vocab_lists)
+                return path
+        decode_frame(values, self.global_meta, self.vocabs).to_csv(path, index=False)
+        return path
+
+    def run_round(self, epoch: int) -> float:
+        c = self.comm
+        t0 = time.time()
+        with self.timer.phase("train", self.device):
+            if self.is_client:
+                self.engine.train_epoch(self.cfg.use_graph)
+        self._epoch_done = epoch + 1
+        with self.timer.phase("aggregate", self.device):
+            self.aggregate()
+        with self.timer.phase("sample_dump", self.device):
+            self.sample_round(epoch)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.time() - t0
+        return dt
+
+    def fit(self):
+        cfg = self.cfg
+        for ep in range(self.start_epoch, cfg.epochs):
+            dt = self.run_round(ep)
+            self.round_times.append(dt)
+            if self.is_fed:
+                ld, lg = self.engine.losses() if self.is_client else (float("nan"), float("nan"))
+                _log(cfg, self.rank, f"EPOCH {ep}: loss_d:{ld:>6.2f}   loss_g:{lg:>6.2f}   round time: {dt:.3f} sec")
+                if self.metrics is not None:
+                    self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,
+                                        **self.timer.last()})
+            if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
+                self.save_checkpoint(ep + 1)
+        if self.is_fed:
+            self.write_timestamps()
+
+    def write_timestamps(self):
+        path = os.path.join(self.cfg.out_dir, "timestamp_experiment.csv")
+        with open(path, "w") as f:
+            for t in self.round_times:
+                f.write(f"{t}\r\n")
+        return path
+
+    # ================================================================= checkpoint / resume
+    def _ckpt_path(self) -> str:
+        d = os.path.join(self.cfg.out_dir, "ckpt")
+        os.makedirs(d, exist_ok=True)
+        return os.path.join(d, f"rank{self.rank}.pt")
+
+    def save_checkpoint(self, epoch: int):
+        e = self.engine
+        state = {"epoch": epoch, "flat": e.flat.cpu(), "mG": e.mG.cpu(), "vG": e.vG.cpu(), "mD": e.mD.cpu(),
+                 "vD": e.vD.cpu(), "stepG": e.stepG.cpu(), "stepD": e.stepD.cpu(), "bn_batches": e.bn_batches,
+                 "round_times": list(self.round_times)}
+        torch.save(state, self._ckpt_path())
+
+    def load_checkpoint(self):
+        p = self._ckpt_path()
+        if not os.path.exists(p):
+            return
+        st = torch.load(p, weights_only=True)
+        e = self.engine
+        for k in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
+            getattr(e, k).copy_(st[k])
+        e.bn_batches = int(st["bn_batches"])
+        self.start_epoch = int(st["epoch"])
+        self.round_times = list(st["round_times"])
+        self._epoch_done = self.start_epoch

@@ -1,0 +1,64 @@
+"""Loader for the in-tree native library ``fed_tgan_amd/_C.so`` (HIP kernels + host C++).
+
+Built by ``csrc/build.py`` (hipcc, ``--offload-arch=gfx950``) and registered as the
+``torch.ops.fedtgan`` namespace.  On a GPU box the HIP backend refuses to fall back to
+eager PyTorch: :func:`require` raises if the library is missing or fails to load.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Sequence
+
+import numpy as np
+import torch
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "_C.so")
+
+_lock = threading.Lock()
+_loaded = None
+_error = None
+
+
+def _load():
+    global _loaded, _error
+    with _lock:
+        if _loaded is not None or _error is not None:
+            return
+        if not os.path.exists(LIB_PATH):
+            _error = f"native library not built: {LIB_PATH} (run `python csrc/build.py`)"
+            return
+        try:
+            torch.ops.load_library(LIB_PATH)
+            _loaded = torch.ops.fedtgan
+        except Exception as e:  # pragma: no cover - surfaced by require()
+            _error = f"failed to load {LIB_PATH}: {e}"
+
+
+def available() -> bool:
+    _load()
+    return _loaded is not None
+
+
+def lib():
+    _load()
+    return _loaded
+
+
+def require():
+    _load()
+    if _loaded is None:
+        raise RuntimeError(_error or "native library unavailable")
+    return _loaded
+
+
+def write_csv(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
+              vocabs: Sequence[Sequence[str]], threads: int = 0) -> None:
+    L = require()
+    flat, offs = [], [0]
+    for v in vocabs:
+        flat.extend(v)
+        offs.append(len(flat))
+    t = torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64))
+    L.write_csv(path, t, list(names), [int(k) for k in kinds], flat, offs, int(threads))

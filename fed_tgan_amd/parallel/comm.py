@@ -1,0 +1,168 @@
+"""Process groups for the federation: a gloo control plane and an RCCL data plane.
+
+The reference moves everything — meta dicts, sklearn objects, whole ``nn.Module``s and
+8.5 MB of state_dicts per client per round — as pickled PyTorch-RPC messages over the
+Gloo/TCP ``PROCESS_GROUP`` agent (`Server/dtds/distributed.py:838-891`, survey §2-E
+M1-M12), serialising the push-back client by client (`:821-823`).
+
+Here the same exchanges are collectives:
+
+* control plane (all ranks, gloo over TCP, keeps the reference ``-ip/-port/-rank/
+  -world_size`` rendezvous): ``all_gather_object`` / ``broadcast_object`` of metadata and
+  GMM parameters (M2-M5), barriers with timeouts (failure detection);
+* data plane (client ranks, ``nccl`` = RCCL over xGMI when every client owns a GPU,
+  otherwise gloo): the per-round aggregation is ONE ``all_reduce(SUM)`` of the flat,
+  pre-scaled ``w_i * [theta_G | theta_D | BN stats]`` buffer — which replaces the
+  reference's gather (M9) + weighted average + serial broadcast (M10).  Every client then
+  holds the aggregate, so there is no push-back step at all.
+
+``Comm`` also works without ``torch.distributed`` (world size 1) so the single-client
+path and the CLI need no rendezvous.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Any, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    def __init__(self, rank: int = 0, world_size: int = 1, client_ranks: Sequence[int] = (0,),
+                 data_backend: str = "gloo", ip: str = "127.0.0.1", port: int = 7788, timeout_s: float = 600.0,
+                 device: torch.device | None = None, init: bool = True):
+        self.rank = rank
+        self.world_size = world_size
+        self.client_ranks = list(client_ranks)
+        self.data_backend = data_backend
+        self.device = device or torch.device("cpu")
+        self.timeout = datetime.timedelta(seconds=timeout_s)
+        self.ctrl = None
+        self.data = None
+        self.initialized = False
+        if world_size > 1 and init:
+            self._init(ip, port)
+
+    def _init(self, ip: str, port: int):
+        os.environ.setdefault("MASTER_ADDR", ip)
+        os.environ.setdefault("MASTER_PORT", str(port))
+        if not dist.is_initialized():
+            dist.init_process_group("gloo", init_method=f"tcp://{ip}:{port}", rank=self.rank,
+                                    world_size=self.world_size, timeout=self.timeout)
+        self.initialized = True
+        self.ctrl = dist.group.WORLD
+        if self.data_backend == "nccl":
+            # every rank must call new_group, members or not
+            self.data = dist.new_group(ranks=self.client_ranks, backend="nccl", timeout=self.timeout)
+        else:
+            # gloo data plane: reduce over every rank; a dedicated federator contributes zeros
+            self.data = self.ctrl
+
+    @classmethod
+    def from_env(cls, data_backend: str = "auto", device: torch.device | None = None) -> "Comm":
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        ip = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500"))
+        if data_backend == "auto":
+            data_backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
+        return cls(rank, ws, list(range(ws)), data_backend, ip, port, device=device)
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def is_client(self) -> bool:
+        return self.rank in self.client_ranks
+
+    @property
+    def n_clients(self) -> int:
+        return len(self.client_ranks)
+
+    @property
+    def client_index(self) -> int:
+        return self.client_ranks.index(self.rank) if self.is_client else -1
+
+    # ------------------------------------------------------------------ control plane
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        if self.world_size == 1:
+            return [obj]
+        out: List[Any] = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.ctrl)
+        return out
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if self.world_size == 1:
+            return obj
+        box = [obj if self.rank == src else None]
+        dist.broadcast_object_list(box, src=src, group=self.ctrl)
+        return box[0]
+
+    def barrier(self):
+        if self.world_size > 1:
+            dist.barrier(group=self.ctrl)
+
+    def all_reduce_cpu(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        if self.world_size > 1:
+            dist.all_reduce(t, op=op, group=self.ctrl)
+        return t
+
+    def max_float(self, x: float) -> float:
+        if self.world_size == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
+        return float(t.item())
+
+    def gather_bytes(self, payload: bytes, dst: int = 0) -> Optional[List[bytes]]:
+        if self.world_size == 1:
+            return [payload]
+        out = [None] * self.world_size if self.rank == dst else None
+        dist.gather_object(payload, out, dst=dst, group=self.ctrl)
+        return out
+
+    # ------------------------------------------------------------------ data plane
+    def weighted_all_reduce(self, flat: torch.Tensor, weight: float) -> torch.Tensor:
+        """flat <- sum_i w_i * flat_i over the data group (in place).
+
+        Non-client ranks (a dedicated federator) contribute zeros and receive the sum too
+        when the data plane spans every rank (gloo).
+        """
+        if self.world_size == 1:
+            if weight != 1.0:
+                flat.mul_(weight)
+            return flat
+        if self.data_backend == "nccl":
+            if self.is_client:
+                flat.mul_(weight)
+                dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.data)
+            return flat
+        # gloo: reduce on host memory
+        host = flat.detach().to("cpu", copy=True) if flat.device.type != "cpu" else flat
+        if self.is_client:
+            host.mul_(weight)
+        else:
+            host.zero_()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.data)
+        if host is not flat:
+            flat.copy_(host)
+        return flat
+
+    def share_with_federator(self, flat: torch.Tensor, federator: int = 0) -> torch.Tensor:
+        """After an RCCL reduce among clients, hand the aggregate to a dataless federator rank."""
+        if self.world_size == 1 or self.data_backend != "nccl" or federator in self.client_ranks:
+            return flat
+        src = self.client_ranks[0]
+        host = flat.detach().to("cpu", copy=True)
+        if self.rank in (src, federator):
+            if self.rank == src:
+                dist.send(host, dst=federator, group=self.ctrl)
+            else:
+                dist.recv(host, src=src, group=self.ctrl)
+                flat.copy_(host)
+        return flat
+
+    def destroy(self):
+        if self.initialized and dist.is_initialized():
+            dist.destroy_process_group()
+            self.initialized = False

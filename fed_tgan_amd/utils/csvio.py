@@ -1,0 +1,72 @@
+"""Synthetic-table CSV writer.
+
+The reference writes every epoch's 40,000-row table with ``DataFrame.to_csv`` after a
+pandas ``Transform.inverse`` pass (`Server/dtds/distributed.py:584-590`), ~1.1 s per epoch on
+the survey box.  The native path formats the numeric decode output directly in C++
+(``csrc/host/csv_writer.cpp``: Python-``repr``-compatible shortest round-trip floats, vocab
+lookups for categoricals, the non-negative ``exp(x)-1`` / ceil rule, multi-threaded over
+row blocks) and writes the file in one call.  Byte-for-byte the output equals the pandas
+path for tables without date columns (tested).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+
+from ..data.decode import KIND_FLOAT, KIND_NONNEG, KIND_VOCAB
+
+
+def _native():
+    from ..ops import native
+    return native.lib() if native.available() else None
+
+
+def available() -> bool:
+    try:
+        return _native() is not None
+    except Exception:
+        return False
+
+
+def _py_float(x: float) -> str:
+    return repr(float(x))
+
+
+def format_table_py(values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
+                    vocabs: Sequence[Sequence[str]]) -> bytes:
+    out = [",".join(names)]
+    cols = []
+    for j, k in enumerate(kinds):
+        v = values[:, j]
+        if k == KIND_FLOAT:
+            cols.append([_py_float(x) for x in v])
+        elif k == KIND_VOCAB:
+            voc = vocabs[j]
+            cols.append([voc[int(x)] for x in v])
+        else:
+            w = np.exp(v) - 1.0
+            neg = w < 0
+            w[neg] = np.ceil(w[neg])
+            cols.append([" " if x == -1.0 else _py_float(x) for x in w])
+    for row in zip(*cols):
+        out.append(",".join(_quote(s) for s in row))
+    return ("\n".join(out) + "\n").encode()
+
+
+def _quote(s: str) -> str:
+    if any(ch in s for ch in ',"\n\r'):
+        return '"' + s.replace('"', '""') + '"'
+    return s
+
+
+def write_table(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
+                vocabs: Sequence[Sequence[str]], threads: int = 0) -> None:
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    lib = _native()
+    if lib is not None:
+        from ..ops import native
+        native.write_csv(path, values, names, kinds, vocabs, threads)
+        return
+    with open(path, "wb") as f:
+        f.write(format_table_py(values, names, kinds, vocabs))
