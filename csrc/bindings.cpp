@@ -1,0 +1,368 @@
+// torch.ops.fedtgan.* — PyTorch bindings of the gfx950 kernels and the native host code.
+// Every op validates shapes/strides on the host before launching (a wrong shape must never
+// reach a kernel) and launches on the current HIP stream so hipGraph capture works.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <string>
+#include <vector>
+
+#include "host/csv_writer.h"
+#include "kernels/launch.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32_2d(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.size(1) <= 1 || t.stride(1) == 1, name, " must have unit column stride");
+}
+
+int ld_of(const Tensor& t) { return (int)(t.size(0) <= 1 ? std::max<int64_t>(t.size(1), 1) : t.stride(0)); }
+
+float* fp(const Tensor& t) { return t.data_ptr<float>(); }
+const float* cfp(const Tensor& t) { return t.data_ptr<float>(); }
+template <typename T>
+T* optp(const optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<T>() : nullptr;
+}
+const uint64_t* ctr_ptr(const optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() >= 1 && t->is_cuda(), "rng_ctr must be a cuda int64 tensor");
+  return reinterpret_cast<const uint64_t*>(t->data_ptr<int64_t>());
+}
+
+void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
+          const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
+          const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
+          const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
+          const optional<Tensor>& bn_rv, double bn_eps) {
+  check_f32_2d(a, "a");
+  check_f32_2d(b, "b");
+  check_f32_2d(c, "c");
+  const int64_t M = ta ? a.size(1) : a.size(0);
+  const int64_t K = ta ? a.size(0) : a.size(1);
+  const int64_t Kb = tb ? b.size(1) : b.size(0);
+  const int64_t N = tb ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: inner dims differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: c is ", c.sizes(), " expected [", M, ", ", N, "]");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm: bias");
+  fedtgan::GemmArgs g{};
+  g.a = cfp(a);
+  g.b = cfp(b);
+  g.c = fp(c);
+  g.bias = optp<float>(bias);
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.lda = ld_of(a); g.ldb = ld_of(b); g.ldc = ld_of(c);
+  g.ta = ta; g.tb = tb;
+  g.alpha = (float)alpha; g.beta = (float)beta;
+  g.epi = (int)epi;
+  g.slope = (float)slope; g.p_drop = (float)p_drop;
+  if (epi == fedtgan::EPI_MASK || epi == fedtgan::EPI_LRELU_DROPOUT) {
+    TORCH_CHECK(ms.has_value() && ms->defined(), "gemm: epilogue needs ms");
+    check_f32_2d(*ms, "ms");
+    TORCH_CHECK(ms->size(0) == M && ms->size(1) == N, "gemm: ms shape");
+    g.ms = fp(*ms);
+    g.ldms = ld_of(*ms);
+  }
+  if (epi == fedtgan::EPI_BN_EVAL_RELU) {
+    TORCH_CHECK(bn_gamma.has_value() && bn_beta.has_value() && bn_rm.has_value() && bn_rv.has_value(), "gemm: bn");
+    g.bn_gamma = optp<float>(bn_gamma); g.bn_beta = optp<float>(bn_beta);
+    g.bn_rm = optp<float>(bn_rm); g.bn_rv = optp<float>(bn_rv);
+    g.bn_eps = (float)bn_eps;
+  }
+  g.splitk = (int)std::max<int64_t>(splitk, 1);
+  if (g.splitk > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined() && ws->scalar_type() == at::kFloat, "gemm: split-K needs ws");
+    int64_t kchunk = ((K + g.splitk - 1) / g.splitk + 31) / 32 * 32;
+    int64_t s_eff = (K + kchunk - 1) / kchunk;
+    TORCH_CHECK(ws->numel() >= s_eff * M * N, "gemm: workspace too small");
+    g.ws = fp(*ws);
+  }
+  g.seed = (uint64_t)seed;
+  g.rng_ctr = ctr_ptr(rng_ctr);
+  g.rng_stream = (uint32_t)stream;
+  fedtgan::launch_gemm(g, cur_stream());
+}
+
+void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<Tensor>& xf, const optional<Tensor>& xr,
+            int64_t Dd, const Tensor& cdf, const Tensor& cond_off, const Tensor& cond_w, const optional<Tensor>& row_off,
+            const optional<Tensor>& row_cnt, const optional<Tensor>& rows, const optional<Tensor>& data,
+            const optional<Tensor>& col, const optional<Tensor>& opt, const optional<Tensor>& step_bump,
+            const optional<Tensor>& metrics, bool zero_metrics, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+  check_f32_2d(h, "h");
+  fedtgan::SampleArgs a{};
+  a.B = (int)h.size(0);
+  a.E = (int)E;
+  a.C = (int)(h.size(1) - cc);
+  a.Dd = (int)Dd;
+  a.n_col = (int)cond_w.numel();
+  a.maxw = cdf.dim() == 2 ? (int)cdf.size(1) : 0;
+  TORCH_CHECK(zc + E <= h.size(1) && cc <= h.size(1), "sample: column ranges");
+  TORCH_CHECK(cond_off.scalar_type() == at::kInt && cond_w.scalar_type() == at::kInt, "sample: int32 tables");
+  TORCH_CHECK(cdf.is_contiguous() && cdf.scalar_type() == at::kFloat, "sample: cdf");
+  a.h = fp(h); a.ldh = ld_of(h); a.zc = (int)zc; a.cc = (int)cc;
+  a.ldx = 0;
+  if (xf.has_value() && xf->defined()) {
+    check_f32_2d(*xf, "xf");
+    TORCH_CHECK(xf->size(0) == a.B && xf->size(1) == Dd + a.C, "sample: xf shape");
+    a.xf = fp(*xf); a.ldx = ld_of(*xf);
+  }
+  if (xr.has_value() && xr->defined()) {
+    check_f32_2d(*xr, "xr");
+    TORCH_CHECK(xr->size(0) == a.B && xr->size(1) == Dd + a.C, "sample: xr shape");
+    TORCH_CHECK(a.B <= 4096, "sample: batch > 4096 not supported by the in-LDS permutation");
+    TORCH_CHECK(row_off.has_value() && row_cnt.has_value() && rows.has_value() && data.has_value(), "sample: tables");
+    TORCH_CHECK(data->size(1) == Dd && data->is_contiguous(), "sample: data");
+    a.xr = fp(*xr);
+    if (a.ldx == 0) a.ldx = ld_of(*xr);
+    TORCH_CHECK(ld_of(*xr) == a.ldx, "sample: xf/xr strides differ");
+    a.row_off = optp<int64_t>(row_off); a.row_cnt = optp<int64_t>(row_cnt); a.rows = optp<int64_t>(rows);
+    a.data = data->data_ptr<float>();
+    a.n_rows = (int)data->size(0);
+  }
+  a.cdf = cfp(cdf);
+  a.cond_off = cond_off.data_ptr<int>();
+  a.cond_w = cond_w.data_ptr<int>();
+  a.col = optp<int>(col);
+  a.opt = optp<int>(opt);
+  a.step_bump = optp<float>(step_bump);
+  a.metrics = optp<float>(metrics);
+  a.zero_metrics = zero_metrics ? 1 : 0;
+  a.seed = (uint64_t)seed;
+  a.rng_ctr = ctr_ptr(rng_ctr);
+  a.rng_stream = (uint32_t)stream;
+  fedtgan::launch_sample(a, cur_stream());
+}
+
+fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Tensor& kind, const Tensor& cidx) {
+  TORCH_CHECK(start.scalar_type() == at::kInt && width.scalar_type() == at::kInt && kind.scalar_type() == at::kInt &&
+                  cidx.scalar_type() == at::kInt,
+              "span tables must be int32");
+  return fedtgan::SpanTables{start.data_ptr<int>(), width.data_ptr<int>(), kind.data_ptr<int>(), cidx.data_ptr<int>(),
+                             (int)start.numel()};
+}
+
+void activate(const Tensor& logits, const Tensor& out, const Tensor& start, const Tensor& width, const Tensor& kind,
+              const Tensor& cidx, double tau, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+  check_f32_2d(logits, "logits");
+  check_f32_2d(out, "out");
+  TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) >= logits.size(1), "activate: shapes");
+  fedtgan::launch_activate(cfp(logits), ld_of(logits), fp(out), ld_of(out), (int)logits.size(0),
+                           spans_of(start, width, kind, cidx), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
+                           (uint32_t)stream, cur_stream());
+}
+
+void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, const Tensor& start, const Tensor& width,
+                const Tensor& kind, const Tensor& cidx, const Tensor& col, const Tensor& opt, const Tensor& dlogits,
+                const Tensor& loss, double tau) {
+  check_f32_2d(dact, "dact");
+  check_f32_2d(act, "act");
+  check_f32_2d(logits, "logits");
+  check_f32_2d(dlogits, "dlogits");
+  const int64_t rows = logits.size(0);
+  TORCH_CHECK(dact.size(0) == rows && act.size(0) == rows && dlogits.size(0) == rows && col.numel() >= rows,
+              "act_bwd_ce: rows");
+  fedtgan::launch_act_bwd_ce(cfp(dact), ld_of(dact), cfp(act), ld_of(act), cfp(logits), ld_of(logits),
+                             spans_of(start, width, kind, cidx), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
+                             ld_of(dlogits), (int)rows, (float)tau, fp(loss), cur_stream());
+}
+
+void slerp(const Tensor& real, const Tensor& fake, const Tensor& out, int64_t seed, const Tensor& rng_ctr,
+           int64_t stream) {
+  check_f32_2d(real, "real");
+  check_f32_2d(fake, "fake");
+  check_f32_2d(out, "out");
+  TORCH_CHECK(real.sizes() == fake.sizes() && real.sizes() == out.sizes(), "slerp: shapes");
+  TORCH_CHECK(ld_of(real) == ld_of(fake) && ld_of(real) == ld_of(out), "slerp: strides");
+  fedtgan::launch_slerp(cfp(real), cfp(fake), fp(out), (int)real.size(0), (int)real.size(1), ld_of(real),
+                        (uint64_t)seed, ctr_ptr(rng_ctr), (uint32_t)stream, cur_stream());
+}
+
+void gp_scale(const Tensor& g, const Tensor& out, double lam, const Tensor& loss) {
+  check_f32_2d(g, "g");
+  check_f32_2d(out, "out");
+  TORCH_CHECK(g.sizes() == out.sizes(), "gp_scale: shapes");
+  fedtgan::launch_gp_scale(cfp(g), ld_of(g), fp(out), ld_of(out), (int)g.size(0), (int)g.size(1), (float)lam,
+                           fp(loss), cur_stream());
+}
+
+void d_head(const Tensor& d, const Tensor& ms, const Tensor& v, const Tensor& e, const Tensor& coef,
+            const Tensor& wloss, const Tensor& y, const Tensor& a, const Tensor& loss) {
+  check_f32_2d(d, "d");
+  check_f32_2d(ms, "ms");
+  check_f32_2d(a, "a");
+  const int64_t rows = d.size(0), cols = d.size(1);
+  TORCH_CHECK(ms.sizes() == d.sizes() && a.sizes() == d.sizes() && v.numel() == cols && coef.numel() >= rows &&
+                  wloss.numel() >= rows && y.numel() >= rows,
+              "d_head: shapes");
+  fedtgan::launch_d_head(cfp(d), ld_of(d), cfp(ms), ld_of(ms), cfp(v), cfp(e), cfp(coef), cfp(wloss), fp(y), fp(a),
+                         ld_of(a), (int)rows, (int)cols, fp(loss), cur_stream());
+}
+
+void colsum(at::TensorList srcs, at::TensorList outs) {
+  TORCH_CHECK(srcs.size() == outs.size() && srcs.size() <= 8, "colsum: up to 8 jobs");
+  std::vector<fedtgan::ColsumJob> jobs;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    check_f32_2d(srcs[i], "colsum src");
+    TORCH_CHECK(outs[i].numel() == srcs[i].size(1) && outs[i].is_contiguous(), "colsum: out");
+    jobs.push_back({cfp(srcs[i]), ld_of(srcs[i]), (int)srcs[i].size(0), (int)srcs[i].size(1), fp(outs[i])});
+  }
+  fedtgan::launch_colsum(jobs.data(), (int)jobs.size(), cur_stream());
+}
+
+void bn_relu_train(const Tensor& a, const Tensor& gamma, const Tensor& beta, const Tensor& out, const Tensor& nhat,
+                   const Tensor& mean, const Tensor& invstd, const Tensor& rm, const Tensor& rv, double momentum,
+                   double eps) {
+  check_f32_2d(a, "a");
+  check_f32_2d(out, "out");
+  check_f32_2d(nhat, "nhat");
+  TORCH_CHECK(a.size(0) <= 1024, "bn_relu_train: batch > 1024 unsupported (rows kept in registers)");
+  TORCH_CHECK(out.sizes() == a.sizes() && nhat.sizes() == a.sizes() && gamma.numel() == a.size(1), "bn: shapes");
+  fedtgan::launch_bn_relu_train(cfp(a), ld_of(a), cfp(gamma), cfp(beta), fp(out), ld_of(out), fp(nhat), ld_of(nhat),
+                                fp(mean), fp(invstd), fp(rm), fp(rv), (int)a.size(0), (int)a.size(1), (float)momentum,
+                                (float)eps, cur_stream());
+}
+
+void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Tensor& gamma, const Tensor& invstd,
+                 const Tensor& da, const Tensor& dgamma, const Tensor& dbeta, const optional<Tensor>& dbias) {
+  check_f32_2d(dr, "dr");
+  check_f32_2d(r, "r");
+  check_f32_2d(nhat, "nhat");
+  check_f32_2d(da, "da");
+  TORCH_CHECK(dr.size(0) <= 1024, "bn_relu_bwd: batch > 1024 unsupported");
+  TORCH_CHECK(r.sizes() == dr.sizes() && nhat.sizes() == dr.sizes() && da.sizes() == dr.sizes(), "bn bwd: shapes");
+  fedtgan::launch_bn_relu_bwd(cfp(dr), ld_of(dr), cfp(r), ld_of(r), cfp(nhat), ld_of(nhat), cfp(gamma), cfp(invstd),
+                              fp(da), ld_of(da), fp(dgamma), fp(dbeta), optp<float>(dbias), (int)dr.size(0),
+                              (int)dr.size(1), cur_stream());
+}
+
+void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& step, double lr, double b1,
+          double b2, double eps, double wd, const optional<Tensor>& rng_bump) {
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam: contiguous");
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: sizes");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0,
+              "adam: buffers must be 16-byte aligned");
+  uint64_t* bump = nullptr;
+  if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
+  fedtgan::launch_adam(fp(p), cfp(g), fp(m), fp(v), cfp(step), p.numel(), (float)lr, (float)b1, (float)b2, (float)eps,
+                       (float)wd, bump, cur_stream());
+}
+
+void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, const Tensor& start,
+                   const Tensor& width, const Tensor& cont, const Tensor& code_off, const Tensor& codes,
+                   const Tensor& mu, const Tensor& sd, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+  check_f32_2d(logits, "logits");
+  TORCH_CHECK(out.scalar_type() == at::kDouble && out.is_contiguous() && out.dim() == 2, "decode: out f64");
+  TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) == kind.numel(), "decode: shapes");
+  TORCH_CHECK(mu.scalar_type() == at::kDouble && sd.scalar_type() == at::kDouble && codes.scalar_type() == at::kDouble,
+              "decode: f64 tables");
+  fedtgan::DecodeArgs a{};
+  a.logits = cfp(logits);
+  a.ldl = ld_of(logits);
+  a.rows = (int)logits.size(0);
+  a.n_cols = (int)kind.numel();
+  a.kind = kind.data_ptr<int>();
+  a.start = start.data_ptr<int>();
+  a.width = width.data_ptr<int>();
+  a.cont = cont.data_ptr<int>();
+  a.code_off = code_off.data_ptr<int>();
+  a.codes = codes.data_ptr<double>();
+  a.mu = mu.data_ptr<double>();
+  a.sd = sd.data_ptr<double>();
+  a.K = mu.dim() == 2 ? (int)mu.size(1) : 1;
+  a.out = out.data_ptr<double>();
+  a.seed = (uint64_t)seed;
+  a.rng_ctr = ctr_ptr(rng_ctr);
+  a.rng_stream = (uint32_t)stream;
+  fedtgan::launch_sample_decode(a, cur_stream());
+}
+
+void rng_bump(const Tensor& ctr) {
+  TORCH_CHECK(ctr.scalar_type() == at::kLong && ctr.is_cuda(), "rng_bump: cuda int64");
+  fedtgan::launch_rng_bump(reinterpret_cast<uint64_t*>(ctr.data_ptr<int64_t>()), cur_stream());
+}
+
+void write_csv(const std::string& path, const Tensor& values, std::vector<std::string> names, std::vector<int64_t> kinds,
+               std::vector<std::string> vocab_flat, std::vector<int64_t> vocab_offsets, int64_t threads) {
+  TORCH_CHECK(!values.is_cuda() && values.scalar_type() == at::kDouble && values.is_contiguous() && values.dim() == 2,
+              "write_csv: values must be a contiguous CPU float64 matrix");
+  const int64_t cols = values.size(1);
+  TORCH_CHECK((int64_t)kinds.size() == cols && (int64_t)names.size() == cols &&
+                  (int64_t)vocab_offsets.size() == cols + 1,
+              "write_csv: descriptors");
+  std::vector<int> k(kinds.begin(), kinds.end());
+  std::vector<std::vector<std::string>> voc((size_t)cols);
+  for (int64_t j = 0; j < cols; ++j)
+    voc[(size_t)j].assign(vocab_flat.begin() + vocab_offsets[(size_t)j], vocab_flat.begin() + vocab_offsets[(size_t)j + 1]);
+  fedtgan::write_csv_file(path, values.data_ptr<double>(), values.size(0), cols, names, k, voc, (int)threads);
+}
+
+std::string py_float(double x) { return fedtgan::format_py_float(x); }
+
+}  // namespace
+
+TORCH_LIBRARY(fedtgan, m) {
+  m.def(
+      "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
+      "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
+      "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps) -> ()");
+  m.def(
+      "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
+      "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
+      "Tensor(f!)? step_bump, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, int stream) -> ()");
+  m.def(
+      "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, float tau, int seed, "
+      "Tensor rng_ctr, int stream) -> ()");
+  m.def(
+      "act_bwd_ce(Tensor dact, Tensor act, Tensor logits, Tensor start, Tensor width, Tensor kind, Tensor cidx, "
+      "Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");
+  m.def("slerp(Tensor real, Tensor fake, Tensor(a!) out, int seed, Tensor rng_ctr, int stream) -> ()");
+  m.def("gp_scale(Tensor g, Tensor(a!) out, float lam, Tensor(b!) loss) -> ()");
+  m.def(
+      "d_head(Tensor d, Tensor ms, Tensor v, Tensor e, Tensor coef, Tensor wloss, Tensor(a!) y, Tensor(b!) a, "
+      "Tensor(c!) loss) -> ()");
+  m.def("colsum(Tensor[] srcs, Tensor(a!)[] outs) -> ()");
+  m.def(
+      "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
+      "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps) -> ()");
+  m.def(
+      "bn_relu_bwd(Tensor dr, Tensor r, Tensor nhat, Tensor gamma, Tensor invstd, Tensor(a!) da, Tensor(b!) dgamma, "
+      "Tensor(c!) dbeta, Tensor(d!)? dbias) -> ()");
+  m.def(
+      "adam(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, "
+      "float wd, Tensor(d!)? rng_bump) -> ()");
+  m.def(
+      "sample_decode(Tensor logits, Tensor(a!) out, Tensor kind, Tensor start, Tensor width, Tensor cont, "
+      "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");
+  m.def("rng_bump(Tensor(a!) ctr) -> ()");
+  m.def(
+      "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
+      "int threads) -> ()");
+  m.def("py_float(float x) -> str", &py_float);
+}
+
+TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
+  m.impl("gemm", &gemm);
+  m.impl("sample", &sample);
+  m.impl("activate", &activate);
+  m.impl("act_bwd_ce", &act_bwd_ce);
+  m.impl("slerp", &slerp);
+  m.impl("gp_scale", &gp_scale);
+  m.impl("d_head", &d_head);
+  m.impl("colsum", &colsum);
+  m.impl("bn_relu_train", &bn_relu_train);
+  m.impl("bn_relu_bwd", &bn_relu_bwd);
+  m.impl("adam", &adam);
+  m.impl("sample_decode", &sample_decode);
+  m.impl("rng_bump", &rng_bump);
+}
+
+TORCH_LIBRARY_IMPL(fedtgan, CPU, m) { m.impl("write_csv", &write_csv); }

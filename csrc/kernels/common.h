@@ -1,0 +1,109 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of fed_tgan_amd.
+//
+// * Philox4x32-10 counter-based RNG.  Every random draw in the training step is addressed by
+//   (seed, stream id, step counter, element index); the step counter lives in device memory
+//   and is bumped by the last kernel of a step, so a captured hipGraph produces fresh numbers
+//   on every replay without any host involvement.
+// * bf16 packing for the MFMA operands (round-to-nearest-even).
+// * wave64 reductions (DPP/shuffle based, 64 lanes -- never 32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fedtgan {
+
+constexpr int WAVE = 64;
+
+struct RngArgs {
+  uint64_t seed;
+  const uint64_t* ctr;  // device-resident step counter
+  uint32_t stream;      // per-call-site stream id
+};
+
+__device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(0xD2511F53u, c.x, hi0);
+    uint32_t lo1 = mulhilo(0xCD9E8D57u, c.z, hi1);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 4 random words for element `idx` of stream `rng.stream` at the current step.
+__device__ __forceinline__ uint4 rng4(const RngArgs& rng, uint64_t step, uint64_t idx) {
+  uint4 c = make_uint4((uint32_t)idx, (uint32_t)(idx >> 32), rng.stream, (uint32_t)step);
+  uint2 k = make_uint2((uint32_t)rng.seed, (uint32_t)(rng.seed >> 32) ^ (uint32_t)(step >> 32));
+  return philox4x32_10(c, k);
+}
+
+// uniform in (0, 1): never exactly 0 or 1 (safe for log(-log(u)) and Box-Muller)
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
+  uint64_t v = ((uint64_t)a << 21) ^ (uint64_t)b;
+  v &= ((1ull << 53) - 1);
+  return ((double)v + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
+  float u1 = u01(a), u2 = u01(b);
+  float r = sqrtf(-2.0f * __logf(u1));
+  float s, c;
+  __sincosf(6.283185307179586f * u2, &s, &c);
+  return make_float2(r * c, r * s);
+}
+
+__device__ __forceinline__ float gumbel(uint32_t x) { return -__logf(-__logf(u01(x))); }
+
+// round-to-nearest-even fp32 -> bf16 bits
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  uint32_t r = ((u >> 16) & 1u) + 0x7FFFu;
+  return (uint16_t)((u + r) >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+// block-wide sum for blockDim.x multiple of 64 (<= 1024); `sh` needs blockDim.x/64 floats
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += sh[i];
+  return t;
+}
+
+}  // namespace fedtgan

@@ -1,0 +1,220 @@
+// Generic skinny-GEMM for the CTGAN step on CDNA4 MFMA (bf16 operands, fp32 accumulate).
+//
+//   C[M,N] = epi( alpha * op(A)[M,K] . op(B)[K,N] + beta * C + bias[N] )
+//
+// op(A) = A or A^T, op(B) = B or B^T, every operand with its own leading dimension so the
+// engine can pass column slices of its concat-free activation buffers (the generator's
+// residual stack, the packed PacGAN input) without copies.
+//
+// Tiling: 64x64 output tile per 256-thread workgroup (4 waves in a 2x2 grid, 32x32 per wave
+// = 2x2 v_mfma_f32_16x16x32_bf16 tiles), BK = 32.  Operands are read from fp32 global memory
+// with coalesced loads along their contiguous dimension, rounded to bf16 and staged in LDS as
+// [row][k] images (k contiguous, row stride padded to 40 elements = 80 B so each lane's
+// 16-byte fragment is a conflict-light ds_read_b128).  Two LDS buffers: the next k-tile's
+// global loads are issued before the current tile's MFMAs (register prefetch), so HBM /
+// Infinity-Cache latency hides under the compute of the previous tile.
+//
+// Split-K (gridDim.z > 1) writes fp32 partial slabs that `gemm_splitk_epilogue` reduces and
+// finishes; with gridDim.z == 1 the epilogue is fused.  Epilogues:
+//   EPI_NONE            out = v
+//   EPI_LRELU_DROPOUT   out = lrelu(v) * keep/(1-p);  ms = lrelu'(v) * keep/(1-p)   (Philox mask)
+//   EPI_MASK            out = v * ms
+//   EPI_RELU            out = max(v, 0)
+#include <algorithm>
+
+#include "common.h"
+#include "launch.h"
+
+namespace fedtgan {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BM = 64, BN = 64, BK = 32, KPAD = 40, NT = 256;
+
+__device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
+  const int epi = g.epi;
+  if (epi == EPI_LRELU_DROPOUT) {
+    const float s = v > 0.f ? 1.f : g.slope;
+    RngArgs rng{g.seed, g.rng_ctr, g.rng_stream};
+    const uint4 r = rng4(rng, step, idx);
+    const float keep = (u01(r.x) >= g.p_drop) ? 1.f / (1.f - g.p_drop) : 0.f;
+    const float f = s * keep;
+    g.ms[(size_t)m * g.ldms + n] = f;
+    return v * f;
+  } else if (epi == EPI_MASK) {
+    return v * g.ms[(size_t)m * g.ldms + n];
+  } else if (epi == EPI_RELU) {
+    return v > 0.f ? v : 0.f;
+  } else if (epi == EPI_BN_EVAL_RELU) {
+    const float y = (v - g.bn_rm[n]) * rsqrtf(g.bn_rv[n] + g.bn_eps) * g.bn_gamma[n] + g.bn_beta[n];
+    return y > 0.f ? y : 0.f;
+  }
+  return v;
+}
+
+// Stage a BM(or BN) x BK tile of an operand into registers (8 fp32 values per thread).
+//   ROWMAJ: element (r, k) at p[r*ld + k] (k contiguous)   -> thread: kp = t%16, r = t/16 + 16*i
+//   else  : element (r, k) at p[k*ld + r] (r contiguous)   -> thread: r = t%64, kp = t/64 + 4*i
+template <bool ROWMAJ>
+__device__ __forceinline__ void load_tile(float (&v)[8], const float* __restrict__ p, int ld, int r0, int rmax, int k0,
+                                          int kmax) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r, k;
+    if (ROWMAJ) {
+      r = r0 + t / 16 + 16 * i;
+      k = k0 + 2 * (t % 16);
+    } else {
+      r = r0 + t % 64;
+      k = k0 + 2 * (t / 64 + 4 * i);
+    }
+    const bool rok = r < rmax;
+    float x0 = 0.f, x1 = 0.f;
+    if (rok && k < kmax) x0 = ROWMAJ ? p[(size_t)r * ld + k] : p[(size_t)k * ld + r];
+    if (rok && k + 1 < kmax) x1 = ROWMAJ ? p[(size_t)r * ld + k + 1] : p[(size_t)(k + 1) * ld + r];
+    v[2 * i] = x0;
+    v[2 * i + 1] = x1;
+  }
+}
+
+template <bool ROWMAJ>
+__device__ __forceinline__ void store_tile(uint16_t* s, const float (&v)[8]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r, kp;
+    if (ROWMAJ) {
+      r = t / 16 + 16 * i;
+      kp = t % 16;
+    } else {
+      r = t % 64;
+      kp = t / 64 + 4 * i;
+    }
+    *reinterpret_cast<uint32_t*>(&s[r * KPAD + 2 * kp]) = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * KPAD];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * KPAD];
+
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int kb = blockIdx.z * g.kchunk;
+  const int ke = min(g.K, kb + g.kchunk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = w >> 1, wn = w & 1;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> row-major in k iff !TA
+  // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged as [n][k]; row-major in k iff TB
+  float ra[8], rb[8];
+  int buf = 0;
+  if (kb < ke) {
+    load_tile<!TA>(ra, g.a, g.lda, m0, g.M, kb, ke);
+    load_tile<TB>(rb, g.b, g.ldb, n0, g.N, kb, ke);
+    store_tile<!TA>(sA[0], ra);
+    store_tile<TB>(sB[0], rb);
+  }
+  __syncthreads();
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) {
+      load_tile<!TA>(ra, g.a, g.lda, m0, g.M, k0 + BK, ke);
+      load_tile<TB>(rb, g.b, g.ldb, n0, g.N, k0 + BK, ke);
+    }
+    const uint16_t* A = sA[buf];
+    const uint16_t* B = sB[buf];
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+      bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      store_tile<!TA>(sA[buf ^ 1], ra);
+      store_tile<TB>(sB[buf ^ 1], rb);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        if (m >= g.M || n >= g.N) continue;
+        const float v0 = acc[i][j][r];
+        if (gridDim.z > 1) {
+          g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = v0;
+          continue;
+        }
+        float v = g.alpha * v0;
+        float* cp = g.c + (size_t)m * g.ldc + n;
+        if (g.beta != 0.f) v += g.beta * (*cp);
+        if (g.bias) v += g.bias[n];
+        *cp = apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n);
+      }
+}
+
+__global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
+  const int splits = g.splitk;
+  const size_t total = (size_t)g.M * g.N;
+  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(idx / g.N), n = (int)(idx % g.N);
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += g.ws[(size_t)z * total + idx];
+    float v = g.alpha * s;
+    float* cp = g.c + (size_t)m * g.ldc + n;
+    if (g.beta != 0.f) v += g.beta * (*cp);
+    if (g.bias) v += g.bias[n];
+    *cp = apply_epi(g, v, m, n, step, idx);
+  }
+}
+
+void launch_gemm(GemmArgs g, hipStream_t stream) {
+  if (g.M <= 0 || g.N <= 0) return;
+  const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
+  if (g.splitk < 1) g.splitk = 1;
+  if (g.K <= 0) g.splitk = 1;
+  int kchunk = (g.K + g.splitk - 1) / g.splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk <= 0) kchunk = BK;
+  g.splitk = (g.K + kchunk - 1) / kchunk;
+  if (g.splitk < 1) g.splitk = 1;
+  g.kchunk = kchunk;
+  dim3 grid(tn, tm, g.splitk), block(NT);
+  if (g.splitk > 1 && g.ws == nullptr) {
+    g.splitk = 1;
+    g.kchunk = g.K;
+    grid.z = 1;
+  }
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<false, true>), grid, block, 0, stream, g);
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<false, false>), grid, block, 0, stream, g);
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<true, false>), grid, block, 0, stream, g);
+  else hipLaunchKernelGGL((gemm_bf16_kernel<true, true>), grid, block, 0, stream, g);
+  if (grid.z > 1) {
+    const size_t total = (size_t)g.M * g.N;
+    int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(gemm_splitk_epilogue, dim3(blocks), dim3(256), 0, stream, g);
+  }
+}
+
+}  // namespace fedtgan

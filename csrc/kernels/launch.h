@@ -1,0 +1,129 @@
+// Host-side launch interface of the fed_tgan_amd HIP kernels (raw pointers + hipStream_t).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fedtgan {
+
+enum Epilogue : int { EPI_NONE = 0, EPI_LRELU_DROPOUT = 1, EPI_MASK = 2, EPI_RELU = 3, EPI_BN_EVAL_RELU = 4 };
+
+struct RngArgs;
+
+struct GemmArgs {
+  const float* a;
+  const float* b;
+  float* c;
+  const float* bias;
+  float* ms;   // EPI_MASK: read; EPI_LRELU_DROPOUT: written (slope * keep / (1 - p))
+  float* ws;   // split-K partial slabs [splitk][M][N]
+  int M, N, K;
+  int lda, ldb, ldc, ldms;
+  int ta, tb;
+  float alpha, beta;
+  int epi;
+  float slope, p_drop;
+  // EPI_BN_EVAL_RELU: out = relu((v - rm) * rsqrt(rv + eps) * gamma + beta)
+  const float* bn_gamma;
+  const float* bn_beta;
+  const float* bn_rm;
+  const float* bn_rv;
+  float bn_eps;
+  uint64_t seed;
+  const uint64_t* rng_ctr;
+  uint32_t rng_stream;
+  int splitk, kchunk;
+};
+
+void launch_gemm(GemmArgs g, hipStream_t stream);
+
+struct SampleArgs {
+  int B, E, C, Dd, n_col, maxw, n_rows;
+  float* h;            // generator input rows: z at h[r*ldh + zc], cond at h[r*ldh + cc]
+  int ldh, zc, cc;
+  float* xf;           // fake block of the D input (cond copy at xf[r*ldx + Dd]); nullable
+  float* xr;           // real block [data row | cond of the permuted fake row]; nullable
+  int ldx;
+  const float* cdf;    // [n_col, maxw]
+  const int* cond_off;
+  const int* cond_w;
+  const int64_t* row_off;   // [n_col, maxw]
+  const int64_t* row_cnt;   // [n_col, maxw]
+  const int64_t* rows;      // CSR row lists
+  const float* data;        // encoded training matrix [n_rows, Dd]
+  int* col;
+  int* opt;
+  float* step_bump;         // optimizer step counter bumped by this launch (nullable)
+  float* metrics;           // zeroed by this launch when zero_metrics
+  int zero_metrics;
+  uint64_t seed;
+  const uint64_t* rng_ctr;
+  uint32_t rng_stream;
+};
+
+void launch_sample(const SampleArgs& a, hipStream_t stream);
+
+struct SpanTables {
+  const int* start;
+  const int* width;
+  const int* kind;      // 0 tanh, 1 softmax
+  const int* cond_idx;  // softmax span -> conditional column index (or -1)
+  int n_span;
+};
+
+void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
+                     uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
+
+void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, const float* logits, int ldl, SpanTables sp,
+                       const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
+                       hipStream_t stream);
+
+void launch_slerp(const float* real, const float* fake, float* out, int rows, int cols, int ld, uint64_t seed,
+                  const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
+
+void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
+                     hipStream_t stream);
+
+void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const float* v, const float* e,
+                   const float* coef, const float* wloss, float* y, float* a, int lda, int rows, int cols, float* loss,
+                   hipStream_t stream);
+
+struct ColsumJob {
+  const float* a;
+  int lda, rows, cols;
+  float* out;
+};
+void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
+
+void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
+                          float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
+                          float momentum, float eps, hipStream_t stream);
+
+void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
+                        const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
+                        float* dbias, int rows, int cols, hipStream_t stream);
+
+void launch_adam(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
+                 float b2, float eps, float wd, uint64_t* rng_ctr_bump, hipStream_t stream);
+
+struct DecodeArgs {
+  const float* logits;
+  int ldl, rows, n_cols;
+  const int* kind;      // per output column: 0 continuous, 1 categorical
+  const int* start;     // span start (continuous: the tanh unit; modes follow)
+  const int* width;     // #valid modes / #categories
+  const int* cont;      // continuous column index into mu/sd
+  const int* code_off;  // categorical: offset into codes
+  const double* codes;
+  const double* mu;     // [n_cont, K]
+  const double* sd;
+  int K;
+  double* out;          // [rows, n_cols]
+  uint64_t seed;
+  const uint64_t* rng_ctr;
+  uint32_t rng_stream;
+};
+void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
+
+void launch_rng_bump(uint64_t* ctr, hipStream_t stream);
+
+}  // namespace fedtgan

@@ -69,15 +69,17 @@ class EngineConfig:
     gen_chunk: int = 8192
 
 
-def get_ops(backend: str, device: torch.device):
+def get_ops(backend: str, device: torch.device, seed: int = 0):
     if backend == "auto":
         backend = "hip" if device.type == "cuda" else "torch"
     if backend == "torch":
         from ..ops.ref import TorchOps
         return TorchOps()
     if backend == "hip":
+        if device.type != "cuda":
+            raise ValueError("the hip backend needs a GPU device")
         from ..ops.hip import HipOps
-        return HipOps()
+        return HipOps(device, seed)
     raise ValueError(backend)
 
 
@@ -87,8 +89,8 @@ class CTGANEngine:
         self.cfg = cfg = cfg or EngineConfig()
         self.layout = layout
         self.device = torch.device(device)
-        self.ops = get_ops(backend, self.device)
         self.seed = int(seed if seed is not None else torch.initial_seed() % (2 ** 31))
+        self.ops = get_ops(backend, self.device, self.seed)
         B, P = cfg.batch_size, cfg.pack
         if B % P:
             raise ValueError("batch_size must be a multiple of pack")
@@ -141,16 +143,23 @@ class CTGANEngine:
         spec.sort(key=lambda t: order[t[2]])
         self.param_spec = spec
         sizes = [int(np.prod(s)) for _, s, _ in spec]
-        total = sum(sizes)
+        # every group starts 64-byte aligned (vectorised optimizer / aggregation kernels)
+        align = 16
+        offsets, pos, prev = [], 0, None
+        for (_, _, grp), n in zip(spec, sizes):
+            if grp != prev:
+                pos = (pos + align - 1) // align * align
+                prev = grp
+            offsets.append(pos)
+            pos += n
+        total = (pos + align - 1) // align * align
         self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
         self.p: Dict[str, torch.Tensor] = {}
-        pos = 0
         self.group_range = {}
-        for (name, shape, grp), n in zip(spec, sizes):
-            self.p[name] = self.flat[pos:pos + n].view(shape)
-            a, _ = self.group_range.get(grp, (pos, pos))
-            self.group_range[grp] = (a, pos + n)
-            pos += n
+        for (name, shape, grp), n, o in zip(spec, sizes, offsets):
+            self.p[name] = self.flat[o:o + n].view(shape)
+            a, _ = self.group_range.get(grp, (o, o))
+            self.group_range[grp] = (a, (o + n + align - 1) // align * align)
         gA, gB = self.group_range["G"]
         dA, dB = self.group_range["D"]
         self.nG, self.nD = gB - gA, dB - dA
@@ -341,13 +350,23 @@ class CTGANEngine:
 
     # ================================================================= steps
     def _d_step(self):
-        o, B, nP = self.ops, self.B, self.nP
-        L = len(self.ddims)
-        o.sample_train(self.tables, B, self.H, self.c_cols, self.z_cols, self.Xd[0:B, self.Dd:], self.Xd[B:2 * B],
-                       self.col, self.opt, stream_id=1)
+        self._d_prepare()
+        self._d_update()
+
+    def _d_prepare(self):
+        """Draw the batch and build the D input: [fake | real | slerp(real, fake)] rows."""
+        o, B = self.ops, self.B
+        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], self.Xd[B:2 * B], self.Dd,
+                       self.col, self.opt, step_counter=self.stepD, metrics=self.metrics, zero_metrics=True,
+                       stream_id=1)
         self._g_forward(self.H, self.logits, training=True)
         o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=2)
         o.slerp(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], stream_id=3)
+
+    def _d_update(self):
+        """D forward on the stacked rows, WGAN + GP backward, D Adam step."""
+        o, B, nP = self.ops, self.B, self.nP
+        L = len(self.ddims)
         allr = slice(0, 3 * nP)
         I = slice(2 * nP, 3 * nP)
         self._d_forward(allr, stream_base=4)
@@ -366,20 +385,28 @@ class CTGANEngine:
         prev = self.X
         for i in range(L):
             o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True)
-            o.colsum(self.A[i][fr], self.g[f"D.{i}.b"])
             prev = self.dl[i]
+        o.colsum_many([self.A[i][fr] for i in range(L)], [self.g[f"D.{i}.b"] for i in range(L)])
         o.gemm(self.dl[L - 1], self.coef3.view(-1, 1), self.g["D.out.W"].view(-1, 1), ta=True)
-        self.g["D.out.b"].zero_()
+        # d(loss)/d(e_out) = sum of the +-1/n_packs seeds = 0 (stays zero from allocation)
         b1, b2 = self.cfg.betas
         o.adam(self.flatD, self.gradD, self.mD, self.vD, self.stepD, self.cfg.lr, b1, b2, self.cfg.adam_eps, 0.0)
 
     def _g_step(self):
-        o, B, nP = self.ops, self.B, self.nP
-        L = len(self.ddims)
-        o.sample_train(self.tables, B, self.H, self.c_cols, self.z_cols, self.Xd[0:B, self.Dd:], None,
-                       self.col, self.opt, stream_id=11)
+        self._g_prepare()
+        self._g_update()
+
+    def _g_prepare(self):
+        o, B = self.ops, self.B
+        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], None, self.Dd,
+                       self.col, self.opt, step_counter=self.stepG, stream_id=11)
         self._g_forward(self.H, self.logits, training=True)
         o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=12)
+
+    def _g_update(self):
+        """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
+        o, B, nP = self.ops, self.B, self.nP
+        L = len(self.ddims)
         fk = slice(0, nP)
         self._d_forward(fk, stream_base=14)
         o.d_head(self.dl[L - 1][fk], self.ms[L - 1][fk], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coefg,
@@ -392,21 +419,21 @@ class CTGANEngine:
         # generator backward
         Lg = len(self.gdims)
         o.gemm(self.dlogits, self.H, self.g["G.out.W"], ta=True)
-        o.colsum(self.dlogits, self.g["G.out.b"])
+        o.colsum_many([self.dlogits], [self.g["G.out.b"]])
         top = self.off[0]
         if Lg:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
         for i in range(Lg - 1, -1, -1):
             a, b_ = self.off[i], self.off[i + 1]
             o.bn_relu_bwd(self.dH[:, b_:a], self.H[:, b_:a], self.nhat[i], self.p[f"G.{i}.gamma"],
-                          self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"])
+                          self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"],
+                          self.g[f"G.{i}.b"])
             o.gemm(self.da[i], self.H[:, a:], self.g[f"G.{i}.W"], ta=True)
-            o.colsum(self.da[i], self.g[f"G.{i}.b"])
             if i > 0:
                 o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0)
         b1, b2 = self.cfg.betas
         o.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
-               self.cfg.l2scale)
+               self.cfg.l2scale, last_in_step=True)
 
     def _one_step(self):
         if hasattr(self.ops, "begin_step"):

@@ -1,0 +1,189 @@
+"""HIP backend of the engine ops: thin dispatch onto ``torch.ops.fedtgan`` (csrc/).
+
+Same method signatures as :class:`fed_tgan_amd.ops.ref.TorchOps`.  There is no silent
+fallback: constructing :class:`HipOps` raises if the native library is not built or does not
+load.  Host-side work per call is limited to picking split-K factors, caching int32 span
+tables on the device and reusing one split-K workspace, so the launch sequence of a step is
+static and hipGraph-capturable.
+
+RNG bookkeeping: one device int64 step counter per engine (``self.ctr``) addresses every
+Philox stream; the generator's Adam launch (last kernel of a step) bumps it, as does each
+generation chunk.  Optimizer step counters are bumped by the sampler launch of the matching
+phase, so Adam itself only reads them.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+from . import native
+
+EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 4
+TILE = 64
+
+
+def _splitk(M: int, N: int, K: int) -> int:
+    tiles = ((M + TILE - 1) // TILE) * ((N + TILE - 1) // TILE)
+    if K < 512 or tiles >= 160:
+        return 1
+    want = max(1, round(256 / tiles))
+    return int(max(1, min(want, K // 128)))
+
+
+class HipOps:
+    name = "hip"
+
+    def __init__(self, device: torch.device, seed: int = 0):
+        self.L = native.require()
+        self.device = device
+        self.seed = int(seed) & ((1 << 62) - 1)
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=device)
+        self.ws = torch.zeros(1 << 20, dtype=torch.float32, device=device)
+        self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
+        self._dec: Dict[int, Tuple] = {}
+        self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
+
+    # ------------------------------------------------------------------ helpers
+    def _workspace(self, n: int) -> torch.Tensor:
+        if self.ws.numel() < n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("split-K workspace must be sized before graph capture")
+            self.ws = torch.zeros(int(n * 1.25), dtype=torch.float32, device=self.device)
+        return self.ws
+
+    def _span_tables(self, spans, cond_spans=None):
+        key = (tuple(spans), tuple(cond_spans or ()))
+        t = self._spans.get(key)
+        if t is None:
+            cidx = []
+            cpos = {s: i for i, (s, _w) in enumerate(cond_spans or [])}
+            ci = 0
+            for s, w, k in spans:
+                if k == 1:
+                    cidx.append(cpos.get(s, ci) if cond_spans else ci)
+                    ci += 1
+                else:
+                    cidx.append(-1)
+            mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
+            t = (mk([s for s, _, _ in spans]), mk([w for _, w, _ in spans]), mk([k for _, _, k in spans]), mk(cidx))
+            self._spans[key] = t
+        return t
+
+    # ------------------------------------------------------------------ GEMM
+    def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
+             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5):
+        M = a.shape[1] if ta else a.shape[0]
+        K = a.shape[0] if ta else a.shape[1]
+        N = b.shape[0] if tb else b.shape[1]
+        sk = _splitk(M, N, K)
+        ws = None
+        if sk > 1:
+            kchunk = ((K + sk - 1) // sk + 31) // 32 * 32
+            s_eff = (K + kchunk - 1) // kchunk
+            ws = self._workspace(s_eff * M * N)
+        g = bn or (None, None, None, None)
+        self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
+                    float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
+                    float(bn_eps))
+
+    def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
+                       momentum=0.1, eps=1e-5):
+        if training:
+            self.gemm(x, W, abuf, tb=True, bias=b)
+            self.L.bn_relu_train(abuf, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps))
+        else:
+            self.gemm(x, W, out, tb=True, bias=b, epi=EPI_BN_EVAL_RELU, bn=(gamma, beta, rmean, rvar), bn_eps=eps)
+
+    def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
+                    eps=1e-5):
+        if not training:
+            raise NotImplementedError("eval-mode BN is fused into the GEMM epilogue on the HIP backend")
+        self.L.bn_relu_train(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps))
+
+    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
+        self.L.bn_relu_bwd(dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias)
+
+    # ------------------------------------------------------------------ samplers
+    def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,
+                     metrics=None, zero_metrics=False, stream_id=0):
+        E = z_cols[1] - z_cols[0]
+        if x_real is not None:
+            self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, x_real, Dd, t["cdf_log"], t["cond_offset"],
+                          t["cond_width"], t["row_offset"], t["row_count"], t["rows"], t["data"], col_out, opt_out,
+                          step_counter, metrics, bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
+        else:
+            self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, None, Dd, t["cdf_log"], t["cond_offset"],
+                          t["cond_width"], None, None, None, None, col_out, opt_out, step_counter, metrics,
+                          bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
+
+    def sample_gen(self, t, h, c_cols, z_cols, col_out=None, opt_out=None, stream_id=0):
+        E = z_cols[1] - z_cols[0]
+        self.L.sample(h, z_cols[0], c_cols[0], E, None, None, 0, t["cdf_emp"], t["cond_offset"], t["cond_width"],
+                      None, None, None, None, col_out, opt_out, None, None, False, self.seed, self.ctr,
+                      int(stream_id) * 16)
+
+    # ------------------------------------------------------------------ activations
+    def activate(self, logits, out, spans, tau=0.2, stream_id=0):
+        st, w, k, ci = self._span_tables(spans)
+        self.L.activate(logits, out, st, w, k, ci, float(tau), self.seed, self.ctr, int(stream_id) * 16)
+
+    def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
+        st, w, k, ci = self._span_tables(spans, cond_spans)
+        self.L.act_bwd_ce(dact, act, logits, st, w, k, ci, col, opt, dlogits, loss_out, float(tau))
+
+    # ------------------------------------------------------------------ gradient penalty
+    def slerp(self, real, fake, out, stream_id=0):
+        self.L.slerp(real, fake, out, self.seed, self.ctr, int(stream_id) * 16)
+
+    def gp_scale(self, g, out, lam, loss_out):
+        self.L.gp_scale(g, out, float(lam), loss_out)
+
+    def d_head(self, d_last, ms_last, v, e, coef, wloss, y, a_last, loss_out):
+        self.L.d_head(d_last, ms_last, v, e, coef, wloss, y, a_last, loss_out)
+
+    def colsum(self, a, out, beta=0.0):
+        if beta != 0.0:
+            raise NotImplementedError
+        self.L.colsum([a], [out])
+
+    def colsum_many(self, srcs, outs):
+        self.L.colsum(list(srcs), list(outs))
+
+    # ------------------------------------------------------------------ optimizer
+    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False):
+        self.L.adam(p, g, m, v, step, float(lr), float(b1), float(b2), float(eps), float(wd),
+                    self.ctr if last_in_step else None)
+
+    # ------------------------------------------------------------------ generation decode
+    def _decode_tables(self, tabs):
+        key = id(tabs)
+        t = self._dec.get(key)
+        if t is None:
+            kind, start, width, cont, code_off, codes = [], [], [], [], [], []
+            for kk, s, w, c, cd in tabs["cols"]:
+                kind.append(kk)
+                start.append(s)
+                width.append(w)
+                cont.append(max(c, 0))
+                code_off.append(len(codes))
+                if cd is not None:
+                    codes.extend(cd.detach().cpu().tolist())
+            mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
+            codes_t = torch.tensor(codes if codes else [0.0], dtype=torch.float64, device=self.device)
+            mu = tabs["mu"].to(self.device, torch.float64).contiguous()
+            sd = tabs["sd"].to(self.device, torch.float64).contiguous()
+            if mu.numel() == 0:
+                mu = torch.zeros(1, 1, dtype=torch.float64, device=self.device)
+                sd = torch.ones(1, 1, dtype=torch.float64, device=self.device)
+            t = (mk(kind), mk(start), mk(width), mk(cont), mk(code_off), codes_t, mu, sd)
+            self._dec[key] = t
+        return t
+
+    def sample_decode(self, logits, out, tabs, stream_id=0):
+        kind, start, width, cont, code_off, codes, mu, sd = self._decode_tables(tabs)
+        self.L.sample_decode(logits, out, kind, start, width, cont, code_off, codes, mu, sd, self.seed, self.ctr,
+                             int(stream_id) * 16)
+        self.L.rng_bump(self.ctr)
+        return out

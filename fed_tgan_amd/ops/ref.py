@@ -51,13 +51,17 @@ class TorchOps:
         c.copy_(acc)
 
     # ------------------------------------------------------------------ samplers
-    def sample_train(self, t, B, h, c_cols, z_cols, x_fake_c, x_real, col_out, opt_out, stream_id=0):
+    def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,
+                     metrics=None, zero_metrics=False, stream_id=0):
         """Draw the training conditional batch, noise, permutation and real rows.
 
-        h[:, z_cols] <- N(0,1); h[:, c_cols] <- c1; x_fake_c <- c1; x_real <- [data[row], c1[perm]].
+        h[:, z_cols] <- N(0,1); h[:, c_cols] <- c1; x_fake[:, Dd:] <- c1; x_real <- [data[row], c1[perm]].
         t: dict of device tables (cdf_log, cond_offset, cond_width, row_offset, row_count, rows, data).
+        (step_counter / metrics are bookkeeping of the HIP backend; eager Adam counts its own steps.)
         """
         dev = h.device
+        B = h.shape[0]
+        x_fake_c = x_fake[:, Dd:]
         n_col = t["cond_width"].numel()
         h[:, z_cols[0]:z_cols[1]].normal_()
         c1 = h[:, c_cols[0]:c_cols[1]]
@@ -129,7 +133,7 @@ class TorchOps:
         a = torch.addmm(b, x, W.t())
         self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps)
 
-    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta):
+    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
         dy = dr * (r > 0).to(dr.dtype)
         dg = (dy * nhat).sum(0)
         db = dy.sum(0)
@@ -137,6 +141,8 @@ class TorchOps:
         dbeta.copy_(db)
         n = dr.shape[0]
         da.copy_(gamma * invstd * (dy - db / n - nhat * (dg / n)))
+        if dbias is not None:
+            dbias.copy_(da.sum(0))
 
     # ------------------------------------------------------------------ activations
     def activate(self, logits, out, spans, tau=0.2, stream_id=0):
@@ -206,8 +212,12 @@ class TorchOps:
         else:
             out.mul_(beta).add_(a.sum(0))
 
+    def colsum_many(self, srcs, outs):
+        for a, o in zip(srcs, outs):
+            o.copy_(a.sum(0))
+
     # ------------------------------------------------------------------ optimizer
-    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd):
+    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False):
         """torch.optim.Adam (L2 weight decay added to the gradient, not AdamW); step is a device counter."""
         step.add_(1)
         if wd != 0.0:

@@ -23,7 +23,7 @@ def small_table(n_rows: int = 1500, seed: int = 0):
     meta, vocabs, _ = merge_categorical_metas([tp.local_meta()])
     enc = tp.encode(vocabs)
     cat = tp.categorical_indices()
-    tr = VGMTransformer().fit(enc, cat, (), seed=0)
+    tr = VGMTransformer().fit(enc, cat, (), seed=0, backend="sklearn" if n_rows <= 5000 else "torch")
     tr.refit(enc, meta, vocabs, cat, (), tr.bank, tr.components)
     X = tr.transform(enc, np.random.default_rng(seed))
     return spec, df, tp, meta, vocabs, enc, tr, X

@@ -1,0 +1,122 @@
+"""HIP engine step vs the torch-autograd oracle of the reference math (bf16-MFMA tolerances).
+
+The batch is drawn by the HIP sampler; the oracle reuses the drawn rows, the Gumbel noise
+recovered from the kernel's own softmax output (g = tau*log(y) - logits, exact up to a
+per-span constant that softmax ignores) and the dropout masks recovered from the saved
+mask*slope buffers.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fed_tgan_amd.models.ctgan import Generator, cond_loss
+from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+
+from helpers import d_forward_masked, keep_mask_from_ms, small_table
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _engine():
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    torch.manual_seed(0)
+    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500), DEV, backend="hip", seed=11)
+    eng.set_training_data(X)
+    return eng, tr
+
+
+def _masks(eng, rows, P, X):
+    masks, h = [], X
+    for i in range(len(eng.ddims)):
+        pre = h @ P[f"D.{i}.W"].t() + P[f"D.{i}.b"]
+        M = keep_mask_from_ms(eng.ms[i][rows], pre)
+        M = torch.where(M > 1.0, torch.full_like(M, 2.0), torch.zeros_like(M))   # snap rounding-level noise
+        masks.append(M)
+        h = F.leaky_relu(pre, 0.2) * M
+    return masks
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def test_hip_d_update_matches_autograd():
+    eng, tr = _engine()
+    B, nP = eng.B, eng.nP
+    eng._d_prepare()
+    torch.cuda.synchronize()
+    Xf = eng.Xd[0:B].reshape(nP, eng.K1).clone()
+    Xr = eng.Xd[B:2 * B].reshape(nP, eng.K1).clone()
+    Xi0 = eng.Xd[2 * B:3 * B].reshape(nP, eng.K1).clone()
+    P = {n: t.detach().clone() for n, t in eng.p.items() if n.startswith("D.")}
+    eng._d_update()
+    torch.cuda.synchronize()
+    L = len(eng.ddims)
+    Q = {n: t.clone().requires_grad_(True) for n, t in P.items()}
+    Ws = [Q[f"D.{i}.W"] for i in range(L)]
+    bs = [Q[f"D.{i}.b"] for i in range(L)]
+    Xi = Xi0.clone().requires_grad_(True)
+    yf = d_forward_masked(Xf, Ws, bs, _masks(eng, slice(0, nP), P, Xf), Q["D.out.W"], Q["D.out.b"])
+    yr = d_forward_masked(Xr, Ws, bs, _masks(eng, slice(nP, 2 * nP), P, Xr), Q["D.out.W"], Q["D.out.b"])
+    yi = d_forward_masked(Xi, Ws, bs, _masks(eng, slice(2 * nP, 3 * nP), P, Xi0), Q["D.out.W"], Q["D.out.b"])
+    g = torch.autograd.grad(yi.sum(), Xi, create_graph=True)[0]
+    pen = ((g.norm(2, dim=1) - 1) ** 2).mean() * 10.0
+    loss = yf.mean() - yr.mean()
+    (loss + pen).backward()
+    assert abs(eng.metrics[0].item() - loss.item()) < 2e-2 * (1 + abs(loss.item()))
+    assert abs(eng.metrics[1].item() - pen.item()) < 2e-2 * (1 + abs(pen.item()))
+    for n, t in Q.items():
+        if n == "D.out.b":
+            assert eng.g[n].abs().max().item() == 0.0
+            continue
+        assert _rel(eng.g[n], t.grad) < 3e-2, (n, _rel(eng.g[n], t.grad))
+
+
+def test_hip_g_update_matches_autograd():
+    eng, tr = _engine()
+    B, nP, Dd = eng.B, eng.nP, eng.Dd
+    eng._d_step()
+    before = {n: t.detach().clone() for n, t in eng.p.items()}
+    eng._g_prepare()
+    torch.cuda.synchronize()
+    x0 = eng.H[:, eng.off[0]:].clone()
+    act_k = eng.Xd[0:B, :Dd].clone()
+    logits_k = eng.logits.clone()
+    eng._g_update()
+    torch.cuda.synchronize()
+    G = Generator(eng.E + eng.C, eng.gdims, Dd).to(DEV)
+    sd = {k: before[n] for k, n in eng.g_key_map()}
+    for i in range(len(eng.gdims)):
+        sd[f"seq.{i}.bn.num_batches_tracked"] = torch.tensor(0)
+    G.load_state_dict(sd)
+    G.train()
+    logits = G(x0)
+    assert _rel(logits, logits_k) < 2e-2
+    acts = []
+    for s, w, k in eng.spans:
+        x = logits[:, s:s + w]
+        if k == 0:
+            acts.append(torch.tanh(x))
+        else:
+            gn = (0.2 * torch.log(act_k[:, s:s + w].clamp_min(1e-30)) - logits_k[:, s:s + w]).detach()
+            acts.append(torch.softmax((x + gn) / 0.2, dim=1))
+    c1 = x0[:, eng.E:]
+    fake = torch.cat(acts + [c1], dim=1).reshape(nP, eng.K1)
+    L = len(eng.ddims)
+    P = {n: before[n] for n in before if n.startswith("D.")}
+    masks = _masks(eng, slice(0, nP), P, fake.detach())
+    y = d_forward_masked(fake, [P[f"D.{i}.W"] for i in range(L)], [P[f"D.{i}.b"] for i in range(L)], masks,
+                         P["D.out.W"], P["D.out.b"])
+    m1 = torch.zeros(B, eng.layout.n_col, device=DEV)
+    m1[torch.arange(B), eng.col.long()] = 1.0
+    ce = cond_loss(logits, tr.output_info, c1, m1)
+    (-y.mean() + ce).backward()
+    assert abs(eng.metrics[3].item() - ce.item()) < 2e-2 * (1 + ce.item())
+    gsd = dict(G.named_parameters())
+    for k, n in eng.g_key_map():
+        if k in gsd and not k.endswith("fc.bias"):
+            assert _rel(eng.g[n], gsd[k].grad) < 5e-2, (k, _rel(eng.g[n], gsd[k].grad))
