@@ -43,7 +43,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
           const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
-          const optional<Tensor>& bn_rv, double bn_eps) {
+          const optional<Tensor>& bn_rv, double bn_eps, bool f32) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -89,6 +89,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.seed = (uint64_t)seed;
   g.rng_ctr = ctr_ptr(rng_ctr);
   g.rng_stream = (uint32_t)stream;
+  g.f32 = f32 ? 1 : 0;
   fedtgan::launch_gemm(g, cur_stream());
 }
 
@@ -313,7 +314,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
-      "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps) -> ()");
+      "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

@@ -80,26 +80,46 @@ __device__ __forceinline__ void load_tile(float (&v)[8], const float* __restrict
 }
 
 template <bool ROWMAJ>
-__device__ __forceinline__ void store_tile(uint16_t* s, const float (&v)[8]) {
+__device__ __forceinline__ void tile_coords(int i, int& r, int& kp) {
   const int t = threadIdx.x;
+  if (ROWMAJ) {
+    r = t / 16 + 16 * i;
+    kp = t % 16;
+  } else {
+    r = t % 64;
+    kp = t / 64 + 4 * i;
+  }
+}
+
+// bf16 image: [row][KPAD] (k contiguous), two k per 32-bit store
+template <bool ROWMAJ>
+__device__ __forceinline__ void store_tile(uint16_t* s, const float (&v)[8]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int r, kp;
-    if (ROWMAJ) {
-      r = t / 16 + 16 * i;
-      kp = t % 16;
-    } else {
-      r = t % 64;
-      kp = t / 64 + 4 * i;
-    }
+    tile_coords<ROWMAJ>(i, r, kp);
     *reinterpret_cast<uint32_t*>(&s[r * KPAD + 2 * kp]) = pack_bf16x2(v[2 * i], v[2 * i + 1]);
   }
 }
 
-template <bool TA, bool TB>
-__global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) uint16_t sA[2][BM * KPAD];
-  __shared__ __attribute__((aligned(16))) uint16_t sB[2][BN * KPAD];
+// fp32 image: [row][KPADF]; odd stride keeps the 16 rows a 16x16x4 fragment reads on distinct banks
+constexpr int KPADF = 33;
+template <bool ROWMAJ>
+__device__ __forceinline__ void store_tile_f32(float* s, const float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r, kp;
+    tile_coords<ROWMAJ>(i, r, kp);
+    s[r * KPADF + 2 * kp] = v[2 * i];
+    s[r * KPADF + 2 * kp + 1] = v[2 * i + 1];
+  }
+}
+
+template <bool TA, bool TB, bool F32>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
+  // one LDS array (two stages of A and B); bf16 mode uses the first half of it
+  constexpr int STAGE = F32 ? (BM + BN) * KPADF * 4 : (BM + BN) * KPAD * 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
 
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int kb = blockIdx.z * g.kchunk;
@@ -113,6 +133,17 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto stage_store = [&](int st, const float (&ra)[8], const float (&rb)[8]) {
+    unsigned char* base = smem + st * STAGE;
+    if constexpr (F32) {
+      store_tile_f32<!TA>(reinterpret_cast<float*>(base), ra);
+      store_tile_f32<TB>(reinterpret_cast<float*>(base) + BM * KPADF, rb);
+    } else {
+      store_tile<!TA>(reinterpret_cast<uint16_t*>(base), ra);
+      store_tile<TB>(reinterpret_cast<uint16_t*>(base) + BM * KPAD, rb);
+    }
+  };
+
   // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> row-major in k iff !TA
   // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged as [n][k]; row-major in k iff TB
   float ra[8], rb[8];
@@ -120,8 +151,7 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmArgs g) {
   if (kb < ke) {
     load_tile<!TA>(ra, g.a, g.lda, m0, g.M, kb, ke);
     load_tile<TB>(rb, g.b, g.ldb, n0, g.N, kb, ke);
-    store_tile<!TA>(sA[0], ra);
-    store_tile<TB>(sB[0], rb);
+    stage_store(0, ra, rb);
   }
   __syncthreads();
   for (int k0 = kb; k0 < ke; k0 += BK) {
@@ -130,22 +160,38 @@ __global__ __launch_bounds__(NT) void gemm_bf16_kernel(GemmArgs g) {
       load_tile<!TA>(ra, g.a, g.lda, m0, g.M, k0 + BK, ke);
       load_tile<TB>(rb, g.b, g.ldb, n0, g.N, k0 + BK, ke);
     }
-    const uint16_t* A = sA[buf];
-    const uint16_t* B = sB[buf];
-    bf16x8 af[2], bfr[2];
+    if constexpr (F32) {
+      const float* A = reinterpret_cast<const float*>(smem + buf * STAGE);
+      const float* B = A + BM * KPADF;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
-      bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+      for (int s4 = 0; s4 < BK / 4; ++s4) {
+        const int kk = 4 * s4 + (lane >> 4);
+        float af[2], bfv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          af[i] = A[(wm * 32 + i * 16 + (lane & 15)) * KPADF + kk];
+          bfv[i] = B[(wn * 32 + i * 16 + (lane & 15)) * KPADF + kk];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
+      const uint16_t* B = A + BM * KPAD;
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+        bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) {
-      store_tile<!TA>(sA[buf ^ 1], ra);
-      store_tile<TB>(sB[buf ^ 1], rb);
-    }
+    if (more) stage_store(buf ^ 1, ra, rb);
     __syncthreads();
     buf ^= 1;
   }
@@ -206,10 +252,17 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
     g.kchunk = g.K;
     grid.z = 1;
   }
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<false, true>), grid, block, 0, stream, g);
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<false, false>), grid, block, 0, stream, g);
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_bf16_kernel<true, false>), grid, block, 0, stream, g);
-  else hipLaunchKernelGGL((gemm_bf16_kernel<true, true>), grid, block, 0, stream, g);
+#define FEDTGAN_GEMM_DISPATCH(F)                                                                         \
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F>), grid, block, 0, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F>), grid, block, 0, stream, g); \
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F>), grid, block, 0, stream, g);   \
+  else hipLaunchKernelGGL((gemm_kernel<true, true, F>), grid, block, 0, stream, g);
+  if (g.f32) {
+    FEDTGAN_GEMM_DISPATCH(true)
+  } else {
+    FEDTGAN_GEMM_DISPATCH(false)
+  }
+#undef FEDTGAN_GEMM_DISPATCH
   if (grid.z > 1) {
     const size_t total = (size_t)g.M * g.N;
     int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);

@@ -32,6 +32,7 @@ struct GemmArgs {
   const uint64_t* rng_ctr;
   uint32_t rng_stream;
   int splitk, kchunk;
+  int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);

@@ -67,9 +67,10 @@ class EngineConfig:
     bn_momentum: float = 0.1
     bn_eps: float = 1e-5
     gen_chunk: int = 8192
+    precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
 
 
-def get_ops(backend: str, device: torch.device, seed: int = 0):
+def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
     if backend == "auto":
         backend = "hip" if device.type == "cuda" else "torch"
     if backend == "torch":
@@ -79,7 +80,7 @@ def get_ops(backend: str, device: torch.device, seed: int = 0):
         if device.type != "cuda":
             raise ValueError("the hip backend needs a GPU device")
         from ..ops.hip import HipOps
-        return HipOps(device, seed)
+        return HipOps(device, seed, precision)
     raise ValueError(backend)
 
 
@@ -90,7 +91,7 @@ class CTGANEngine:
         self.layout = layout
         self.device = torch.device(device)
         self.seed = int(seed if seed is not None else torch.initial_seed() % (2 ** 31))
-        self.ops = get_ops(backend, self.device, self.seed)
+        self.ops = get_ops(backend, self.device, self.seed, cfg.precision)
         B, P = cfg.batch_size, cfg.pack
         if B % P:
             raise ValueError("batch_size must be a multiple of pack")

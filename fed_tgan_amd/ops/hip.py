@@ -35,8 +35,11 @@ def _splitk(M: int, N: int, K: int) -> int:
 class HipOps:
     name = "hip"
 
-    def __init__(self, device: torch.device, seed: int = 0):
+    def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16"):
         self.L = native.require()
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
+        self.f32 = precision == "fp32"
         self.device = device
         self.seed = int(seed) & ((1 << 62) - 1)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=device)
@@ -86,7 +89,7 @@ class HipOps:
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
-                    float(bn_eps))
+                    float(bn_eps), self.f32)
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5):

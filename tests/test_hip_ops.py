@@ -31,23 +31,33 @@ def mat(*shape, seed=0):
     return torch.randn(*shape, generator=g).to(DEV)
 
 
+@pytest.fixture(scope="module")
+def hip32():
+    from fed_tgan_amd.ops.hip import HipOps
+    return HipOps(DEV, seed=1234, precision="fp32")
+
+
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(150, 256, 6240), (50, 6240, 256), (500, 323, 941), (7, 5, 3), (256, 430, 500)])
-def test_gemm_layouts(hip, ta, tb, M, N, K):
-    a = mat(*( (K, M) if ta else (M, K) ), seed=1)
-    b = mat(*( (N, K) if tb else (K, N) ), seed=2)
+def test_gemm_layouts(hip, hip32, ta, tb, M, N, K):
+    a = mat(*((K, M) if ta else (M, K)), seed=1)
+    b = mat(*((N, K) if tb else (K, N)), seed=2)
     bias = mat(N, seed=3)
+    ref32 = (a.double().t() if ta else a.double()) @ (b.double().t() if tb else b.double()) + bias.double()
+    # bf16 operands: equal to the fp32 product of the bf16-rounded inputs
     c = torch.zeros(M, N, device=DEV)
     hip.gemm(a, b, c, ta=ta, tb=tb, bias=bias)
     A = bf(a).t() if ta else bf(a)
     B = bf(b).t() if tb else bf(b)
     ref = A @ B + bias
     torch.cuda.synchronize()
-    err = (c - ref).abs().max().item()
-    assert err <= 1e-4 * math.sqrt(K) * 10 + 1e-5, err
-    # and close to the true fp32 product at bf16 input precision
-    ref32 = ((a.t() if ta else a) @ (b.t() if tb else b)) + bias
-    assert (c - ref32).abs().max().item() < 0.05 * math.sqrt(K) / 8 + 0.05
+    assert (c - ref).abs().max().item() <= 1e-4 * math.sqrt(K) * 10 + 1e-5
+    assert (c.double() - ref32).abs().max().item() < 4e-3 * math.sqrt(K) * 6 + 1e-3   # bf16 input rounding
+    # exact-fp32 MFMA path: fp32 rounding only
+    c32 = torch.zeros(M, N, device=DEV)
+    hip32.gemm(a, b, c32, ta=ta, tb=tb, bias=bias)
+    torch.cuda.synchronize()
+    assert (c32.double() - ref32).abs().max().item() < 2e-6 * K + 1e-5
 
 
 def test_gemm_strided_views_alpha_beta_mask(hip):
@@ -220,7 +230,7 @@ def test_slerp_on_arc(hip):
     om = torch.acos(cos)
     alpha = torch.asin((sol[:, 1] * torch.sin(om)).clamp(-1, 1)) / om
     wa = torch.sin((1 - alpha) * om) / torch.sin(om)
-    assert torch.allclose(wa, sol[:, 0], atol=1e-4)
+    assert torch.allclose(wa, sol[:, 0], atol=2e-3)
     assert (alpha >= -1e-5).all() and (alpha <= 1 + 1e-5).all()
     assert 0.35 < alpha.mean().item() < 0.65
 

@@ -29,11 +29,12 @@ def main():
     ap.add_argument("--backend", default="torch")
     ap.add_argument("--rows", type=int, default=40000)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--precision", default="bf16")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     _, _, _, _, _, _, tr, X = small_table(args.rows, 0)
     print("layout data_dim", tr.layout.data_dim, "n_opt", tr.layout.n_opt, flush=True)
-    eng = CTGANEngine(tr.layout, EngineConfig(), dev, backend=args.backend, seed=1)
+    eng = CTGANEngine(tr.layout, EngineConfig(precision=args.precision), dev, backend=args.backend, seed=1)
     eng.set_training_data(X)
     eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
     t_eager = timeit(lambda: eng.train_steps(1, use_graph=False), args.steps, dev)
