@@ -143,27 +143,32 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
   fedtgan::launch_sample(a, cur_stream());
 }
 
-fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Tensor& kind, const Tensor& cidx) {
+fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Tensor& kind, const Tensor& cidx,
+                             const Tensor& elem) {
   TORCH_CHECK(start.scalar_type() == at::kInt && width.scalar_type() == at::kInt && kind.scalar_type() == at::kInt &&
-                  cidx.scalar_type() == at::kInt,
+                  cidx.scalar_type() == at::kInt && elem.scalar_type() == at::kInt,
               "span tables must be int32");
+  TORCH_CHECK(start.numel() == width.numel() && start.numel() == kind.numel() && start.numel() == cidx.numel(),
+              "span tables: sizes");
   return fedtgan::SpanTables{start.data_ptr<int>(), width.data_ptr<int>(), kind.data_ptr<int>(), cidx.data_ptr<int>(),
-                             (int)start.numel()};
+                             elem.data_ptr<int>(), (int)start.numel(), (int)elem.numel()};
 }
 
 void activate(const Tensor& logits, const Tensor& out, const Tensor& start, const Tensor& width, const Tensor& kind,
-              const Tensor& cidx, double tau, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+              const Tensor& cidx, const Tensor& elem, double tau, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
   check_f32_2d(logits, "logits");
   check_f32_2d(out, "out");
   TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) >= logits.size(1), "activate: shapes");
+  TORCH_CHECK(elem.numel() == logits.size(1), "activate: elem_span must cover every data column");
   fedtgan::launch_activate(cfp(logits), ld_of(logits), fp(out), ld_of(out), (int)logits.size(0),
-                           spans_of(start, width, kind, cidx), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
+                           spans_of(start, width, kind, cidx, elem), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
                            (uint32_t)stream, cur_stream());
 }
 
 void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, const Tensor& start, const Tensor& width,
-                const Tensor& kind, const Tensor& cidx, const Tensor& col, const Tensor& opt, const Tensor& dlogits,
-                const Tensor& loss, double tau) {
+                const Tensor& kind, const Tensor& cidx, const Tensor& elem, const Tensor& col, const Tensor& opt,
+                const Tensor& dlogits, const Tensor& loss, double tau) {
+  TORCH_CHECK(elem.numel() == logits.size(1), "act_bwd_ce: elem_span must cover every data column");
   check_f32_2d(dact, "dact");
   check_f32_2d(act, "act");
   check_f32_2d(logits, "logits");
@@ -172,7 +177,7 @@ void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, con
   TORCH_CHECK(dact.size(0) == rows && act.size(0) == rows && dlogits.size(0) == rows && col.numel() >= rows,
               "act_bwd_ce: rows");
   fedtgan::launch_act_bwd_ce(cfp(dact), ld_of(dact), cfp(act), ld_of(act), cfp(logits), ld_of(logits),
-                             spans_of(start, width, kind, cidx), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
+                             spans_of(start, width, kind, cidx, elem), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
                              ld_of(dlogits), (int)rows, (float)tau, fp(loss), cur_stream());
 }
 
@@ -320,11 +325,11 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
       "Tensor(f!)? step_bump, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def(
-      "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, float tau, int seed, "
-      "Tensor rng_ctr, int stream) -> ()");
+      "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, Tensor elem, "
+      "float tau, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def(
       "act_bwd_ce(Tensor dact, Tensor act, Tensor logits, Tensor start, Tensor width, Tensor kind, Tensor cidx, "
-      "Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");
+      "Tensor elem, Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");
   m.def("slerp(Tensor real, Tensor fake, Tensor(a!) out, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def("gp_scale(Tensor g, Tensor(a!) out, float lam, Tensor(b!) loss) -> ()");
   m.def(

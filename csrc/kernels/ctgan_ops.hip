@@ -23,34 +23,46 @@
 namespace fedtgan {
 
 // ============================================================================ sampling
+// One wave per batch row.  The option of the sampled conditional column is found with a
+// lane-parallel inverse-CDF search (each lane tests one CDF entry, a ballot picks the first
+// hit) -- one memory round trip instead of a serial scan over the span.
 constexpr int SAMPLE_THREADS = 256;
-constexpr int SAMPLE_ROWS = 8;     // rows per workgroup
+constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
+constexpr int SAMPLE_ROWS_PER_WAVE = 2;
+constexpr int SAMPLE_ROWS = SAMPLE_WAVES * SAMPLE_ROWS_PER_WAVE;   // rows per workgroup
 constexpr int MAX_PERM = 4096;
 
-__device__ __forceinline__ void draw_cond(const SampleArgs& a, uint64_t step, int b, int& col, int& opt) {
+__device__ __forceinline__ void draw_cond_wave(const SampleArgs& a, uint64_t step, int b, int lane, int& col,
+                                               int& opt) {
   RngArgs rng{a.seed, a.rng_ctr, a.rng_stream};
   const uint4 r = rng4(rng, step, (uint64_t)b);
   col = min((int)(u01(r.x) * a.n_col), a.n_col - 1);
   const float u = u01(r.y);
   const float* cdf = a.cdf + (size_t)col * a.maxw;
   const int w = a.cond_w[col];
-  int o = 0;
-  while (o < w - 1 && !(cdf[o] > u)) ++o;
-  opt = o;
+  int found = w - 1;
+  for (int base = 0; base < w; base += 64) {
+    const int i = base + lane;
+    const float cv = cdf[min(i, a.maxw - 1)];
+    const unsigned long long hit = __ballot(i < w && cv > u);
+    if (hit) {
+      found = base + __ffsll((long long)hit) - 1;
+      break;
+    }
+  }
+  opt = min(found, w - 1);
 }
 
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   __shared__ uint64_t keys[MAX_PERM];
-  __shared__ int perm_rows[SAMPLE_ROWS];
   const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (blockIdx.x == 0 && tid == 0) {
     if (a.step_bump) a.step_bump[0] += 1.0f;
     if (a.zero_metrics && a.metrics) {
       a.metrics[0] = 0.f; a.metrics[1] = 0.f; a.metrics[2] = 0.f; a.metrics[3] = 0.f;
     }
   }
-  const int r0 = blockIdx.x * SAMPLE_ROWS;
   const bool with_real = a.xr != nullptr && a.n_col > 0;
   // ---- random permutation of the batch (identical in every workgroup: same Philox keys)
   if (with_real) {
@@ -76,46 +88,44 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
         __syncthreads();
       }
     }
-    if (tid < SAMPLE_ROWS && r0 + tid < a.B) perm_rows[tid] = (int)(keys[r0 + tid] & 0xffffffffu);
-    __syncthreads();
   }
-  // ---- this workgroup's rows: noise + conditional vector
-  for (int rr = 0; rr < SAMPLE_ROWS; ++rr) {
-    const int b = r0 + rr;
+  RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
+  RngArgs rp{a.seed, a.rng_ctr, a.rng_stream + 3u};
+  for (int q = 0; q < SAMPLE_ROWS_PER_WAVE; ++q) {
+    const int b = blockIdx.x * SAMPLE_ROWS + wv * SAMPLE_ROWS_PER_WAVE + q;
     if (b >= a.B) break;
     int col = 0, opt = 0;
-    if (a.n_col > 0) draw_cond(a, step, b, col, opt);
+    if (a.n_col > 0) draw_cond_wave(a, step, b, lane, col, opt);
     const int hot = a.n_col > 0 ? a.cond_off[col] + opt : -1;
     float* hrow = a.h + (size_t)b * a.ldh;
-    RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
-    for (int i = tid; i < (a.E + 1) / 2; i += blockDim.x) {
+    for (int i = lane; i < (a.E + 1) / 2; i += 64) {
       const uint4 r = rng4(rz, step, (uint64_t)b * a.E + i);
       const float2 z = box_muller(r.x, r.y);
       hrow[a.zc + 2 * i] = z.x;
       if (2 * i + 1 < a.E) hrow[a.zc + 2 * i + 1] = z.y;
     }
-    for (int i = tid; i < a.C; i += blockDim.x) {
+    float* xf = a.xf ? a.xf + (size_t)b * a.ldx + a.Dd : nullptr;
+    for (int i = lane; i < a.C; i += 64) {
       const float v = (i == hot) ? 1.f : 0.f;
       hrow[a.cc + i] = v;
-      if (a.xf) a.xf[(size_t)b * a.ldx + a.Dd + i] = v;
+      if (xf) xf[i] = v;
     }
-    if (tid == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
+    if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
     if (!with_real) continue;
-    // real row for the permuted condition
-    const int p = perm_rows[rr];
+    // real row drawn for the condition of fake row perm[b]
+    const int p = (int)(keys[b] & 0xffffffffu);
     int pc = 0, po = 0;
-    draw_cond(a, step, p, pc, po);
+    draw_cond_wave(a, step, p, lane, pc, po);
     const int64_t cnt = a.row_cnt[(size_t)pc * a.maxw + po];
-    RngArgs rp{a.seed, a.rng_ctr, a.rng_stream + 3u};
-    const uint4 rr4 = rng4(rp, step, (uint64_t)b);
-    int64_t pick = (int64_t)(u01d(rr4.x, rr4.y) * (double)(cnt > 0 ? cnt : 1));
+    const uint4 r4 = rng4(rp, step, (uint64_t)b);
+    int64_t pick = (int64_t)(u01d(r4.x, r4.y) * (double)(cnt > 0 ? cnt : 1));
     if (pick >= cnt) pick = cnt > 0 ? cnt - 1 : 0;
     const int64_t row = a.rows[a.row_off[(size_t)pc * a.maxw + po] + pick];
     const float* src = a.data + (size_t)row * a.Dd;
     float* dst = a.xr + (size_t)b * a.ldx;
-    for (int i = tid; i < a.Dd; i += blockDim.x) dst[i] = src[i];
+    for (int i = lane; i < a.Dd; i += 64) dst[i] = src[i];
     const int phot = a.cond_off[pc] + po;
-    for (int i = tid; i < a.C; i += blockDim.x) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
+    for (int i = lane; i < a.C; i += 64) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
   }
 }
 
@@ -125,93 +135,135 @@ void launch_sample(const SampleArgs& a, hipStream_t stream) {
 }
 
 // ============================================================================ activation
-// one thread per (row, span); softmax spans are short (<= a few dozen options)
-__global__ __launch_bounds__(256) void activate_kernel(const float* __restrict__ logits, int ldl, float* __restrict__ out,
-                                                       int ldo, int rows, SpanTables sp, float inv_tau, uint64_t seed,
-                                                       const uint64_t* ctr, uint32_t stream_id) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)rows * sp.n_span) return;
-  const int r = (int)(idx / sp.n_span), s = (int)(idx % sp.n_span);
-  const int st = sp.start[s], w = sp.width[s];
-  const float* x = logits + (size_t)r * ldl + st;
-  float* y = out + (size_t)r * ldo + st;
-  if (sp.kind[s] == 0) {
-    for (int i = 0; i < w; ++i) y[i] = tanhf(x[i]);
-    return;
-  }
+// One wave per row.  Element-parallel pass: Gumbel-perturbed logits (or tanh) into an LDS row
+// image; span-parallel pass: each lane reduces one softmax span (max, sum) from LDS;
+// element-parallel pass: normalise and store.
+constexpr int ACT_WAVES = 4;
+
+__global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* __restrict__ logits, int ldl,
+                                                                  float* __restrict__ out, int ldo, int rows,
+                                                                  SpanTables sp, float inv_tau, uint64_t seed,
+                                                                  const uint64_t* ctr, uint32_t stream_id) {
+  extern __shared__ float act_smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * ACT_WAVES + wv;
+  if (r >= rows) return;
+  const int D = sp.dim, S = sp.n_span;
+  float* v = act_smem + (size_t)wv * (D + 2 * S);
+  float* stat = v + D;
+  const float* x = logits + (size_t)r * ldl;
+  float* y = out + (size_t)r * ldo;
   const uint64_t step = ctr ? *ctr : 0ull;
   RngArgs rng{seed, ctr, stream_id};
-  const uint64_t base = ((uint64_t)r << 20) + (uint64_t)st;
-  float mx = -INFINITY;
-  for (int i = 0; i < w; i += 4) {
-    const uint4 u = rng4(rng, step, base + i);
-    const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
-    for (int q = 0; q < 4 && i + q < w; ++q) {
-      const float v = (x[i + q] + gumbel(uu[q])) * inv_tau;
-      y[i + q] = v;
-      mx = fmaxf(mx, v);
+  const uint64_t base = (uint64_t)r << 20;
+  for (int j = lane; j < D; j += 64) {
+    const int s = sp.elem_span[j];
+    const float xv = x[j];
+    if (sp.kind[s] == 0) {
+      y[j] = tanhf(xv);
+    } else {
+      v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
     }
   }
-  float sum = 0.f;
-  for (int i = 0; i < w; ++i) {
-    const float e = __expf(y[i] - mx);
-    y[i] = e;
-    sum += e;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int s = lane; s < S; s += 64) {
+    if (sp.kind[s] == 0) continue;
+    const int st = sp.start[s], w = sp.width[s];
+    float m = -INFINITY;
+    for (int i = 0; i < w; ++i) m = fmaxf(m, v[st + i]);
+    float sum = 0.f;
+    for (int i = 0; i < w; ++i) sum += __expf(v[st + i] - m);
+    stat[2 * s] = m;
+    stat[2 * s + 1] = 1.f / sum;
   }
-  const float inv = 1.f / sum;
-  for (int i = 0; i < w; ++i) y[i] *= inv;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int j = lane; j < D; j += 64) {
+    const int s = sp.elem_span[j];
+    if (sp.kind[s] != 0) y[j] = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
+  }
 }
+
+static size_t act_smem_bytes(const SpanTables& sp) { return (size_t)ACT_WAVES * (sp.dim + 2 * sp.n_span) * sizeof(float); }
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream) {
-  const int64_t n = (int64_t)rows * sp.n_span;
-  if (n == 0) return;
-  hipLaunchKernelGGL(activate_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, logits, ldl, out, ldo,
-                     rows, sp, 1.f / tau, seed, ctr, stream_id);
+  if (rows == 0) return;
+  hipLaunchKernelGGL(activate_kernel, dim3((rows + ACT_WAVES - 1) / ACT_WAVES), dim3(ACT_WAVES * 64),
+                     act_smem_bytes(sp), stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id);
 }
 
-__global__ __launch_bounds__(256) void act_bwd_ce_kernel(const float* __restrict__ dact, int ldd,
-                                                         const float* __restrict__ act, int lda,
-                                                         const float* __restrict__ logits, int ldl, SpanTables sp,
-                                                         const int* __restrict__ col, const int* __restrict__ opt,
-                                                         float* __restrict__ dl, int ldg, int rows, float inv_tau,
-                                                         float* loss) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)rows * sp.n_span) return;
-  const int r = (int)(idx / sp.n_span), s = (int)(idx % sp.n_span);
-  const int st = sp.start[s], w = sp.width[s];
-  const float* g = dact + (size_t)r * ldd + st;
-  const float* y = act + (size_t)r * lda + st;
-  float* d = dl + (size_t)r * ldg + st;
-  if (sp.kind[s] == 0) {
-    for (int i = 0; i < w; ++i) d[i] = g[i] * (1.f - y[i] * y[i]);
-    return;
+// backward of the activation + fused conditional cross-entropy, one wave per row
+__global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float* __restrict__ dact, int ldd,
+                                                                    const float* __restrict__ act, int lda,
+                                                                    const float* __restrict__ logits, int ldl,
+                                                                    SpanTables sp, const int* __restrict__ col,
+                                                                    const int* __restrict__ opt, float* __restrict__ dl,
+                                                                    int ldg, int rows, float inv_tau, float* loss) {
+  extern __shared__ float act_smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * ACT_WAVES + wv;
+  if (r >= rows) return;
+  const int D = sp.dim, S = sp.n_span;
+  float* gy = act_smem + (size_t)wv * (D + 2 * S);
+  float* stat = gy + D;
+  const float* g = dact + (size_t)r * ldd;
+  const float* y = act + (size_t)r * lda;
+  const float* x = logits + (size_t)r * ldl;
+  float* d = dl + (size_t)r * ldg;
+  __shared__ float ce_stat[ACT_WAVES][3];   // lse, span start, width of the conditioned span
+  if (lane == 0) { ce_stat[wv][0] = 0.f; ce_stat[wv][1] = 0.f; ce_stat[wv][2] = 0.f; }
+  for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const int cr = col[r];
+  for (int s = lane; s < S; s += 64) {
+    if (sp.kind[s] == 0) continue;
+    const int st = sp.start[s], w = sp.width[s];
+    float dot = 0.f;
+    for (int i = 0; i < w; ++i) dot += gy[st + i];
+    stat[2 * s] = dot;
+    if (sp.cond_idx[s] == cr) {
+      float m = -INFINITY;
+      for (int i = 0; i < w; ++i) m = fmaxf(m, x[st + i]);
+      float sum = 0.f;
+      for (int i = 0; i < w; ++i) sum += __expf(x[st + i] - m);
+      const float lse = m + __logf(sum);
+      ce_stat[wv][0] = lse;
+      ce_stat[wv][1] = (float)st;
+      ce_stat[wv][2] = (float)w;
+      const int o = min(opt[r], w - 1);
+      atomicAdd(loss, (lse - x[st + o]) / (float)rows);
+    }
   }
-  float dot = 0.f;
-  for (int i = 0; i < w; ++i) dot += g[i] * y[i];
-  for (int i = 0; i < w; ++i) d[i] = y[i] * (g[i] - dot) * inv_tau;
-  const int ci = sp.cond_idx[s];
-  if (ci >= 0 && col[r] == ci) {
-    const float* x = logits + (size_t)r * ldl + st;
-    float mx = -INFINITY;
-    for (int i = 0; i < w; ++i) mx = fmaxf(mx, x[i]);
-    float sum = 0.f;
-    for (int i = 0; i < w; ++i) sum += __expf(x[i] - mx);
-    const float lse = mx + __logf(sum);
-    const int o = min(opt[r], w - 1);
-    const float invB = 1.f / (float)rows;
-    for (int i = 0; i < w; ++i) d[i] += (__expf(x[i] - lse) - (i == o ? 1.f : 0.f)) * invB;
-    atomicAdd(loss, (lse - x[o]) * invB);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const float lse = ce_stat[wv][0];
+  const int cst = (int)ce_stat[wv][1], cw = (int)ce_stat[wv][2];
+  const int ot = cst + min(opt[r], max(cw - 1, 0));
+  const float invB = 1.f / (float)rows;
+  for (int j = lane; j < D; j += 64) {
+    const int s = sp.elem_span[j];
+    float v;
+    if (sp.kind[s] == 0) {
+      const float yy = y[j];
+      v = g[j] * (1.f - yy * yy);
+    } else {
+      v = y[j] * (g[j] - stat[2 * s]) * inv_tau;
+      if (j >= cst && j < cst + cw) v += (__expf(x[j] - lse) - (j == ot ? 1.f : 0.f)) * invB;
+    }
+    d[j] = v;
   }
 }
 
 void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, const float* logits, int ldl, SpanTables sp,
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
                        hipStream_t stream) {
-  const int64_t n = (int64_t)rows * sp.n_span;
-  if (n == 0) return;
-  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, dact, ldd, act, lda,
-                     logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss);
+  if (rows == 0) return;
+  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + ACT_WAVES - 1) / ACT_WAVES), dim3(ACT_WAVES * 64),
+                     act_smem_bytes(sp), stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
+                     1.f / tau, loss);
 }
 
 // ============================================================================ gradient penalty pieces
@@ -257,9 +309,15 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
   __shared__ float sh[8];
   const int r = blockIdx.x;
   const float* x = g + (size_t)r * ldg;
-  float s = 0.f;
-  for (int i = threadIdx.x; i < cols; i += blockDim.x) s += x[i] * x[i];
-  s = block_sum(s, sh);
+  float s0 = 0.f, s1 = 0.f;
+  int i = threadIdx.x;
+  for (; i + (int)blockDim.x < cols; i += 2 * blockDim.x) {
+    const float u = x[i], w = x[i + blockDim.x];
+    s0 += u * u;
+    s1 += w * w;
+  }
+  if (i < cols) s0 += x[i] * x[i];
+  const float s = block_sum(s0 + s1, sh);
   const float n = sqrtf(s);
   const float coef = lam * 2.f * (n - 1.f) / (fmaxf(n, 1e-30f) * (float)rows);
   float* o = out + (size_t)r * ldo;
@@ -350,8 +408,12 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
 }
 
 // ============================================================================ batch norm + relu
-constexpr int BN_COLS = 32, BN_GROUPS = 16, BN_MAXR = 64;   // rows per thread kept in registers: rows <= 1024
+// One workgroup owns BN_COLS columns; its BN_GROUPS row-groups keep up to MAXR rows per thread in
+// registers, so statistics, normalisation and the backward need a single pass over global memory.
+// Loads use clamped (always valid) addresses and are masked afterwards (no predicated loads).
+constexpr int BN_COLS = 16, BN_GROUPS = 32;
 
+template <int MAXR>
 __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
@@ -362,12 +424,14 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
   const int lc = threadIdx.x % BN_COLS, grp = threadIdx.x / BN_COLS;
   const int c = blockIdx.x * BN_COLS + lc;
   const bool ok = c < cols;
-  float x[BN_MAXR];
+  const int cc = min(c, cols - 1);
+  float x[MAXR];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < BN_MAXR; ++i) {
+  for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
-    x[i] = (ok && r < rows) ? a[(size_t)r * lda + c] : 0.f;
+    const float v = a[(size_t)min(r, rows - 1) * lda + cc];
+    x[i] = (r < rows) ? v : 0.f;
     s += x[i];
   }
   red[grp][lc] = s;
@@ -381,7 +445,7 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
   const float mu = stat[0][lc];
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < BN_MAXR; ++i) {
+  for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
     const float d = (r < rows) ? x[i] - mu : 0.f;
     q += d * d;
@@ -405,7 +469,7 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
   if (!ok) return;
   const float is = stat[1][lc], gm = gamma[c], bt = beta[c];
 #pragma unroll
-  for (int i = 0; i < BN_MAXR; ++i) {
+  for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
     if (r < rows) {
       const float n = (x[i] - mu) * is;
@@ -419,10 +483,19 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           float momentum, float eps, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_relu_train_kernel, dim3((cols + BN_COLS - 1) / BN_COLS), dim3(BN_COLS * BN_GROUPS), 0, stream, a,
-                     lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, momentum, eps);
+  const dim3 grid((cols + BN_COLS - 1) / BN_COLS), block(BN_COLS * BN_GROUPS);
+  if (rows <= 8 * BN_GROUPS)
+    hipLaunchKernelGGL(bn_relu_train_kernel<8>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
+                       invstd, rm, rv, rows, cols, momentum, eps);
+  else if (rows <= 16 * BN_GROUPS)
+    hipLaunchKernelGGL(bn_relu_train_kernel<16>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
+                       invstd, rm, rv, rows, cols, momentum, eps);
+  else
+    hipLaunchKernelGGL(bn_relu_train_kernel<32>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
+                       invstd, rm, rv, rows, cols, momentum, eps);
 }
 
+template <int MAXR>
 __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
@@ -432,17 +505,19 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
   const int lc = threadIdx.x % BN_COLS, grp = threadIdx.x / BN_COLS;
   const int c = blockIdx.x * BN_COLS + lc;
   const bool ok = c < cols;
-  float dy[BN_MAXR], nh[BN_MAXR];
+  const int cc = min(c, cols - 1);
+  float dy[MAXR], nh[MAXR];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < BN_MAXR; ++i) {
+  for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
-    float d = 0.f, n = 0.f;
-    if (ok && r < rows) {
-      const float rr = r_[(size_t)r * ldr + c];
-      d = rr > 0.f ? dr[(size_t)r * lddr + c] : 0.f;
-      n = nhat[(size_t)r * ldn + c];
-    }
+    const size_t rr = (size_t)min(r, rows - 1);
+    const float rv = r_[rr * ldr + cc];
+    const float dv = dr[rr * lddr + cc];
+    const float nv = nhat[rr * ldn + cc];
+    const bool in = r < rows;
+    const float d = (in && rv > 0.f) ? dv : 0.f;
+    const float n = in ? nv : 0.f;
     dy[i] = d;
     nh[i] = n;
     s1 += d;
@@ -459,15 +534,14 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
     if (ok) { dbeta[c] = t1; dgamma[c] = t2; }
   }
   __syncthreads();
-  if (!ok) return;
   const float sdy = stat[0][lc], sdyn = stat[1][lc];
-  const float k = gamma[c] * invstd[c];
+  const float k = gamma[cc] * invstd[cc];
   const float invn = 1.f / (float)rows;
   float sda = 0.f;
 #pragma unroll
-  for (int i = 0; i < BN_MAXR; ++i) {
+  for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
-    if (r < rows) {
+    if (r < rows && ok) {
       const float v = k * (dy[i] - sdy * invn - nh[i] * sdyn * invn);
       da[(size_t)r * ldda + c] = v;
       sda += v;
@@ -477,7 +551,7 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
     __syncthreads();
     red[0][grp][lc] = sda;
     __syncthreads();
-    if (grp == 0) {
+    if (grp == 0 && ok) {
       float t = 0.f;
       for (int i = 0; i < BN_GROUPS; ++i) t += red[0][i][lc];
       dbias[c] = t;
@@ -488,8 +562,16 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_relu_bwd_kernel, dim3((cols + BN_COLS - 1) / BN_COLS), dim3(BN_COLS * BN_GROUPS), 0, stream, dr,
-                     lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols);
+  const dim3 grid((cols + BN_COLS - 1) / BN_COLS), block(BN_COLS * BN_GROUPS);
+  if (rows <= 8 * BN_GROUPS)
+    hipLaunchKernelGGL(bn_relu_bwd_kernel<8>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
+                       ldda, dgamma, dbeta, dbias, rows, cols);
+  else if (rows <= 16 * BN_GROUPS)
+    hipLaunchKernelGGL(bn_relu_bwd_kernel<16>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
+                       ldda, dgamma, dbeta, dbias, rows, cols);
+  else
+    hipLaunchKernelGGL(bn_relu_bwd_kernel<32>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
+                       ldda, dgamma, dbeta, dbias, rows, cols);
 }
 
 // ============================================================================ Adam

@@ -59,7 +59,12 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
 template <bool ROWMAJ>
 __device__ __forceinline__ void load_tile(float (&v)[8], const float* __restrict__ p, int ld, int r0, int rmax, int k0,
                                           int kmax) {
+  // Every load is issued unconditionally from a clamped (always valid) address and the
+  // out-of-range lanes are zeroed afterwards: a predicated load would make hipcc branch
+  // around each one and wait vmcnt(0) per element (8 serial round trips per operand).
   const int t = threadIdx.x;
+  float x[8];
+  bool ok[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int r, k;
@@ -70,13 +75,15 @@ __device__ __forceinline__ void load_tile(float (&v)[8], const float* __restrict
       r = r0 + t % 64;
       k = k0 + 2 * (t / 64 + 4 * i);
     }
-    const bool rok = r < rmax;
-    float x0 = 0.f, x1 = 0.f;
-    if (rok && k < kmax) x0 = ROWMAJ ? p[(size_t)r * ld + k] : p[(size_t)k * ld + r];
-    if (rok && k + 1 < kmax) x1 = ROWMAJ ? p[(size_t)r * ld + k + 1] : p[(size_t)(k + 1) * ld + r];
-    v[2 * i] = x0;
-    v[2 * i + 1] = x1;
+    const int rc = min(r, rmax - 1);
+    const int kc0 = min(k, kmax - 1), kc1 = min(k + 1, kmax - 1);
+    x[2 * i] = ROWMAJ ? p[(size_t)rc * ld + kc0] : p[(size_t)kc0 * ld + rc];
+    x[2 * i + 1] = ROWMAJ ? p[(size_t)rc * ld + kc1] : p[(size_t)kc1 * ld + rc];
+    ok[2 * i] = r < rmax && k < kmax;
+    ok[2 * i + 1] = r < rmax && k + 1 < kmax;
   }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = ok[i] ? x[i] : 0.f;
 }
 
 template <bool ROWMAJ>
@@ -225,9 +232,17 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(idx / g.N), n = (int)(idx % g.N);
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += g.ws[(size_t)z * total + idx];
-    float v = g.alpha * s;
+    // independent partial sums so the slab loads are in flight together
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int z = 0;
+    for (; z + 4 <= splits; z += 4) {
+      s0 += g.ws[(size_t)z * total + idx];
+      s1 += g.ws[(size_t)(z + 1) * total + idx];
+      s2 += g.ws[(size_t)(z + 2) * total + idx];
+      s3 += g.ws[(size_t)(z + 3) * total + idx];
+    }
+    for (; z < splits; ++z) s0 += g.ws[(size_t)z * total + idx];
+    float v = g.alpha * ((s0 + s1) + (s2 + s3));
     float* cp = g.c + (size_t)m * g.ldc + n;
     if (g.beta != 0.f) v += g.beta * (*cp);
     if (g.bias) v += g.bias[n];

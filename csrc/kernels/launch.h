@@ -68,7 +68,9 @@ struct SpanTables {
   const int* width;
   const int* kind;      // 0 tanh, 1 softmax
   const int* cond_idx;  // softmax span -> conditional column index (or -1)
+  const int* elem_span; // data column -> span index
   int n_span;
+  int dim;              // data_dim (sum of widths)
 };
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,

@@ -25,11 +25,19 @@ TILE = 64
 
 
 def _splitk(M: int, N: int, K: int) -> int:
+    """Split-K factor: aim for ~384 workgroups with >= 128-deep K slices.
+
+    One workgroup can only pull ~60-100 GB/s from L2 / Infinity Cache, so a GEMM with few
+    output tiles must spread its K range over many CUs; the partial slabs cost
+    splits * M * N * 4 bytes of extra traffic, capped here at ~6 MB.
+    """
     tiles = ((M + TILE - 1) // TILE) * ((N + TILE - 1) // TILE)
-    if K < 512 or tiles >= 160:
+    if K < 256 or tiles >= 256:
         return 1
-    want = max(1, round(256 / tiles))
-    return int(max(1, min(want, K // 128)))
+    want = -(-384 // tiles)
+    cap_k = max(1, K // 128)
+    cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
+    return int(max(1, min(want, cap_k, cap_ws)))
 
 
 class HipOps:
@@ -69,8 +77,12 @@ class HipOps:
                     ci += 1
                 else:
                     cidx.append(-1)
+            elem = []
+            for i, (s, w, k) in enumerate(spans):
+                elem.extend([i] * w)
             mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
-            t = (mk([s for s, _, _ in spans]), mk([w for _, w, _ in spans]), mk([k for _, _, k in spans]), mk(cidx))
+            t = (mk([s for s, _, _ in spans]), mk([w for _, w, _ in spans]), mk([k for _, _, k in spans]), mk(cidx),
+                 mk(elem))
             self._spans[key] = t
         return t
 
@@ -129,12 +141,12 @@ class HipOps:
 
     # ------------------------------------------------------------------ activations
     def activate(self, logits, out, spans, tau=0.2, stream_id=0):
-        st, w, k, ci = self._span_tables(spans)
-        self.L.activate(logits, out, st, w, k, ci, float(tau), self.seed, self.ctr, int(stream_id) * 16)
+        st, w, k, ci, el = self._span_tables(spans)
+        self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16)
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
-        st, w, k, ci = self._span_tables(spans, cond_spans)
-        self.L.act_bwd_ce(dact, act, logits, st, w, k, ci, col, opt, dlogits, loss_out, float(tau))
+        st, w, k, ci, el = self._span_tables(spans, cond_spans)
+        self.L.act_bwd_ce(dact, act, logits, st, w, k, ci, el, col, opt, dlogits, loss_out, float(tau))
 
     # ------------------------------------------------------------------ gradient penalty
     def slerp(self, real, fake, out, stream_id=0):
