@@ -124,5 +124,5 @@ def test_hip_g_update_matches_autograd(precision):
     gsd = dict(G.named_parameters())
     for k, n in eng.g_key_map():
         if k in gsd and not k.endswith("fc.bias"):
-            tol = 5e-2 if precision == "bf16" else 5e-3
+            tol = 8e-2 if precision == "bf16" else 5e-3
             assert _rel(eng.g[n], gsd[k].grad) < tol, (k, _rel(eng.g[n], gsd[k].grad))

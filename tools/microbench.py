@@ -1,0 +1,86 @@
+"""Per-op device cost inside hipGraphs: capture N back-to-back calls of one op, replay, time.
+
+Reports microseconds per call (including the kernel-boundary cost inside a graph), which is
+what a captured training step actually pays per launch.
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+
+
+def per_call(fn, dev, n=50, reps=20):
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            fn()
+    g.replay()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t) / (reps * n) * 1e6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="bf16")
+    args = ap.parse_args()
+    from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+    from helpers import small_table
+    dev = torch.device("cuda:0")
+    _, _, _, _, _, _, tr, X = small_table(40000, 0)
+    eng = CTGANEngine(tr.layout, EngineConfig(precision=args.precision), dev, backend="hip", seed=1)
+    eng.set_training_data(X)
+    o = eng.ops
+    nP, B = eng.nP, eng.B
+    res = {}
+    res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
+    shapes = {
+        "G0 fwd 500x256x(E+C) NT": (eng.H[:, eng.off[0]:], eng.p["G.0.W"], eng.abuf[0], False, True),
+        "G1 fwd 500x256x(E+C+256) NT": (eng.H[:, eng.off[1]:], eng.p["G.1.W"], eng.abuf[1], False, True),
+        "Gout fwd 500xDdxHw NT": (eng.H, eng.p["G.out.W"], eng.logits, False, True),
+        "D0 fwd 150x256xK1 NT": (eng.X, eng.p["D.0.W"], eng.dl[0], False, True),
+        "D1 fwd 150x256x256 NT": (eng.dl[0], eng.p["D.1.W"], eng.dl[1], False, True),
+        "A chain 150x256x256 NN": (eng.A[1], eng.p["D.1.W"], eng.A[0], False, False),
+        "gp g 50xK1x256 NN": (eng.A[0][:nP], eng.p["D.0.W"], eng.gbuf, False, False),
+        "dV0 256xK1x150 TN": (eng.A[0], eng.X, eng.g["D.0.W"], True, False),
+        "dWout DdxHwx500 TN": (eng.dlogits, eng.H, eng.g["G.out.W"], True, False),
+        "dH 500x512xDd NN": (eng.dlogits, eng.p["G.out.W"][:, :eng.off[0]], eng.dH[:, :eng.off[0]], False, False),
+    }
+    for name, (a, b, c, ta, tb) in shapes.items():
+        res[name] = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
+    t = eng.tables
+    res["sample_train D"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B],
+                                                            eng.Xd[B:2 * B], eng.Dd, eng.col, eng.opt), dev)
+    res["sample_train G"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B], None,
+                                                            eng.Dd, eng.col, eng.opt), dev)
+    res["activate"] = per_call(lambda: o.activate(eng.logits, eng.Xd[0:B, :eng.Dd], eng.spans), dev)
+    res["act_bwd_ce"] = per_call(lambda: o.act_bwd_ce(eng.gbuf.view(B, eng.Din)[:, :eng.Dd], eng.Xd[0:B, :eng.Dd],
+                                                      eng.logits, eng.spans, eng.cond_spans, eng.col, eng.opt,
+                                                      eng.dlogits, eng.metrics[3:4]), dev)
+    res["bn_relu_train"] = per_call(lambda: o.bn_relu_fwd(eng.abuf[0], eng.p["G.0.gamma"], eng.p["G.0.beta"],
+                                                          eng.H[:, eng.off[1]:eng.off[0]], eng.nhat[0], eng.bn_mean[0],
+                                                          eng.bn_invstd[0], eng.p["G.0.rm"], eng.p["G.0.rv"]), dev)
+    res["adam D"] = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8, 0.0),
+                             dev)
+    res["slerp"] = per_call(lambda: o.slerp(eng.Xd[B:2 * B], eng.Xd[0:B], eng.Xd[2 * B:3 * B]), dev)
+    res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[2 * nP:], 10.0, eng.metrics[1:2]), dev)
+    res["full step (graph)"] = per_call(eng._one_step, dev, n=5, reps=20)
+    for k, v in res.items():
+        print(f"{v:9.2f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
