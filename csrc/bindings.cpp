@@ -81,9 +81,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.splitk = (int)std::max<int64_t>(splitk, 1);
   if (g.splitk > 1) {
     TORCH_CHECK(ws.has_value() && ws->defined() && ws->scalar_type() == at::kFloat, "gemm: split-K needs ws");
-    int64_t kchunk = ((K + g.splitk - 1) / g.splitk + 31) / 32 * 32;
-    int64_t s_eff = (K + kchunk - 1) / kchunk;
-    TORCH_CHECK(ws->numel() >= s_eff * M * N, "gemm: workspace too small");
+    // the launcher rounds K slices up to whole bursts, so the effective split count never exceeds splitk
+    TORCH_CHECK(ws->numel() >= (int64_t)g.splitk * M * N, "gemm: workspace too small");
     g.ws = fp(*ws);
   }
   g.seed = (uint64_t)seed;
@@ -150,8 +149,10 @@ fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Ten
               "span tables must be int32");
   TORCH_CHECK(start.numel() == width.numel() && start.numel() == kind.numel() && start.numel() == cidx.numel(),
               "span tables: sizes");
-  return fedtgan::SpanTables{start.data_ptr<int>(), width.data_ptr<int>(), kind.data_ptr<int>(), cidx.data_ptr<int>(),
-                             elem.data_ptr<int>(), (int)start.numel(), (int)elem.numel()};
+  fedtgan::SpanTables sp{start.data_ptr<int>(), width.data_ptr<int>(), kind.data_ptr<int>(), cidx.data_ptr<int>(),
+                         elem.data_ptr<int>(), (int)start.numel(), (int)elem.numel()};
+  TORCH_CHECK(fedtgan::activation_smem_bytes(sp) <= 160 * 1024, "activation: row image exceeds the 160 KiB LDS");
+  return sp;
 }
 
 void activate(const Tensor& logits, const Tensor& out, const Tensor& start, const Tensor& width, const Tensor& kind,

@@ -53,8 +53,33 @@ __device__ __forceinline__ void draw_cond_wave(const SampleArgs& a, uint64_t ste
   opt = min(found, w - 1);
 }
 
+// Keyed pseudo-random permutation of [0, n): a 4-round Feistel network on the smallest even
+// number of bits covering n, with cycle walking.  Every thread evaluates perm(b) on its own --
+// no sort, no LDS, no barrier -- and a fresh key per step gives a fresh permutation.
+__device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint4 key) {
+  int bits = 2;
+  while ((1u << bits) < n) bits += 2;
+  const int h = bits / 2;
+  const uint32_t mask = (1u << h) - 1u;
+  const uint32_t ks[4] = {key.x, key.y, key.z, key.w};
+  do {
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      uint32_t f = (R ^ ks[r]) * 0x9E3779B1u;
+      f ^= f >> 15;
+      f *= 0x85EBCA77u;
+      f ^= f >> 13;
+      const uint32_t nl = R;
+      R = L ^ (f & mask);
+      L = nl;
+    }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
-  __shared__ uint64_t keys[MAX_PERM];
   const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (blockIdx.x == 0 && tid == 0) {
@@ -64,31 +89,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     }
   }
   const bool with_real = a.xr != nullptr && a.n_col > 0;
-  // ---- random permutation of the batch (identical in every workgroup: same Philox keys)
-  if (with_real) {
-    int p2 = 1;
-    while (p2 < a.B) p2 <<= 1;
-    RngArgs rk{a.seed, a.rng_ctr, a.rng_stream + 1u};
-    for (int i = tid; i < p2; i += blockDim.x) {
-      uint64_t k = ~0ull;
-      if (i < a.B) k = ((uint64_t)rng4(rk, step, (uint64_t)i).x << 32) | (uint64_t)i;
-      keys[i] = k;
-    }
-    __syncthreads();
-    for (int size = 2; size <= p2; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int i = tid; i < p2; i += blockDim.x) {
-          const int j = i ^ stride;
-          if (j > i) {
-            const bool up = (i & size) == 0;
-            const uint64_t ki = keys[i], kj = keys[j];
-            if ((ki > kj) == up) { keys[i] = kj; keys[j] = ki; }
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
+  RngArgs rk{a.seed, a.rng_ctr, a.rng_stream + 1u};
+  const uint4 pkey = rng4(rk, step, 0ull);
   RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
   RngArgs rp{a.seed, a.rng_ctr, a.rng_stream + 3u};
   for (int q = 0; q < SAMPLE_ROWS_PER_WAVE; ++q) {
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
     if (!with_real) continue;
     // real row drawn for the condition of fake row perm[b]
-    const int p = (int)(keys[b] & 0xffffffffu);
+    const int p = (int)feistel_perm((uint32_t)b, (uint32_t)a.B, pkey);
     int pc = 0, po = 0;
     draw_cond_wave(a, step, p, lane, pc, po);
     const int64_t cnt = a.row_cnt[(size_t)pc * a.maxw + po];
@@ -135,21 +137,53 @@ void launch_sample(const SampleArgs& a, hipStream_t stream) {
 }
 
 // ============================================================================ activation
-// One wave per row.  Element-parallel pass: Gumbel-perturbed logits (or tanh) into an LDS row
-// image; span-parallel pass: each lane reduces one softmax span (max, sum) from LDS;
-// element-parallel pass: normalise and store.
+// One wave per row; the span tables are staged in LDS once per workgroup (one memory round
+// trip), so the per-element work never chases a global pointer.
+//   element-parallel: Gumbel-perturbed logits (or tanh) into an LDS row image
+//   span-parallel   : one lane per softmax span reduces (max, sum) from LDS
+//   element-parallel: normalise and store
 constexpr int ACT_WAVES = 4;
+
+struct ActSmem {
+  int* elem;    // [D]  element -> span
+  int* kind;    // [S]
+  int* start;   // [S]
+  int* width;   // [S]
+  int* cidx;    // [S]
+  float* rows;  // [ACT_WAVES][D + 2S]
+};
+
+__device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float* smem) {
+  const int D = sp.dim, S = sp.n_span;
+  ActSmem t;
+  t.elem = reinterpret_cast<int*>(smem);
+  t.kind = t.elem + D;
+  t.start = t.kind + S;
+  t.width = t.start + S;
+  t.cidx = t.width + S;
+  t.rows = reinterpret_cast<float*>(t.cidx + S);
+  for (int i = threadIdx.x; i < D; i += blockDim.x) t.elem[i] = sp.elem_span[i];
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    t.kind[i] = sp.kind[i];
+    t.start[i] = sp.start[i];
+    t.width[i] = sp.width[i];
+    t.cidx[i] = sp.cond_idx[i];
+  }
+  __syncthreads();
+  return t;
+}
 
 __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* __restrict__ logits, int ldl,
                                                                   float* __restrict__ out, int ldo, int rows,
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
                                                                   const uint64_t* ctr, uint32_t stream_id) {
   extern __shared__ float act_smem[];
+  const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * ACT_WAVES + wv;
   if (r >= rows) return;
   const int D = sp.dim, S = sp.n_span;
-  float* v = act_smem + (size_t)wv * (D + 2 * S);
+  float* v = t.rows + (size_t)wv * (D + 2 * S);
   float* stat = v + D;
   const float* x = logits + (size_t)r * ldl;
   float* y = out + (size_t)r * ldo;
@@ -157,19 +191,15 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   RngArgs rng{seed, ctr, stream_id};
   const uint64_t base = (uint64_t)r << 20;
   for (int j = lane; j < D; j += 64) {
-    const int s = sp.elem_span[j];
     const float xv = x[j];
-    if (sp.kind[s] == 0) {
-      y[j] = tanhf(xv);
-    } else {
-      v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
-    }
+    if (t.kind[t.elem[j]] == 0) y[j] = tanhf(xv);
+    else v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
   }
-  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   for (int s = lane; s < S; s += 64) {
-    if (sp.kind[s] == 0) continue;
-    const int st = sp.start[s], w = sp.width[s];
+    if (t.kind[s] == 0) continue;
+    const int st = t.start[s], w = t.width[s];
     float m = -INFINITY;
     for (int i = 0; i < w; ++i) m = fmaxf(m, v[st + i]);
     float sum = 0.f;
@@ -177,15 +207,17 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
     stat[2 * s] = m;
     stat[2 * s + 1] = 1.f / sum;
   }
-  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   for (int j = lane; j < D; j += 64) {
-    const int s = sp.elem_span[j];
-    if (sp.kind[s] != 0) y[j] = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
+    const int s = t.elem[j];
+    if (t.kind[s] != 0) y[j] = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
   }
 }
 
-static size_t act_smem_bytes(const SpanTables& sp) { return (size_t)ACT_WAVES * (sp.dim + 2 * sp.n_span) * sizeof(float); }
+static size_t act_smem_bytes(const SpanTables& sp) {
+  return (size_t)(sp.dim + 4 * sp.n_span) * sizeof(int) + (size_t)ACT_WAVES * (sp.dim + 2 * sp.n_span) * sizeof(float);
+}
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream) {
@@ -202,51 +234,58 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
                                                                     int ldg, int rows, float inv_tau, float* loss) {
   extern __shared__ float act_smem[];
+  const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * ACT_WAVES + wv;
   if (r >= rows) return;
   const int D = sp.dim, S = sp.n_span;
-  float* gy = act_smem + (size_t)wv * (D + 2 * S);
+  float* gy = t.rows + (size_t)wv * (D + 2 * S);
   float* stat = gy + D;
   const float* g = dact + (size_t)r * ldd;
   const float* y = act + (size_t)r * lda;
   const float* x = logits + (size_t)r * ldl;
   float* d = dl + (size_t)r * ldg;
-  __shared__ float ce_stat[ACT_WAVES][3];   // lse, span start, width of the conditioned span
-  if (lane == 0) { ce_stat[wv][0] = 0.f; ce_stat[wv][1] = 0.f; ce_stat[wv][2] = 0.f; }
-  for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   const int cr = col[r];
+  const int orow = opt[r];
+  for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int ce_span = -1;
   for (int s = lane; s < S; s += 64) {
-    if (sp.kind[s] == 0) continue;
-    const int st = sp.start[s], w = sp.width[s];
+    if (t.kind[s] == 0) continue;
+    const int st = t.start[s], w = t.width[s];
     float dot = 0.f;
     for (int i = 0; i < w; ++i) dot += gy[st + i];
     stat[2 * s] = dot;
-    if (sp.cond_idx[s] == cr) {
-      float m = -INFINITY;
-      for (int i = 0; i < w; ++i) m = fmaxf(m, x[st + i]);
-      float sum = 0.f;
-      for (int i = 0; i < w; ++i) sum += __expf(x[st + i] - m);
-      const float lse = m + __logf(sum);
-      ce_stat[wv][0] = lse;
-      ce_stat[wv][1] = (float)st;
-      ce_stat[wv][2] = (float)w;
-      const int o = min(opt[r], w - 1);
-      atomicAdd(loss, (lse - x[st + o]) / (float)rows);
-    }
+    if (t.cidx[s] == cr) ce_span = s;
   }
-  __builtin_amdgcn_wave_barrier();
+  // the conditioned span of this row (exactly one lane found it): wave-parallel log-sum-exp
+  const unsigned long long who = __ballot(ce_span >= 0);
+  int cst = 0, cw = 0;
+  float lse = 0.f;
+  if (who) {
+    const int src = __ffsll((long long)who) - 1;
+    const int cs = __shfl(ce_span, src, 64);
+    cst = t.start[cs];
+    cw = t.width[cs];
+    float m = -INFINITY;
+    for (int i = lane; i < cw; i += 64) m = fmaxf(m, x[cst + i]);
+    m = wave_max(m);
+    float sm = 0.f;
+    for (int i = lane; i < cw; i += 64) sm += __expf(x[cst + i] - m);
+    sm = wave_sum(sm);
+    lse = m + __logf(sm);
+    const int o = min(orow, cw - 1);
+    if (lane == 0) atomicAdd(loss, (lse - x[cst + o]) / (float)rows);
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  const float lse = ce_stat[wv][0];
-  const int cst = (int)ce_stat[wv][1], cw = (int)ce_stat[wv][2];
-  const int ot = cst + min(opt[r], max(cw - 1, 0));
+  __builtin_amdgcn_wave_barrier();
+  const int ot = cst + min(orow, max(cw - 1, 0));
   const float invB = 1.f / (float)rows;
   for (int j = lane; j < D; j += 64) {
-    const int s = sp.elem_span[j];
+    const int s = t.elem[j];
     float v;
-    if (sp.kind[s] == 0) {
+    if (t.kind[s] == 0) {
       const float yy = y[j];
       v = g[j] * (1.f - yy * yy);
     } else {
@@ -265,6 +304,8 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
                      act_smem_bytes(sp), stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
                      1.f / tau, loss);
 }
+
+size_t activation_smem_bytes(const SpanTables& sp) { return act_smem_bytes(sp); }
 
 // ============================================================================ gradient penalty pieces
 // one wave per row

@@ -1,25 +1,32 @@
-// Generic skinny-GEMM for the CTGAN step on CDNA4 MFMA (bf16 operands, fp32 accumulate).
+// Generic skinny-GEMM for the CTGAN step on CDNA4 matrix cores.
 //
 //   C[M,N] = epi( alpha * op(A)[M,K] . op(B)[K,N] + beta * C + bias[N] )
 //
 // op(A) = A or A^T, op(B) = B or B^T, every operand with its own leading dimension so the
-// engine can pass column slices of its concat-free activation buffers (the generator's
+// engine passes column slices of its concat-free activation buffers (the generator's
 // residual stack, the packed PacGAN input) without copies.
 //
-// Tiling: 64x64 output tile per 256-thread workgroup (4 waves in a 2x2 grid, 32x32 per wave
-// = 2x2 v_mfma_f32_16x16x32_bf16 tiles), BK = 32.  Operands are read from fp32 global memory
-// with coalesced loads along their contiguous dimension, rounded to bf16 and staged in LDS as
-// [row][k] images (k contiguous, row stride padded to 40 elements = 80 B so each lane's
-// 16-byte fragment is a conflict-light ds_read_b128).  Two LDS buffers: the next k-tile's
-// global loads are issued before the current tile's MFMAs (register prefetch), so HBM /
-// Infinity-Cache latency hides under the compute of the previous tile.
-//
-// Split-K (gridDim.z > 1) writes fp32 partial slabs that `gemm_splitk_epilogue` reduces and
-// finishes; with gridDim.z == 1 the epilogue is fused.  Epilogues:
+// The step's GEMMs are small (M <= 500, N <= ~6k, K <= ~6k): what costs is memory latency,
+// not FLOPs.  Hence:
+//   * 64x64 output tile per 256-thread workgroup (4 waves in a 2x2 grid, 32x32 per wave);
+//   * the workgroup's whole K-chunk (KC = 128 bf16 / 64 fp32) is fetched in ONE burst --
+//     every thread issues all of its loads back to back from clamped, always-valid
+//     addresses (no predicated loads, which hipcc would serialise with vmcnt(0) each) -- so
+//     a chunk costs one memory round trip, and the next chunk's burst is in flight while the
+//     current one is multiplied out of LDS;
+//   * operands are rounded to bf16 once, while staging into [row][k] LDS images (row stride
+//     KC+8 elements: every 16-lane ds_read_b128 group lands on distinct banks), then
+//     v_mfma_f32_16x16x32_bf16 with fp32 accumulation; or, with g.f32, kept in fp32 and fed
+//     to v_mfma_f32_16x16x4_f32 (exact fp32, same numerics as an fmaf chain);
+//   * split-K over gridDim.z spreads a K-heavy GEMM with few output tiles over many CUs
+//     (one CU alone pulls only ~60-100 GB/s); fp32 partial slabs are reduced by
+//     `gemm_splitk_epilogue`, which also applies the epilogue; with one split it is fused.
+// Epilogues:
 //   EPI_NONE            out = v
 //   EPI_LRELU_DROPOUT   out = lrelu(v) * keep/(1-p);  ms = lrelu'(v) * keep/(1-p)   (Philox mask)
 //   EPI_MASK            out = v * ms
 //   EPI_RELU            out = max(v, 0)
+//   EPI_BN_EVAL_RELU    out = relu((v - rm) * rsqrt(rv + eps) * gamma + beta)   (eval BatchNorm)
 #include <algorithm>
 
 #include "common.h"
@@ -30,7 +37,7 @@ namespace fedtgan {
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int BM = 64, BN = 64, BK = 32, KPAD = 40, NT = 256;
+constexpr int BM = 64, BN = 64, NT = 256;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
   const int epi = g.epi;
@@ -53,80 +60,84 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
   return v;
 }
 
-// Stage a BM(or BN) x BK tile of an operand into registers (8 fp32 values per thread).
-//   ROWMAJ: element (r, k) at p[r*ld + k] (k contiguous)   -> thread: kp = t%16, r = t/16 + 16*i
-//   else  : element (r, k) at p[k*ld + r] (r contiguous)   -> thread: r = t%64, kp = t/64 + 4*i
-template <bool ROWMAJ>
-__device__ __forceinline__ void load_tile(float (&v)[8], const float* __restrict__ p, int ld, int r0, int rmax, int k0,
-                                          int kmax) {
-  // Every load is issued unconditionally from a clamped (always valid) address and the
-  // out-of-range lanes are zeroed afterwards: a predicated load would make hipcc branch
-  // around each one and wait vmcnt(0) per element (8 serial round trips per operand).
-  const int t = threadIdx.x;
-  float x[8];
-  bool ok[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r, k;
+// ----------------------------------------------------------------------------- chunk staging
+// A chunk is R=64 rows x KC k-values of one operand.  Thread mapping (NPT = KC/8 pairs each):
+//   ROWMAJ (k contiguous in memory):  pair column kp = t % (KC/2), row = t / (KC/2) + (NT/(KC/2)) * i
+//   else   (row contiguous):          row = t % 64,                kp  = t / 64 + (NT/64) * i
+template <int KC, bool ROWMAJ>
+struct Chunk {
+  static constexpr int NPAIR = KC / 8;  // (64 * KC / 2) / 256 pairs per thread
+  float x[2 * NPAIR];
+
+  __device__ __forceinline__ static void coords(int i, int& r, int& kp) {
+    const int t = threadIdx.x;
     if (ROWMAJ) {
-      r = r0 + t / 16 + 16 * i;
-      k = k0 + 2 * (t % 16);
+      r = t / (KC / 2) + (NT / (KC / 2)) * i;
+      kp = t % (KC / 2);
     } else {
-      r = r0 + t % 64;
-      k = k0 + 2 * (t / 64 + 4 * i);
+      r = t % 64;
+      kp = t / 64 + (NT / 64) * i;
     }
-    const int rc = min(r, rmax - 1);
-    const int kc0 = min(k, kmax - 1), kc1 = min(k + 1, kmax - 1);
-    x[2 * i] = ROWMAJ ? p[(size_t)rc * ld + kc0] : p[(size_t)kc0 * ld + rc];
-    x[2 * i + 1] = ROWMAJ ? p[(size_t)rc * ld + kc1] : p[(size_t)kc1 * ld + rc];
-    ok[2 * i] = r < rmax && k < kmax;
-    ok[2 * i + 1] = r < rmax && k + 1 < kmax;
   }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = ok[i] ? x[i] : 0.f;
-}
 
-template <bool ROWMAJ>
-__device__ __forceinline__ void tile_coords(int i, int& r, int& kp) {
-  const int t = threadIdx.x;
-  if (ROWMAJ) {
-    r = t / 16 + 16 * i;
-    kp = t % 16;
-  } else {
-    r = t % 64;
-    kp = t / 64 + 4 * i;
-  }
-}
-
-// bf16 image: [row][KPAD] (k contiguous), two k per 32-bit store
-template <bool ROWMAJ>
-__device__ __forceinline__ void store_tile(uint16_t* s, const float (&v)[8]) {
+  __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0, int rmax, int k0, int kmax) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r, kp;
-    tile_coords<ROWMAJ>(i, r, kp);
-    *reinterpret_cast<uint32_t*>(&s[r * KPAD + 2 * kp]) = pack_bf16x2(v[2 * i], v[2 * i + 1]);
-  }
-}
-
-// fp32 image: [row][KPADF]; odd stride keeps the 16 rows a 16x16x4 fragment reads on distinct banks
-constexpr int KPADF = 33;
-template <bool ROWMAJ>
-__device__ __forceinline__ void store_tile_f32(float* s, const float (&v)[8]) {
+    for (int i = 0; i < NPAIR; ++i) {
+      int r, kp;
+      coords(i, r, kp);
+      r += r0;
+      const int k = k0 + 2 * kp;
+      const int rc = min(r, rmax - 1);
+      const int kc0 = min(k, kmax - 1), kc1 = min(k + 1, kmax - 1);
+      x[2 * i] = ROWMAJ ? p[(size_t)rc * ld + kc0] : p[(size_t)kc0 * ld + rc];
+      x[2 * i + 1] = ROWMAJ ? p[(size_t)rc * ld + kc1] : p[(size_t)kc1 * ld + rc];
+    }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int r, kp;
-    tile_coords<ROWMAJ>(i, r, kp);
-    s[r * KPADF + 2 * kp] = v[2 * i];
-    s[r * KPADF + 2 * kp + 1] = v[2 * i + 1];
+    for (int i = 0; i < NPAIR; ++i) {
+      int r, kp;
+      coords(i, r, kp);
+      r += r0;
+      const int k = k0 + 2 * kp;
+      if (!(r < rmax && k < kmax)) x[2 * i] = 0.f;
+      if (!(r < rmax && k + 1 < kmax)) x[2 * i + 1] = 0.f;
+    }
   }
-}
+
+  // bf16 image [row][KC + 8]
+  __device__ __forceinline__ void store_bf16(uint16_t* s) const {
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      int r, kp;
+      coords(i, r, kp);
+      *reinterpret_cast<uint32_t*>(&s[r * (KC + 8) + 2 * kp]) = pack_bf16x2(x[2 * i], x[2 * i + 1]);
+    }
+  }
+
+  // fp32 image [row][KC + 1]
+  __device__ __forceinline__ void store_f32(float* s) const {
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      int r, kp;
+      coords(i, r, kp);
+      s[r * (KC + 1) + 2 * kp] = x[2 * i];
+      s[r * (KC + 1) + 2 * kp + 1] = x[2 * i + 1];
+    }
+  }
+};
+
+template <bool F32>
+struct Cfg {
+  static constexpr int KC = F32 ? 64 : 128;
+  static constexpr int LD = F32 ? KC + 1 : KC + 8;            // LDS row stride (elements)
+  static constexpr int ESZ = F32 ? 4 : 2;
+  static constexpr int STAGE = (BM + BN) * LD * ESZ;          // bytes per stage (A image + B image)
+};
 
 template <bool TA, bool TB, bool F32>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
-  // one LDS array (two stages of A and B); bf16 mode uses the first half of it
-  constexpr int STAGE = F32 ? (BM + BN) * KPADF * 4 : (BM + BN) * KPAD * 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+  using C = Cfg<F32>;
+  constexpr int KC = C::KC;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::STAGE];
 
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int kb = blockIdx.z * g.kchunk;
@@ -140,44 +151,46 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto stage_store = [&](int st, const float (&ra)[8], const float (&rb)[8]) {
-    unsigned char* base = smem + st * STAGE;
+  // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> staged [m][k]; k-contiguous in memory iff !TA
+  // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged [n][k]; k-contiguous in memory iff TB
+  Chunk<KC, !TA> ca;
+  Chunk<KC, TB> cb;
+  auto stage = [&](int st) {
+    unsigned char* base = smem + st * C::STAGE;
     if constexpr (F32) {
-      store_tile_f32<!TA>(reinterpret_cast<float*>(base), ra);
-      store_tile_f32<TB>(reinterpret_cast<float*>(base) + BM * KPADF, rb);
+      ca.store_f32(reinterpret_cast<float*>(base));
+      cb.store_f32(reinterpret_cast<float*>(base) + BM * C::LD);
     } else {
-      store_tile<!TA>(reinterpret_cast<uint16_t*>(base), ra);
-      store_tile<TB>(reinterpret_cast<uint16_t*>(base) + BM * KPAD, rb);
+      ca.store_bf16(reinterpret_cast<uint16_t*>(base));
+      cb.store_bf16(reinterpret_cast<uint16_t*>(base) + BM * C::LD);
     }
   };
 
-  // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> row-major in k iff !TA
-  // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged as [n][k]; row-major in k iff TB
-  float ra[8], rb[8];
   int buf = 0;
   if (kb < ke) {
-    load_tile<!TA>(ra, g.a, g.lda, m0, g.M, kb, ke);
-    load_tile<TB>(rb, g.b, g.ldb, n0, g.N, kb, ke);
-    stage_store(0, ra, rb);
+    ca.load(g.a, g.lda, m0, g.M, kb, ke);
+    cb.load(g.b, g.ldb, n0, g.N, kb, ke);
+    stage(0);
   }
   __syncthreads();
-  for (int k0 = kb; k0 < ke; k0 += BK) {
-    const bool more = k0 + BK < ke;
-    if (more) {
-      load_tile<!TA>(ra, g.a, g.lda, m0, g.M, k0 + BK, ke);
-      load_tile<TB>(rb, g.b, g.ldb, n0, g.N, k0 + BK, ke);
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+    const bool more = k0 + KC < ke;
+    if (more) {  // next burst in flight while this chunk is multiplied
+      ca.load(g.a, g.lda, m0, g.M, k0 + KC, ke);
+      cb.load(g.b, g.ldb, n0, g.N, k0 + KC, ke);
     }
+    const int kvalid = min(KC, ke - k0);
     if constexpr (F32) {
-      const float* A = reinterpret_cast<const float*>(smem + buf * STAGE);
-      const float* B = A + BM * KPADF;
-#pragma unroll
-      for (int s4 = 0; s4 < BK / 4; ++s4) {
+      const float* A = reinterpret_cast<const float*>(smem + buf * C::STAGE);
+      const float* B = A + BM * C::LD;
+      const int nsteps = (kvalid + 3) / 4;
+      for (int s4 = 0; s4 < nsteps; ++s4) {
         const int kk = 4 * s4 + (lane >> 4);
         float af[2], bfv[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          af[i] = A[(wm * 32 + i * 16 + (lane & 15)) * KPADF + kk];
-          bfv[i] = B[(wn * 32 + i * 16 + (lane & 15)) * KPADF + kk];
+          af[i] = A[(wm * 32 + i * 16 + (lane & 15)) * C::LD + kk];
+          bfv[i] = B[(wn * 32 + i * 16 + (lane & 15)) * C::LD + kk];
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -185,20 +198,23 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
     } else {
-      const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + buf * STAGE);
-      const uint16_t* B = A + BM * KPAD;
-      bf16x8 af[2], bfr[2];
+      const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + buf * C::STAGE);
+      const uint16_t* B = A + BM * C::LD;
+      const int nsteps = (kvalid + 31) / 32;
+      for (int s = 0; s < nsteps; ++s) {
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
-        bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * KPAD + 8 * (lane >> 4)]);
+        for (int i = 0; i < 2; ++i) {
+          af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
+          bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) stage_store(buf ^ 1, ra, rb);
+    if (more) stage(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
@@ -250,23 +266,18 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
   }
 }
 
+int gemm_kc(int f32) { return f32 ? Cfg<true>::KC : Cfg<false>::KC; }
+
 void launch_gemm(GemmArgs g, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0) return;
+  const int KC = gemm_kc(g.f32);
   const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
-  if (g.splitk < 1) g.splitk = 1;
-  if (g.K <= 0) g.splitk = 1;
-  int kchunk = (g.K + g.splitk - 1) / g.splitk;
-  kchunk = ((kchunk + BK - 1) / BK) * BK;
-  if (kchunk <= 0) kchunk = BK;
-  g.splitk = (g.K + kchunk - 1) / kchunk;
-  if (g.splitk < 1) g.splitk = 1;
+  if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
+  int kchunk = (std::max(g.K, 1) + g.splitk - 1) / g.splitk;
+  kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
+  g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
   g.kchunk = kchunk;
   dim3 grid(tn, tm, g.splitk), block(NT);
-  if (g.splitk > 1 && g.ws == nullptr) {
-    g.splitk = 1;
-    g.kchunk = g.K;
-    grid.z = 1;
-  }
 #define FEDTGAN_GEMM_DISPATCH(F)                                                                         \
   if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F>), grid, block, 0, stream, g);       \
   else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F>), grid, block, 0, stream, g); \

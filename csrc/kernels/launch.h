@@ -73,6 +73,8 @@ struct SpanTables {
   int dim;              // data_dim (sum of widths)
 };
 
+size_t activation_smem_bytes(const SpanTables& sp);   // dynamic LDS of the activation kernels
+
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
 

@@ -24,20 +24,20 @@ EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 
 TILE = 64
 
 
-def _splitk(M: int, N: int, K: int) -> int:
-    """Split-K factor: aim for ~384 workgroups with >= 128-deep K slices.
+def _splitk(M: int, N: int, K: int, kc: int = 128) -> int:
+    """Split-K factor for the burst GEMM (one K-burst = ``kc`` values per operand row).
 
-    One workgroup can only pull ~60-100 GB/s from L2 / Infinity Cache, so a GEMM with few
-    output tiles must spread its K range over many CUs; the partial slabs cost
-    splits * M * N * 4 bytes of extra traffic, capped here at ~6 MB.
+    One workgroup only pulls ~60-100 GB/s from L2 / Infinity Cache, so a GEMM with few output
+    tiles spreads its K range over many CUs: aim for ~256-384 workgroups, at most ~2 bursts per
+    split, and cap the fp32 partial slabs (splits * M * N * 4 B) at ~6 MB.
     """
     tiles = ((M + TILE - 1) // TILE) * ((N + TILE - 1) // TILE)
-    if K < 256 or tiles >= 256:
+    bursts = -(-K // kc)
+    if bursts <= 1 or tiles >= 256:
         return 1
-    want = -(-384 // tiles)
-    cap_k = max(1, K // 128)
+    want = max(-(-320 // tiles), -(-bursts // 2))
     cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
-    return int(max(1, min(want, cap_k, cap_ws)))
+    return int(max(1, min(want, bursts, cap_ws)))
 
 
 class HipOps:
@@ -92,12 +92,10 @@ class HipOps:
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
-        sk = _splitk(M, N, K)
+        sk = _splitk(M, N, K, 64 if self.f32 else 128)
         ws = None
         if sk > 1:
-            kchunk = ((K + sk - 1) // sk + 31) // 32 * 32
-            s_eff = (K + kchunk - 1) // kchunk
-            ws = self._workspace(s_eff * M * N)
+            ws = self._workspace(sk * M * N)
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
