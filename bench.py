@@ -98,7 +98,8 @@ def main():
             "metric": "sec_per_epoch", "value": round(sec_per_epoch, 6), "unit": "s/epoch", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(sec_per_epoch * 1000.0, 3),
             "higher_is_better": False, "scaling": "weak",
-            "vs_baseline": round(sec_per_epoch / BASELINE_SEC_PER_EPOCH, 6), "dtype": "fp32",
+            "vs_baseline": round(sec_per_epoch / BASELINE_SEC_PER_EPOCH, 6),
+            "dtype": cfg.engine.precision if rt.engine.ops.name == "hip" else "fp32",
             "data": "synthetic (Intrusion schema, 40000 rows per client)",
             "config": {"model": "Fed-TGAN CTGAN (G 256x256 residual+BN, D 256x256 pack10, WGAN-GP slerp)",
                        "global_batch": 500 * world, "seq_len": None, "parallelism": f"fed{world}",

@@ -55,15 +55,19 @@ __device__ __forceinline__ double u01d(uint32_t a, uint32_t b) {
   return ((double)v + 0.5) * (1.0 / 9007199254740992.0);
 }
 
+// NOTE: the fast __logf is not monotone-safe next to 1.0 (it can return +0 or a tiny positive
+// value for u = 1 - 2^-25), which would turn -log(u) into <= 0 and poison Box-Muller / Gumbel
+// with NaN.  The accurate logf is used for log(u) and the results are clamped.
+__device__ __forceinline__ float neg_log_u(uint32_t x) { return fmaxf(-logf(u01(x)), 1e-30f); }
+
 __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
-  float u1 = u01(a), u2 = u01(b);
-  float r = sqrtf(-2.0f * __logf(u1));
+  const float r = sqrtf(2.0f * neg_log_u(a));
   float s, c;
-  __sincosf(6.283185307179586f * u2, &s, &c);
+  __sincosf(6.283185307179586f * u01(b), &s, &c);
   return make_float2(r * c, r * s);
 }
 
-__device__ __forceinline__ float gumbel(uint32_t x) { return -__logf(-__logf(u01(x))); }
+__device__ __forceinline__ float gumbel(uint32_t x) { return -logf(neg_log_u(x)); }
 
 // round-to-nearest-even fp32 -> bf16 bits
 __device__ __forceinline__ uint16_t f2bf(float f) {
