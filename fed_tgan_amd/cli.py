@@ -1,0 +1,180 @@
+"""Command-line entry point, flag-compatible with the reference ``python -m dtds.distributed``.
+
+Reference flags (`Server/dtds/distributed.py:895-934`, `R/README.md:10-23`) keep their meaning:
+
+    -rank R            this process' rank; 0 = federator, 1..K = clients (world_size = K + 1)
+    -ip / -port        rendezvous address of the federator (default 127.0.0.1:7788)
+    -world_size W      clients + 1
+    -epochs / -epoch   federated rounds
+    -datapath P        each client's local CSV ('{client}' / '{rank}' are substituted);
+                       a missing file means "generate a synthetic shard of the dataset schema"
+    -name -E_interval -report -problem_type -target_column -selected_variables
+    -categorical_list -nonnegative_list -date_dic
+    (list flags take comma-separated values; -date_dic takes JSON)
+
+Without ``-rank`` the whole federation is launched locally (the reference's intended but broken
+``mp.spawn`` path, `Server/dtds/distributed.py:956-971`): one federator + (world_size-1) clients,
+or with ``-colocated`` one process per client where rank 0 is also the federator (the MI355X
+layout: one process per GPU, RCCL data plane).
+
+New flags: -config (dataset spec JSON or builtin name), -backend {auto,hip,torch},
+-precision {bf16,fp32}, -data_backend {auto,gloo,nccl}, -synthetic_rows, -shard
+{independent,iid,dirichlet,skew}, -alpha, -n_sample, -aggregation {weighted,uniform}, -gmm
+{torch,sklearn}, -seed, -out_dir, -ckpt_every, -resume, -local_clients (single-process
+multi-client emulation), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan}.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+from typing import List, Optional
+
+import torch
+
+from .data.schema import DatasetSpec, get_spec
+
+
+def _csv_list(s: str) -> List[str]:
+    return [x.strip() for x in s.split(",") if x.strip()]
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="python -m dtds.distributed", allow_abbrev=True,
+                                description="Federated CTGAN (Fed-TGAN) on MI355X")
+    p.add_argument("-rank", type=int, default=None)
+    p.add_argument("-ip", type=str, default="127.0.0.1")
+    p.add_argument("-port", type=int, default=7788)
+    p.add_argument("-name", type=str, default=None)
+    p.add_argument("-datapath", type=str, default="data/raw/Intrusion_train.csv")
+    p.add_argument("-epochs", type=int, default=10)
+    p.add_argument("-E_interval", type=int, default=1)
+    p.add_argument("-world_size", type=int, default=2)
+    p.add_argument("-report", action="store_true")
+    p.add_argument("-problem_type", type=str, default=None)
+    p.add_argument("-target_column", type=str, default=None)
+    p.add_argument("-selected_variables", type=_csv_list, default=None)
+    p.add_argument("-categorical_list", type=_csv_list, default=None)
+    p.add_argument("-nonnegative_list", type=_csv_list, default=None)
+    p.add_argument("-date_dic", type=json.loads, default=None)
+    # new
+    p.add_argument("-config", type=str, default="intrusion")
+    p.add_argument("-colocated", action="store_true")
+    p.add_argument("-backend", type=str, default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("-precision", type=str, default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("-data_backend", type=str, default="auto", choices=["auto", "gloo", "nccl"])
+    p.add_argument("-synthetic_rows", type=int, default=40000)
+    p.add_argument("-shard", type=str, default="independent", choices=["independent", "iid", "dirichlet", "skew"])
+    p.add_argument("-alpha", type=float, default=0.5)
+    p.add_argument("-n_sample", type=int, default=None)
+    p.add_argument("-aggregation", type=str, default="weighted", choices=["weighted", "uniform"])
+    p.add_argument("-gmm", type=str, default="torch", choices=["torch", "sklearn"])
+    p.add_argument("-gmm_pool_cap", type=int, default=0)
+    p.add_argument("-seed", type=int, default=0)
+    p.add_argument("-out_dir", type=str, default=".")
+    p.add_argument("-ckpt_every", type=int, default=0)
+    p.add_argument("-resume", action="store_true")
+    p.add_argument("-local_clients", type=int, default=0)
+    p.add_argument("-drop_client_prob", type=float, default=0.0)
+    p.add_argument("-metrics_log", type=str, default=None)
+    p.add_argument("-mode", type=str, default="fedavg", choices=["fedavg", "mdgan"])
+    p.add_argument("-batch_size", type=int, default=500)
+    p.add_argument("-timeout", type=float, default=600.0)
+    p.add_argument("-dump_real", action="store_true", help="write the synthetic client shards under out_dir/data/raw")
+    p.add_argument("-quiet", action="store_true")
+    return p
+
+
+def spec_from_args(args) -> DatasetSpec:
+    spec = get_spec(args.config)
+    if args.name:
+        spec.name = args.name.replace("_train", "") if args.name.endswith("_train") else args.name
+    for flag, field in (("selected_variables", "selected_variables"), ("categorical_list", "categorical_list"),
+                        ("nonnegative_list", "nonnegative_list"), ("date_dic", "date_dic"),
+                        ("target_column", "target_column"), ("problem_type", "problem_type")):
+        v = getattr(args, flag)
+        if v is not None:
+            setattr(spec, field, v)
+    if args.n_sample:
+        spec.n_sample = args.n_sample
+    return spec
+
+
+def fed_config_from_args(args):
+    from .fed.runtime import FedConfig
+    from .models.engine import EngineConfig
+    return FedConfig(spec=spec_from_args(args), epochs=args.epochs, datapath=args.datapath,
+                     synthetic_rows=args.synthetic_rows, shard_mode=args.shard, dirichlet_alpha=args.alpha,
+                     out_dir=args.out_dir, n_sample=args.n_sample, aggregation=args.aggregation,
+                     gmm_backend=args.gmm, gmm_pool_cap=args.gmm_pool_cap, backend=args.backend, seed=args.seed,
+                     engine=EngineConfig(batch_size=args.batch_size, precision=args.precision),
+                     ckpt_every=args.ckpt_every, resume=args.resume, verbose=not args.quiet,
+                     metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
+                     dump_real=args.dump_real)
+
+
+def pick_device(rank: int, colocated: bool, backend: str) -> torch.device:
+    if backend == "torch" or not torch.cuda.is_available():
+        return torch.device("cpu")
+    n = torch.cuda.device_count()
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    idx = local % n if colocated else max(local - 1, 0) % n
+    torch.cuda.set_device(idx)
+    return torch.device("cuda", idx)
+
+
+def run_rank(rank: int, args) -> None:
+    """One process of the federation (the reference ``run()``, `Server/dtds/distributed.py:838-891`)."""
+    from .fed.runtime import FedRuntime
+    from .parallel.comm import Comm
+    world = args.world_size
+    colocated = args.colocated
+    device = pick_device(rank, colocated, args.backend)
+    if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
+        torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
+    client_ranks = list(range(world)) if colocated else list(range(1, world))
+    data_backend = args.data_backend
+    if data_backend == "auto":
+        data_backend = "nccl" if (device.type == "cuda" and colocated) else "gloo"
+    comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
+    try:
+        rt = FedRuntime(fed_config_from_args(args), comm, device, federator=0)
+        rt.initialize()
+        rt.fit()
+        comm.barrier()
+    finally:
+        comm.destroy()
+
+
+def _spawn_entry(rank: int, args) -> None:
+    run_rank(rank, args)
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def main(argv: Optional[List[str]] = None) -> None:
+    args = build_parser().parse_args(argv)
+    if args.local_clients:
+        from .fed.local import run_local_emulation
+        run_local_emulation(fed_config_from_args(args), args.local_clients, backend=args.backend)
+        return
+    if args.rank is not None:
+        run_rank(args.rank, args)
+        return
+    # no rank given: launch the whole federation on this node
+    if args.world_size <= 1 or (args.world_size == 1 and not args.colocated):
+        args.colocated = True
+    if args.port == 7788:
+        args.port = free_port()
+    import torch.multiprocessing as mp
+    mp.spawn(_spawn_entry, args=(args,), nprocs=args.world_size, join=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -79,11 +79,58 @@ class FedConfig:
     use_graph: Optional[bool] = None
     verbose: bool = True
     metrics_log: Optional[str] = None
+    drop_client_prob: float = 0.0           # fault injection: a client misses a round with this probability
+    mode: str = "fedavg"                    # fedavg | mdgan
+    dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
     if cfg.verbose and rank == 0:
         print(*msg, flush=True)
+
+
+def federate_gmm(banks: List[VGMBank], rows: List[int], cfg: FedConfig, device) -> tuple:
+    """Federator side of ``uniform_continuous_gmm`` (`Server/dtds/distributed.py:689-765`).
+
+    Draw ``int(N * n_i / N)`` samples from every client's VGM per continuous column, measure each
+    client's Wasserstein-1 distance to the pooled sample, and fit one global VGM on the pool.
+    Returns (global bank as dict, valid-component masks, normalised W1 distances [K, n_cont]).
+    """
+    rng = np.random.default_rng(cfg.seed + 12345)
+    n_total = int(np.sum(rows))
+    if cfg.gmm_pool_cap and n_total > cfg.gmm_pool_cap:
+        n_total = cfg.gmm_pool_cap
+    share = [float(r) / float(np.sum(rows)) for r in rows]
+    n_cont = banks[0].n
+    pooled, per_client = [], [[] for _ in banks]
+    for j in range(n_cont):
+        parts = [b.sample_column(j, int(n_total * share[i]), rng) for i, b in enumerate(banks)]
+        for i, p in enumerate(parts):
+            per_client[i].append(p)
+        pooled.append(np.concatenate(parts))
+    e_hat = continuous_client_distances(pooled, per_client) if n_cont else np.zeros((len(banks), 0))
+    gb = fit_vgm(pooled, backend=cfg.gmm_backend, seed=cfg.seed, device=device)
+    comps = gb.components()
+    return gb.to_dict(), comps.tolist(), e_hat
+
+
+def round_alive_mask(cfg: FedConfig, epoch: int, k: int) -> np.ndarray:
+    """Fault injection: which clients take part in round ``epoch`` (deterministic in the seed).
+
+    At least one client always survives.  With ``drop_client_prob == 0`` every client is alive.
+    """
+    if cfg.drop_client_prob <= 0:
+        return np.ones(k, dtype=bool)
+    rng = np.random.default_rng([cfg.seed, 7, epoch])
+    alive = rng.random(k) >= cfg.drop_client_prob
+    if not alive.any():
+        alive[rng.integers(0, k)] = True
+    return alive
+
+
+def effective_weights(weights: np.ndarray, alive: np.ndarray) -> np.ndarray:
+    w = np.where(alive, weights, 0.0)
+    return w / w.sum()
 
 
 class FedRuntime:
@@ -110,11 +157,24 @@ class FedRuntime:
         if cfg.datapath and os.path.exists(cfg.datapath.format(client=idx, rank=self.rank)):
             return pd.read_csv(cfg.datapath.format(client=idx, rank=self.rank))
         if cfg.shard_mode == "independent":
-            return generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx)
-        full = generate(cfg.spec, cfg.synthetic_rows * k, seed=cfg.seed)
-        parts = shard(full, k, cfg.shard_mode, seed=cfg.seed, target=cfg.spec.target_column,
-                      alpha=cfg.dirichlet_alpha)
-        return parts[idx]
+            df = generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx)
+        else:
+            full = generate(cfg.spec, cfg.synthetic_rows * k, seed=cfg.seed)
+            df = shard(full, k, cfg.shard_mode, seed=cfg.seed, target=cfg.spec.target_column,
+                       alpha=cfg.dirichlet_alpha)[idx]
+        if cfg.dump_real:
+            d = os.path.join(cfg.out_dir, "data", "raw")
+            os.makedirs(d, exist_ok=True)
+            df.to_csv(os.path.join(d, f"{self.name}_train_client{idx}.csv"), index=False)
+        return df
+
+    def merge_real_shards(self):
+        """Federator: concatenate the clients' synthetic shards into data/raw/{name}_train.csv (for the
+        evaluators, which compare against the full real table like `Server/similarity_analysis.py:96`)."""
+        d = os.path.join(self.cfg.out_dir, "data", "raw")
+        parts = [os.path.join(d, f"{self.name}_train_client{i}.csv") for i in range(self.comm.n_clients)]
+        if all(os.path.exists(p) for p in parts):
+            pd.concat([pd.read_csv(p) for p in parts]).to_csv(os.path.join(d, f"{self.name}_train.csv"), index=False)
 
     # ================================================================= init protocol
     def initialize(self):
@@ -184,14 +244,12 @@ class FedRuntime:
         # ---- engine + F. initial weights
         torch.manual_seed(cfg.seed + self.rank)
         self.engine = CTGANEngine(lay, cfg.engine, self.device, backend=cfg.backend, seed=cfg.seed * 7919 + self.rank)
+        if getattr(self, "thread_local_capture", False):
+            self.engine.capture_mode = "thread_local"
         if self.is_client:
             self.engine.set_training_data(self.train_matrix)
         self.engine.set_generation_tables(self.gen_cond, self.transformer)
-        first = c.client_ranks[0]
-        if c.world_size > 1:
-            host = self.engine.flat.detach().cpu()
-            torch.distributed.broadcast(host, src=first, group=c.ctrl)
-            self.engine.flat.copy_(host)
+        c.broadcast_tensor(self.engine.flat, src=c.client_ranks[0])
         self.steps = [n // cfg.engine.batch_size for n in self.rows]
         if cfg.resume:
             self.load_checkpoint()
@@ -200,23 +258,7 @@ class FedRuntime:
                              f"steps/epoch={self.steps}")
 
     def _global_gmm(self, banks: List[VGMBank], rows: List[int]):
-        cfg = self.cfg
-        rng = np.random.default_rng(cfg.seed + 12345)
-        n_total = int(np.sum(rows))
-        if cfg.gmm_pool_cap and n_total > cfg.gmm_pool_cap:
-            n_total = cfg.gmm_pool_cap
-        share = [float(r) / float(np.sum(rows)) for r in rows]
-        n_cont = banks[0].n
-        pooled, per_client = [], [[] for _ in banks]
-        for j in range(n_cont):
-            parts = [b.sample_column(j, int(n_total * share[i]), rng) for i, b in enumerate(banks)]
-            for i, p in enumerate(parts):
-                per_client[i].append(p)
-            pooled.append(np.concatenate(parts))
-        e_hat = continuous_client_distances(pooled, per_client) if n_cont else np.zeros((len(banks), 0))
-        gb = fit_vgm(pooled, backend=cfg.gmm_backend, seed=cfg.seed, device=self.device)
-        comps = gb.components()
-        return gb.to_dict(), comps.tolist(), e_hat
+        return federate_gmm(banks, rows, self.cfg, self.device)
 
     def _write_meta_artifacts(self):
         mdir = os.path.join(self.cfg.out_dir, "models")
@@ -227,15 +269,18 @@ class FedRuntime:
             pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
 
     # ================================================================= rounds
-    def aggregate(self):
+    def aggregate(self, alive: np.ndarray | None = None):
+        """Weighted FedAvg of every G/D parameter and BN statistic (`Server/dtds/distributed.py:86-106`)
+        as one all-reduce of the pre-scaled flat buffer; clients that missed the round get weight 0."""
         c = self.comm
-        w = float(self.weights[c.client_index]) if self.is_client else 0.0
+        wts = self.weights if alive is None else effective_weights(self.weights, alive)
+        w = float(wts[c.client_index]) if self.is_client else 0.0
         c.weighted_all_reduce(self.engine.flat, w)
         c.share_with_federator(self.engine.flat, self.federator)
         # num_batches_tracked: weighted average of every client's counter, truncated (reference cast)
         ep = self.engine
         counts = np.asarray([2 * s for s in self.steps], dtype=np.float64) * (self._epoch_done)
-        ep.bn_batches = int(np.sum(self.weights * counts))
+        ep.bn_batches = int(np.sum(wts * counts))
 
     def sample_round(self, epoch: int):
         """Generate n_sample rows, decode, and (federator) write the epoch CSV."""
@@ -277,12 +322,13 @@ class FedRuntime:
     def run_round(self, epoch: int) -> float:
         c = self.comm
         t0 = time.time()
+        alive = round_alive_mask(self.cfg, epoch, c.n_clients)
         with self.timer.phase("train", self.device):
-            if self.is_client:
+            if self.is_client and alive[c.client_index]:
                 self.engine.train_epoch(self.cfg.use_graph)
         self._epoch_done = epoch + 1
         with self.timer.phase("aggregate", self.device):
-            self.aggregate()
+            self.aggregate(alive if self.cfg.drop_client_prob > 0 else None)
         with self.timer.phase("sample_dump", self.device):
             self.sample_round(epoch)
         if self.device.type == "cuda":
@@ -305,12 +351,15 @@ class FedRuntime:
                 self.save_checkpoint(ep + 1)
         if self.is_fed:
             self.write_timestamps()
+            if cfg.dump_real:
+                self.merge_real_shards()
 
     def write_timestamps(self):
+        """One per-round wall time per line, no header (`Server/dtds/distributed.py:827-829`)."""
+        import csv
         path = os.path.join(self.cfg.out_dir, "timestamp_experiment.csv")
-        with open(path, "w") as f:
-            for t in self.round_times:
-                f.write(f"{t}\r\n")
+        with open(path, "w", newline="") as f:
+            csv.writer(f, dialect="excel").writerows([[t] for t in self.round_times])
         return path
 
     # ================================================================= checkpoint / resume

@@ -121,6 +121,7 @@ class CTGANEngine:
         self._gen_bufs = None
         self.graph = None
         self.graph_steps = 0
+        self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
 
     # ================================================================= parameters
@@ -476,7 +477,7 @@ class CTGANEngine:
         for dst, src in zip((self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD), snap):
             dst.copy_(src)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
             self._one_step()
         self.graph = g
 

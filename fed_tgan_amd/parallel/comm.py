@@ -102,6 +102,16 @@ class Comm:
         if self.world_size > 1:
             dist.barrier(group=self.ctrl)
 
+    def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        """Broadcast a tensor over the control plane (device tensors are staged through host memory)."""
+        if self.world_size == 1:
+            return t
+        host = t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t
+        dist.broadcast(host, src=src, group=self.ctrl)
+        if host is not t:
+            t.copy_(host)
+        return t
+
     def all_reduce_cpu(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
         if self.world_size > 1:
             dist.all_reduce(t, op=op, group=self.ctrl)
