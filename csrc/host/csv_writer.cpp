@@ -6,7 +6,8 @@
 //     position is in (-4, 16], otherwise d.ddde[+-]XX with >= 2 exponent digits; "-0.0" kept);
 //     NaN -> empty field (pandas na_rep)
 //   * categoricals: vocabulary string of the integer code (QUOTE_MINIMAL quoting)
-//   * non-negative columns: v = exp(x) - 1, ceil(v) when v < 0, v == -1 -> " "
+//   * non-negative columns: the caller maps v = exp(x) - 1 (ceil when v < 0) with numpy's exp --
+//     libm's exp differs from numpy's in the last ulp for some inputs -- and v == -1 is written " "
 // Rows are formatted in parallel blocks by worker threads and written with one fwrite each.
 #include "csv_writer.h"
 
@@ -112,11 +113,9 @@ std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, in
           append_field(out, voc[(size_t)k]);
           break;
         }
-        case 2: {  // non-negative inverse log
-          double v = std::exp(x) - 1.0;
-          if (v < 0) v = std::ceil(v);
-          if (v == -1.0) out.push_back(' ');
-          else append_py_float(out, v);
+        case 2: {  // non-negative column, already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
+          if (x == -1.0) out.push_back(' ');
+          else append_py_float(out, x);
           break;
         }
         default:

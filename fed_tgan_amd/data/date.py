@@ -75,6 +75,7 @@ def join_dates(df: pd.DataFrame, date_columns: Dict[str, str]) -> pd.DataFrame:
         elems = d_fmt.split("-")
         names = [col + PART_SUFFIX[e] for e in elems]
         joined = df[names].astype(str).agg("-".join, axis=1)
+        fmt = "-".join(PART_STRFTIME[e] for e in elems)
 
         def rebuild(s: str):
             if EMPTY in s:
@@ -82,7 +83,8 @@ def join_dates(df: pd.DataFrame, date_columns: Dict[str, str]) -> pd.DataFrame:
             p = s.split("-")
             if len(p) >= 3:
                 p[2] = _repair_day(p[0], p[1], p[2])
-            ts = pd.to_datetime("-".join(p))
+            # explicit format: the reference's bare to_datetime reads "20-01-31" as 2031-01-20
+            ts = pd.to_datetime("-".join(p), format=fmt)
             if o_fmt == "yymmdd":
                 return int(ts.strftime("%y%m%d"))
             return ts

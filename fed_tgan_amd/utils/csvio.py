@@ -34,12 +34,14 @@ def _py_float(x: float) -> str:
 
 
 def format_table_py(values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
-                    vocabs: Sequence[Sequence[str]]) -> bytes:
-    out = [",".join(names)]
+                    vocabs: Sequence[Sequence[str]], empty_minus_one=None) -> bytes:
+    out = [",".join(_quote(n) for n in names)]
     cols = []
     for j, k in enumerate(kinds):
         v = values[:, j]
-        if k == KIND_FLOAT:
+        if k == KIND_FLOAT and empty_minus_one is not None and empty_minus_one[j]:
+            cols.append([" " if x == -1.0 else _py_float(x) for x in v])
+        elif k == KIND_FLOAT:
             cols.append([_py_float(x) for x in v])
         elif k == KIND_VOCAB:
             voc = vocabs[j]
@@ -62,11 +64,18 @@ def _quote(s: str) -> str:
 
 def write_table(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
                 vocabs: Sequence[Sequence[str]], threads: int = 0) -> None:
-    values = np.ascontiguousarray(values, dtype=np.float64)
+    values = np.array(values, dtype=np.float64, copy=True)
+    for j, k in enumerate(kinds):
+        if k == KIND_NONNEG:     # exp(x)-1 with numpy's exp (bit-identical to the pandas path)
+            w = np.exp(values[:, j]) - 1.0
+            neg = w < 0
+            w[neg] = np.ceil(w[neg])
+            values[:, j] = w
     lib = _native()
     if lib is not None:
         from ..ops import native
         native.write_csv(path, values, names, kinds, vocabs, threads)
         return
+    kinds_py = [KIND_FLOAT if k == KIND_NONNEG else k for k in kinds]
     with open(path, "wb") as f:
-        f.write(format_table_py(values, names, kinds, vocabs))
+        f.write(format_table_py(values, names, kinds_py, vocabs, empty_minus_one=[k == KIND_NONNEG for k in kinds]))

@@ -1,0 +1,61 @@
+"""Federated statistics (vocab merge, JSD / W1 client distances, aggregation weights) vs the reference math."""
+import numpy as np
+import pytest
+from scipy.spatial import distance
+from scipy.stats import wasserstein_distance
+
+from fed_tgan_amd.fed.stats import (aggregation_weights, jensenshannon, merge_categorical_metas,
+                                    normalise_over_clients, softmax, uniform_weights, wasserstein_1d)
+
+
+def test_jsd_matches_scipy():
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        p, q = rng.random(7), rng.random(7)
+        q[rng.integers(0, 7)] = 0
+        assert jensenshannon(p, q) == pytest.approx(distance.jensenshannon(p, q), abs=1e-12)
+        assert jensenshannon(p, q, 2.0) == pytest.approx(distance.jensenshannon(p, q, 2.0), abs=1e-12)
+
+
+def test_w1_matches_scipy():
+    rng = np.random.default_rng(1)
+    for n, m in ((10, 10), (100, 37), (1000, 2000)):
+        u, v = rng.normal(size=n), rng.normal(1, 2, size=m)
+        assert wasserstein_1d(u, v) == pytest.approx(wasserstein_distance(u, v), rel=1e-10)
+
+
+def _meta(counts):
+    return {"columns": [{"column_name": "c", "type": "categorical", "i2s": counts},
+                        {"column_name": "x", "type": "continous"}]}
+
+
+def test_vocab_merge_order_and_weights():
+    m1 = _meta({"a": 5, "b": 3})
+    m2 = _meta({"b": 6, "c": 1})
+    merged, vocabs, d_hat = merge_categorical_metas([m1, m2])
+    assert merged["columns"][0]["i2s"] == ["b", "a", "c"]       # by global frequency
+    assert vocabs[0].tolist() == ["a", "b", "c"]                # label codes alphabetical
+    glob = np.array([5, 9, 1.0])
+    d1 = distance.jensenshannon(glob, [5, 3, 0])
+    d2 = distance.jensenshannon(glob, [0, 6, 1])
+    assert d_hat[:, 0] == pytest.approx([d1 / (d1 + d2), d2 / (d1 + d2)])
+
+
+def test_identical_clients_uniform():
+    m = _meta({"a": 5, "b": 3})
+    _, _, d_hat = merge_categorical_metas([m, m, m])
+    assert np.allclose(d_hat, 1.0 / 3)                         # all-zero column -> 1/K
+    e_hat = normalise_over_clients(np.zeros((3, 2)), zero_fill_uniform=False)
+    w = aggregation_weights(d_hat, e_hat, [100, 100, 100])
+    assert np.allclose(w, 1.0 / 3)
+
+
+def test_aggregation_weight_formula():
+    d_hat = np.array([[0.2, 0.5], [0.8, 0.5]])
+    e_hat = np.array([[0.3], [0.7]])
+    rows = [300, 100]
+    s = e_hat.sum(1) + d_hat.sum(1)
+    raw = (1 - s / s.sum()) * np.array([0.75, 0.25])
+    assert aggregation_weights(d_hat, e_hat, rows) == pytest.approx(np.exp(raw) / np.exp(raw).sum())
+    assert softmax(np.array([0.0, 0.0])) == pytest.approx([0.5, 0.5])
+    assert uniform_weights(4) == pytest.approx([0.25] * 4)
