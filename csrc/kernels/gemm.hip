@@ -11,9 +11,11 @@
 //   * 64x64 output tile per 256-thread workgroup (4 waves in a 2x2 grid, 32x32 per wave);
 //   * the workgroup's whole K-chunk (KC = 128 bf16 / 64 fp32) is fetched in ONE burst --
 //     every thread issues all of its loads back to back from clamped, always-valid
-//     addresses (no predicated loads, which hipcc would serialise with vmcnt(0) each) -- so
-//     a chunk costs one memory round trip, and the next chunk's burst is in flight while the
-//     current one is multiplied out of LDS;
+//     addresses (no predicated loads, which hipcc would serialise with vmcnt(0) each), as
+//     16-B loads wherever the operand is 16-B aligned with a leading dimension divisible by
+//     4 (the engine pads its buffers so that the step's operands are) -- so a chunk costs one
+//     memory round trip, and the next chunk's burst is in flight while the current one is
+//     multiplied out of LDS;
 //   * operands are rounded to bf16 once, while staging into [row][k] LDS images (row stride
 //     KC+8 elements: every 16-lane ds_read_b128 group lands on distinct banks), then
 //     v_mfma_f32_16x16x32_bf16 with fp32 accumulation; or, with g.f32, kept in fp32 and fed
@@ -61,66 +63,130 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
 }
 
 // ----------------------------------------------------------------------------- chunk staging
-// A chunk is R=64 rows x KC k-values of one operand.  Thread mapping (NPT = KC/8 pairs each):
-//   ROWMAJ (k contiguous in memory):  pair column kp = t % (KC/2), row = t / (KC/2) + (NT/(KC/2)) * i
-//   else   (row contiguous):          row = t % 64,                kp  = t / 64 + (NT/64) * i
+// A chunk is R=64 rows x KC k-values of one operand, held as NV = KC/16 float4 per thread.
+//   ROWMAJ (k contiguous in memory): v[i] = row r, k = 4q..4q+3
+//       q = t % (KC/4), r = t / (KC/4) + (NT/(KC/4)) * i          (a wave reads 2 rows x KC floats)
+//   else   (rows contiguous):        v[2i], v[2i+1] = rows 4rq..4rq+3 at k = 2kp and 2kp+1
+//       rq = t % 16,    kp = t / 16 + 16 * i                      (a wave reads 4 k-lines x 64 rows)
+// With a 16-B aligned base, a leading dimension and a vector extent divisible by 4 ("vec"),
+// every load is a 16-B global_load_dwordx4 (one CU pulls several times more bytes per
+// instruction than with dword loads); otherwise every element is a clamped dword load.
+// Out-of-range elements are zeroed after all loads of the burst have been issued.
 template <int KC, bool ROWMAJ>
 struct Chunk {
-  static constexpr int NPAIR = KC / 8;  // (64 * KC / 2) / 256 pairs per thread
-  float x[2 * NPAIR];
+  static constexpr int NV = KC / 16;
+  f32x4 v[NV];
 
-  __device__ __forceinline__ static void coords(int i, int& r, int& kp) {
+  // vec: wave-uniform -- base 16-B aligned, ld % 4 == 0 and the vector extent (kmax for ROWMAJ,
+  // rmax otherwise) % 4 == 0, so every float4 is entirely inside or entirely outside the
+  // operand and its address can simply be clamped; the two paths are straight-line code.
+  __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0, int rmax, int k0, int kmax,
+                                       bool vec) {
     const int t = threadIdx.x;
-    if (ROWMAJ) {
-      r = t / (KC / 2) + (NT / (KC / 2)) * i;
-      kp = t % (KC / 2);
+    if constexpr (ROWMAJ) {
+      if (vec) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
+          const int k = min(k0 + 4 * (t % (KC / 4)), kmax - 4);
+          v[i] = *reinterpret_cast<const f32x4*>(p + (size_t)min(rr, rmax - 1) * ld + k);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
+          const int k = k0 + 4 * (t % (KC / 4));
+          const float* row = p + (size_t)min(rr, rmax - 1) * ld;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[i][e] = row[min(k + e, kmax - 1)];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
+        const int k = k0 + 4 * (t % (KC / 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (rr >= rmax || k + e >= kmax) v[i][e] = 0.f;
+      }
     } else {
-      r = t % 64;
-      kp = t / 64 + (NT / 64) * i;
-    }
-  }
-
-  __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0, int rmax, int k0, int kmax) {
+      if (vec) {
 #pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {
-      int r, kp;
-      coords(i, r, kp);
-      r += r0;
-      const int k = k0 + 2 * kp;
-      const int rc = min(r, rmax - 1);
-      const int kc0 = min(k, kmax - 1), kc1 = min(k + 1, kmax - 1);
-      x[2 * i] = ROWMAJ ? p[(size_t)rc * ld + kc0] : p[(size_t)kc0 * ld + rc];
-      x[2 * i + 1] = ROWMAJ ? p[(size_t)rc * ld + kc1] : p[(size_t)kc1 * ld + rc];
-    }
+        for (int i = 0; i < NV / 2; ++i) {
+          const int rr = min(r0 + 4 * (t % 16), rmax - 4);
+          const int k = k0 + 2 * (t / 16 + 16 * i);
+          v[2 * i] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k, kmax - 1) * ld + rr);
+          v[2 * i + 1] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k + 1, kmax - 1) * ld + rr);
+        }
+      } else {
 #pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {
-      int r, kp;
-      coords(i, r, kp);
-      r += r0;
-      const int k = k0 + 2 * kp;
-      if (!(r < rmax && k < kmax)) x[2 * i] = 0.f;
-      if (!(r < rmax && k + 1 < kmax)) x[2 * i + 1] = 0.f;
+        for (int i = 0; i < NV / 2; ++i) {
+          const int rr = r0 + 4 * (t % 16);
+          const int k = k0 + 2 * (t / 16 + 16 * i);
+          const float* l0 = p + (size_t)min(k, kmax - 1) * ld;
+          const float* l1 = p + (size_t)min(k + 1, kmax - 1) * ld;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rc = min(rr + e, rmax - 1);
+            v[2 * i][e] = l0[rc];
+            v[2 * i + 1][e] = l1[rc];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NV / 2; ++i) {
+        const int rr = r0 + 4 * (t % 16);
+        const int k = k0 + 2 * (t / 16 + 16 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (rr + e >= rmax || k >= kmax) v[2 * i][e] = 0.f;
+          if (rr + e >= rmax || k + 1 >= kmax) v[2 * i + 1][e] = 0.f;
+        }
+      }
     }
   }
 
   // bf16 image [row][KC + 8]
   __device__ __forceinline__ void store_bf16(uint16_t* s) const {
+    const int t = threadIdx.x;
+    if constexpr (ROWMAJ) {
 #pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {
-      int r, kp;
-      coords(i, r, kp);
-      *reinterpret_cast<uint32_t*>(&s[r * (KC + 8) + 2 * kp]) = pack_bf16x2(x[2 * i], x[2 * i + 1]);
+      for (int i = 0; i < NV; ++i) {
+        const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
+        *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) =
+            uint2{pack_bf16x2(v[i][0], v[i][1]), pack_bf16x2(v[i][2], v[i][3])};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV / 2; ++i) {
+        const int rq = t % 16, kp = t / 16 + 16 * i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *reinterpret_cast<uint32_t*>(&s[(4 * rq + e) * (KC + 8) + 2 * kp]) = pack_bf16x2(v[2 * i][e], v[2 * i + 1][e]);
+      }
     }
   }
 
   // fp32 image [row][KC + 1]
   __device__ __forceinline__ void store_f32(float* s) const {
+    const int t = threadIdx.x;
+    if constexpr (ROWMAJ) {
 #pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {
-      int r, kp;
-      coords(i, r, kp);
-      s[r * (KC + 1) + 2 * kp] = x[2 * i];
-      s[r * (KC + 1) + 2 * kp + 1] = x[2 * i + 1];
+      for (int i = 0; i < NV; ++i) {
+        const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[r * (KC + 1) + 4 * q + e] = v[i][e];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV / 2; ++i) {
+        const int rq = t % 16, kp = t / 16 + 16 * i;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[(4 * rq + e) * (KC + 1) + 2 * kp] = v[2 * i][e];
+          s[(4 * rq + e) * (KC + 1) + 2 * kp + 1] = v[2 * i + 1][e];
+        }
+      }
     }
   }
 };
@@ -166,18 +232,22 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
     }
   };
 
+  // 16-B operand loads (see Chunk::load); the vector extent is K for k-contiguous operands
+  // (every split boundary is a multiple of KC), the row count otherwise
+  const bool va = ((uintptr_t)g.a % 16 == 0) && (g.lda % 4 == 0) && ((TA ? g.M : g.K) % 4 == 0);
+  const bool vb = ((uintptr_t)g.b % 16 == 0) && (g.ldb % 4 == 0) && ((TB ? g.K : g.N) % 4 == 0);
   int buf = 0;
   if (kb < ke) {
-    ca.load(g.a, g.lda, m0, g.M, kb, ke);
-    cb.load(g.b, g.ldb, n0, g.N, kb, ke);
+    ca.load(g.a, g.lda, m0, g.M, kb, ke, va);
+    cb.load(g.b, g.ldb, n0, g.N, kb, ke, vb);
     stage(0);
   }
   __syncthreads();
   for (int k0 = kb; k0 < ke; k0 += KC) {
     const bool more = k0 + KC < ke;
     if (more) {  // next burst in flight while this chunk is multiplied
-      ca.load(g.a, g.lda, m0, g.M, k0 + KC, ke);
-      cb.load(g.b, g.ldb, n0, g.N, k0 + KC, ke);
+      ca.load(g.a, g.lda, m0, g.M, k0 + KC, ke, va);
+      cb.load(g.b, g.ldb, n0, g.N, k0 + KC, ke, vb);
     }
     const int kvalid = min(KC, ke - k0);
     if constexpr (F32) {

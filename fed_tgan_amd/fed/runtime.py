@@ -144,7 +144,7 @@ class FedRuntime:
         self.is_client = comm.is_client
         self.name = cfg.spec.name
         self.n_sample = cfg.n_sample or cfg.spec.n_sample
-        self.timer = PhaseTimer()
+        self.timer = PhaseTimer(sync=True)    # device-synchronised phase boundaries (3 per round)
         self.round_times: List[float] = []
         self.start_epoch = 0
         self.metrics = MetricsLog(cfg.metrics_log) if (cfg.metrics_log and self.is_fed) else None

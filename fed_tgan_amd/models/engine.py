@@ -36,6 +36,7 @@ step is ONE GEMM over the stacked [fake; real; interp] rows.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 from typing import Dict, List, Sequence, Tuple
 
@@ -47,6 +48,22 @@ from .ctgan import Discriminator, Generator
 from .samplers import CondTables, RowIndex
 
 EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU = 0, 1, 2, 3
+
+
+def _ceil4(n: int) -> int:
+    return (int(n) + 3) // 4 * 4
+
+
+def _padded_rows(rows: int, cols: int, device) -> torch.Tensor:
+    """[rows, cols] view of a zeroed [rows, ceil4(cols)] buffer (16-B aligned row starts)."""
+    return torch.zeros(rows, _ceil4(cols), dtype=torch.float32, device=device)[:, :cols]
+
+
+def _ext(t: torch.Tensor, cols: int) -> torch.Tensor:
+    """Widen a row-strided 2-D view to ``cols`` columns, into its storage's zero padding."""
+    if t.shape[1] == cols:
+        return t
+    return t.as_strided((t.shape[0], cols), t.stride(), t.storage_offset())
 
 
 @dataclasses.dataclass
@@ -68,6 +85,7 @@ class EngineConfig:
     bn_eps: float = 1e-5
     gen_chunk: int = 8192
     precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
+    streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -116,6 +134,11 @@ class CTGANEngine:
         self.cond_spans = [(int(s), int(w)) for s, w in zip(layout.cond_start, layout.cond_width)]
         self._build_params()
         self._build_buffers()
+        # side streams ("lanes") for independent work inside a step; the captured graph keeps the
+        # fork/join edges, so its branches run concurrently on the device
+        self.lanes = None
+        if self.device.type == "cuda" and cfg.streams:
+            self.lanes = [None] + [torch.cuda.Stream(self.device) for _ in range(3)]
         self.tables: Dict[str, torch.Tensor] = {}
         self.gen_tables = None
         self._gen_bufs = None
@@ -144,7 +167,12 @@ class CTGANEngine:
         order = {"G": 0, "D": 1, "S": 2}
         spec.sort(key=lambda t: order[t[2]])
         self.param_spec = spec
-        sizes = [int(np.prod(s)) for _, s, _ in spec]
+        # 2-D weights are stored with their rows padded to a multiple of 4 floats (zero columns
+        # that stay zero under Adam, L2 decay and aggregation) and every tensor starts 16-B
+        # aligned, so the GEMMs read them with 16-B loads; self.p / self.g expose the logical
+        # [rows, cols] views, _ext() widens them to the padded width
+        store = [(s[0], _ceil4(s[1])) if len(s) == 2 else s for _, s, _ in spec]
+        sizes = [int(np.prod(s)) for s in store]
         # every group starts 64-byte aligned (vectorised optimizer / aggregation kernels)
         align = 16
         offsets, pos, prev = [], 0, None
@@ -152,14 +180,20 @@ class CTGANEngine:
             if grp != prev:
                 pos = (pos + align - 1) // align * align
                 prev = grp
+            pos = _ceil4(pos)
             offsets.append(pos)
             pos += n
         total = (pos + align - 1) // align * align
         self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
         self.p: Dict[str, torch.Tensor] = {}
         self.group_range = {}
-        for (name, shape, grp), n, o in zip(spec, sizes, offsets):
-            self.p[name] = self.flat[o:o + n].view(shape)
+
+        def view(buf, o, n, shape, st):
+            v = buf[o:o + n].view(st)
+            return v[:, :shape[1]] if len(shape) == 2 else v
+
+        for (name, shape, grp), n, o, st in zip(spec, sizes, offsets, store):
+            self.p[name] = view(self.flat, o, n, shape, st)
             a, _ = self.group_range.get(grp, (o, o))
             self.group_range[grp] = (a, (o + n + align - 1) // align * align)
         gA, gB = self.group_range["G"]
@@ -170,13 +204,11 @@ class CTGANEngine:
         self.gradG = torch.zeros(self.nG, dtype=torch.float32, device=self.device)
         self.gradD = torch.zeros(self.nD, dtype=torch.float32, device=self.device)
         self.g: Dict[str, torch.Tensor] = {}
-        for (name, shape, grp), n in zip(spec, sizes):
+        for (name, shape, grp), n, o, st in zip(spec, sizes, offsets, store):
             if grp == "S":
                 continue
-            base = self.p[name].data_ptr() - (self.flatG if grp == "G" else self.flatD).data_ptr()
-            buf = self.gradG if grp == "G" else self.gradD
-            o = base // 4
-            self.g[name] = buf[o:o + n].view(shape)
+            base = o - (gA if grp == "G" else dA)
+            self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st)
         self.mG = torch.zeros_like(self.gradG)
         self.vG = torch.zeros_like(self.gradG)
         self.mD = torch.zeros_like(self.gradD)
@@ -213,13 +245,13 @@ class CTGANEngine:
         return m
 
     def g_state_dict(self) -> Dict[str, torch.Tensor]:
-        sd = {k: self.p[n].detach().cpu().clone() for k, n in self.g_key_map()}
+        sd = {k: self.p[n].detach().contiguous().cpu().clone() for k, n in self.g_key_map()}
         for i in range(len(self.gdims)):
             sd[f"seq.{i}.bn.num_batches_tracked"] = torch.tensor(self.bn_batches, dtype=torch.int64)
         return sd
 
     def d_state_dict(self) -> Dict[str, torch.Tensor]:
-        return {k: self.p[n].detach().cpu().clone() for k, n in self.d_key_map()}
+        return {k: self.p[n].detach().contiguous().cpu().clone() for k, n in self.d_key_map()}
 
     def load_g_state_dict(self, sd):
         with torch.no_grad():
@@ -250,17 +282,20 @@ class CTGANEngine:
         dev, f32 = self.device, torch.float32
         B, nP = self.B, self.nP
         z = lambda *s: torch.zeros(*s, dtype=f32, device=dev)  # noqa: E731
-        self.H = z(B, self.Hw)
+        self.H = _padded_rows(B, self.Hw, dev)
         self.abuf = [z(B, g) for g in self.gdims]
         self.nhat = [z(B, g) for g in self.gdims]
         self.bn_mean = [z(g) for g in self.gdims]
         self.bn_invstd = [z(g) for g in self.gdims]
         self.da = [z(B, g) for g in self.gdims]
-        self.logits = z(B, self.Dd)
-        self.dlogits = z(B, self.Dd)
-        self.dH = z(B, self.Hw)
+        self.logits = _padded_rows(B, self.Dd, dev)
+        self.dlogits = _padded_rows(B, self.Dd, dev)
+        self.dH = _padded_rows(B, self.Hw, dev)
         self.Xd = z(3 * B, self.Din)
         self.X = self.Xd.view(3 * nP, self.K1)
+        # the G phase's fake rows have their own buffer so its prepare can overlap the D update
+        self.Xg = z(B, self.Din)
+        self.XgP = self.Xg.view(nP, self.K1)
         self.dact = None
         self.dl = [z(3 * nP, h) for h in self.ddims]
         self.ms = [z(3 * nP, h) for h in self.ddims]
@@ -325,20 +360,31 @@ class CTGANEngine:
         self._gen_bufs = None
 
     # ================================================================= forward pieces
+    def _kpad(self, H, a: int, W: torch.Tensor):
+        """(H[:, a:], W) widened over their zero padding to a K divisible by 4 when H's row
+        stride allows it (16-B GEMM loads along K); otherwise the logical views."""
+        x = H[:, a:]
+        kp = _ceil4(x.shape[1])
+        if kp != x.shape[1] and H.stride(0) >= a + kp and W.stride(0) >= kp:
+            return _ext(x, kp), _ext(W, kp)
+        return x, W
+
     def _g_forward(self, H, logits, training: bool, nhat=True):
         o = self.ops
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
-            o.linear_bn_relu(H[:, a:], self.p[f"G.{i}.W"], self.p[f"G.{i}.b"], self.p[f"G.{i}.gamma"],
+            x, W = self._kpad(H, a, self.p[f"G.{i}.W"])
+            o.linear_bn_relu(x, W, self.p[f"G.{i}.b"], self.p[f"G.{i}.gamma"],
                              self.p[f"G.{i}.beta"], H[:, b_:a],
                              self.abuf[i] if nhat else None, self.nhat[i] if nhat else None,
                              self.bn_mean[i], self.bn_invstd[i], self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
                              training, self.cfg.bn_momentum, self.cfg.bn_eps)
-        o.gemm(H, self.p["G.out.W"], logits, tb=True, bias=self.p["G.out.b"])
+        x, W = self._kpad(H, 0, self.p["G.out.W"])
+        o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
 
-    def _d_forward(self, rows: slice, stream_base: int):
+    def _d_forward(self, rows: slice, stream_base: int, X=None):
         o = self.ops
-        inp = self.X[rows]
+        inp = (self.X if X is None else X)[rows]
         for i in range(len(self.ddims)):
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][rows], tb=True, bias=self.p[f"D.{i}.b"], epi=EPI_LRELU_DROPOUT,
                    ms=self.ms[i][rows], slope=self.cfg.lrelu_slope, p_drop=self.cfg.dropout_p,
@@ -349,6 +395,30 @@ class CTGANEngine:
         o = self.ops
         for i in range(len(self.ddims) - 1, 0, -1):
             o.gemm(self.A[i][rows], self.p[f"D.{i}.W"], self.A[i - 1][rows], epi=EPI_MASK, ms=self.ms[i - 1][rows])
+
+    # ================================================================= lanes
+    @contextlib.contextmanager
+    def _lane(self, k: int):
+        """Issue the enclosed launches on side stream ``k`` (forked from the current stream)."""
+        if self.lanes is None:
+            yield
+            return
+        s = self.lanes[k]
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        prev = getattr(self.ops, "lane", 0)
+        self.ops.lane = k
+        try:
+            with torch.cuda.stream(s):
+                yield
+        finally:
+            self.ops.lane = prev
+
+    def _join(self, *ks: int):
+        if self.lanes is None:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for k in ks:
+            cur.wait_stream(self.lanes[k])
 
     # ================================================================= steps
     def _d_step(self):
@@ -378,18 +448,20 @@ class CTGANEngine:
         # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
         o.gemm(self.A[0][I], self.p["D.0.W"], self.gbuf)
         o.gp_scale(self.gbuf, self.X[I], self.cfg.gp_lambda, self.metrics[1:2])
+        # R-chain on the main lane; each layer's weight-gradient GEMM (one GEMM over the stacked
+        # rows) starts on a side lane as soon as its right operand is complete
         inp = self.X[I]
-        for i in range(L):
-            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I])
-            inp = self.dl[i][I]
-        # weight gradients: one GEMM per layer over the stacked rows
-        fr = slice(0, 2 * nP)
         prev = self.X
         for i in range(L):
-            o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True)
+            with self._lane(1 + i % 2):
+                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True)
+            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I])
+            inp = self.dl[i][I]
             prev = self.dl[i]
+        fr = slice(0, 2 * nP)
         o.colsum_many([self.A[i][fr] for i in range(L)], [self.g[f"D.{i}.b"] for i in range(L)])
         o.gemm(self.dl[L - 1], self.coef3.view(-1, 1), self.g["D.out.W"].view(-1, 1), ta=True)
+        self._join(1, 2)
         # d(loss)/d(e_out) = sum of the +-1/n_packs seeds = 0 (stays zero from allocation)
         b1, b2 = self.cfg.betas
         o.adam(self.flatD, self.gradD, self.mD, self.vD, self.stepD, self.cfg.lr, b1, b2, self.cfg.adam_eps, 0.0)
@@ -400,28 +472,30 @@ class CTGANEngine:
 
     def _g_prepare(self):
         o, B = self.ops, self.B
-        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], None, self.Dd,
+        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xg, None, self.Dd,
                        self.col, self.opt, step_counter=self.stepG, stream_id=11)
         self._g_forward(self.H, self.logits, training=True)
-        o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=12)
+        o.activate(self.logits, self.Xg[:, :self.Dd], self.spans, self.cfg.tau, stream_id=12)
 
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
         o, B, nP = self.ops, self.B, self.nP
         L = len(self.ddims)
         fk = slice(0, nP)
-        self._d_forward(fk, stream_base=14)
+        self._d_forward(fk, stream_base=14, X=self.XgP)
         o.d_head(self.dl[L - 1][fk], self.ms[L - 1][fk], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coefg,
                  self.coefg, self.y[fk], self.A[L - 1][fk], self.metrics[2:3])
         self._a_chain(fk)
         o.gemm(self.A[0][fk], self.p["D.0.W"], self.gbuf)            # d(-mean D)/dX, packed
         dx = self.gbuf.view(B, self.Din)
-        o.act_bwd_ce(dx[:, :self.Dd], self.Xd[0:B, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
+        o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
                      self.opt, self.dlogits, self.metrics[3:4], self.cfg.tau)
-        # generator backward
+        # generator backward: the dH chain on the main lane, weight gradients on side lanes
         Lg = len(self.gdims)
-        o.gemm(self.dlogits, self.H, self.g["G.out.W"], ta=True)
-        o.colsum_many([self.dlogits], [self.g["G.out.b"]])
+        with self._lane(1):
+            x, dW = self._kpad(self.H, 0, self.g["G.out.W"])
+            o.gemm(self.dlogits, x, dW, ta=True)
+            o.colsum_many([self.dlogits], [self.g["G.out.b"]])
         top = self.off[0]
         if Lg:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
@@ -430,9 +504,15 @@ class CTGANEngine:
             o.bn_relu_bwd(self.dH[:, b_:a], self.H[:, b_:a], self.nhat[i], self.p[f"G.{i}.gamma"],
                           self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"],
                           self.g[f"G.{i}.b"])
-            o.gemm(self.da[i], self.H[:, a:], self.g[f"G.{i}.W"], ta=True)
             if i > 0:
+                with self._lane(2 + i % 2):
+                    x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
+                    o.gemm(self.da[i], x, dW, ta=True)
                 o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0)
+            else:
+                x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
+                o.gemm(self.da[i], x, dW, ta=True)
+        self._join(1, 2, 3)
         b1, b2 = self.cfg.betas
         o.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
                self.cfg.l2scale, last_in_step=True)
@@ -440,8 +520,14 @@ class CTGANEngine:
     def _one_step(self):
         if hasattr(self.ops, "begin_step"):
             self.ops.begin_step(self)
-        self._d_step()
-        self._g_step()
+        # the G phase's sampling + generator forward only depends on G (unchanged by the D
+        # step), so it runs on lane 3 while the D update runs on the main lane
+        self._d_prepare()
+        with self._lane(3):
+            self._g_prepare()
+        self._d_update()
+        self._join(3)
+        self._g_update()
         if hasattr(self.ops, "end_step"):
             self.ops.end_step(self)
 
@@ -515,7 +601,6 @@ class CTGANEngine:
     def _gen_buffers(self, n: int):
         if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n:
             m = max(n, min(self.cfg.gen_chunk, n))
-            self._gen_bufs = (torch.zeros(m, self.Hw, device=self.device),
-                              torch.zeros(m, self.Dd, device=self.device))
+            self._gen_bufs = (_padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device))
         H, lg = self._gen_bufs
         return H[:n], lg[:n]

@@ -3,7 +3,7 @@
 Same method signatures as :class:`fed_tgan_amd.ops.ref.TorchOps`.  There is no silent
 fallback: constructing :class:`HipOps` raises if the native library is not built or does not
 load.  Host-side work per call is limited to picking split-K factors, caching int32 span
-tables on the device and reusing one split-K workspace, so the launch sequence of a step is
+tables on the device and reusing one split-K workspace per stream lane, so the launch sequence of a step is
 static and hipGraph-capturable.
 
 RNG bookkeeping: one device int64 step counter per engine (``self.ctr``) addresses every
@@ -51,18 +51,23 @@ class HipOps:
         self.device = device
         self.seed = int(seed) & ((1 << 62) - 1)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=device)
-        self.ws = torch.zeros(1 << 20, dtype=torch.float32, device=device)
+        self.split_override = None   # int: force the split-K factor (tuning / microbenchmarks)
+        self.lane = 0          # set by the engine while it issues work on a side stream
+        self._ws: Dict[int, torch.Tensor] = {}
         self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
         self._dec: Dict[int, Tuple] = {}
         self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
 
     # ------------------------------------------------------------------ helpers
     def _workspace(self, n: int) -> torch.Tensor:
-        if self.ws.numel() < n:
+        """Split-K slab of the current lane (concurrent lanes never share one)."""
+        ws = self._ws.get(self.lane)
+        if ws is None or ws.numel() < n:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")
-            self.ws = torch.zeros(int(n * 1.25), dtype=torch.float32, device=self.device)
-        return self.ws
+            ws = torch.zeros(max(1 << 20, int(n * 1.25)), dtype=torch.float32, device=self.device)
+            self._ws[self.lane] = ws
+        return ws
 
     def _span_tables(self, spans, cond_spans=None):
         key = (tuple(spans), tuple(cond_spans or ()))
@@ -92,7 +97,7 @@ class HipOps:
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
-        sk = _splitk(M, N, K, 64 if self.f32 else 128)
+        sk = self.split_override or _splitk(M, N, K, 64 if self.f32 else 128)
         ws = None
         if sk > 1:
             ws = self._workspace(sk * M * N)

@@ -196,3 +196,24 @@ def test_deeper_discriminator_gp():
         ref = t.grad if t.grad is not None else torch.zeros_like(t)
         scale = ref.abs().max().clamp_min(1e-6)
         assert (eng.g[n] - ref).abs().max() / scale < 2e-4, n
+
+
+def test_padded_storage_stays_zero():
+    """Weights live in rows padded to 4 floats (16-B GEMM loads); the padding columns and the
+    activation buffers' padding must stay exactly zero through training (they enter K sums)."""
+    from fed_tgan_amd.models.engine import _ceil4, _ext
+    eng, _ = _setup(batch=100)
+    eng.ops = type(eng.ops).__mro__[1]()       # plain TorchOps
+    eng.train_steps(3, use_graph=False)
+    padded = 0
+    for n, t in list(eng.p.items()) + [("g." + k, v) for k, v in eng.g.items()]:
+        if t.dim() == 2 and t.shape[1] % 4:
+            padded += 1
+            full = _ext(t, _ceil4(t.shape[1]))
+            assert torch.count_nonzero(full[:, t.shape[1]:]) == 0, n
+    assert padded > 0
+    for buf in (eng.H, eng.dH, eng.logits):
+        if buf.shape[1] % 4:
+            assert torch.count_nonzero(_ext(buf, _ceil4(buf.shape[1]))[:, buf.shape[1]:]) == 0
+    x, W = eng._kpad(eng.H, 0, eng.p["G.out.W"])
+    assert x.shape[1] % 4 == 0 and W.shape[1] == x.shape[1]

@@ -228,11 +228,13 @@ def test_slerp_on_arc(hip):
     sol = torch.linalg.lstsq(A, o.unsqueeze(2)).solution.squeeze(2)
     cos = (r / r.norm(dim=1, keepdim=True) * f / f.norm(dim=1, keepdim=True)).sum(1).clamp(-1, 1)
     om = torch.acos(cos)
-    alpha = torch.asin((sol[:, 1] * torch.sin(om)).clamp(-1, 1)) / om
-    wa = torch.sin((1 - alpha) * om) / torch.sin(om)
-    well = (alpha > 0.02) & (alpha < 0.98)          # asin is ill-conditioned at the arc ends
-    assert torch.allclose(wa[well], sol[well, 0], atol=2e-3)
-    assert (alpha >= -1e-5).all() and (alpha <= 1 + 1e-5).all()
+    # on the arc: wa = sin((1-a)om)/sin(om), wb = sin(a om)/sin(om)  <=>  (wa + wb cos om, wb sin om) is the
+    # unit vector at angle a*om, so its norm is 1 and its angle gives a
+    wa, wb = sol[:, 0], sol[:, 1]
+    u, v = wa + wb * torch.cos(om), wb * torch.sin(om)
+    assert torch.allclose(u * u + v * v, torch.ones_like(u), atol=2e-3)
+    alpha = torch.atan2(v, u) / om
+    assert (alpha >= -1e-3).all() and (alpha <= 1 + 1e-3).all()
     assert 0.35 < alpha.mean().item() < 0.65
 
 

@@ -33,9 +33,20 @@ def per_call(fn, dev, n=50, reps=20):
     return (time.perf_counter() - t) / (reps * n) * 1e6
 
 
+def step_only(eng, dev):
+    for _ in range(2):
+        a = per_call(eng._one_step, dev, n=5, reps=20)
+        lanes, eng.lanes = eng.lanes, None
+        b = per_call(eng._one_step, dev, n=5, reps=20)
+        eng.lanes = lanes
+        print(f"full step: side lanes {a:8.2f} us   one stream {b:8.2f} us")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
+    ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -46,6 +57,8 @@ def main():
     o = eng.ops
     nP, B = eng.nP, eng.B
     res = {}
+    if args.step_only:
+        return step_only(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
     shapes = {
         "G0 fwd 500x256x(E+C) NT": (eng.H[:, eng.off[0]:], eng.p["G.0.W"], eng.abuf[0], False, True),
@@ -58,7 +71,24 @@ def main():
         "dV0 256xK1x150 TN": (eng.A[0], eng.X, eng.g["D.0.W"], True, False),
         "dWout DdxHwx500 TN": (eng.dlogits, eng.H, eng.g["G.out.W"], True, False),
         "dH 500x512xDd NN": (eng.dlogits, eng.p["G.out.W"][:, :eng.off[0]], eng.dH[:, :eng.off[0]], False, False),
+        "R0 50x256xK1 NT": (eng.X[2 * nP:], eng.p["D.0.W"], eng.dl[0][2 * nP:], False, True),
+        "dW1 256x(E+C+256)x500 TN": (eng.da[1], eng.H[:, eng.off[1]:], eng.g["G.1.W"], True, False),
     }
+    if args.split_sweep:
+        for name, (a, b, c, ta, tb) in shapes.items():
+            K = a.shape[0] if ta else a.shape[1]
+            kc = 64 if o.f32 else 128
+            bursts = -(-K // kc)
+            row = []
+            for sk in [0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48]:
+                if sk > bursts:
+                    break
+                o.split_override = sk or None
+                us = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
+                row.append(f"{'auto' if sk == 0 else sk}:{us:.1f}")
+            o.split_override = None
+            print(f"{name:28s} " + "  ".join(row), flush=True)
+        return
     for name, (a, b, c, ta, tb) in shapes.items():
         res[name] = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
     t = eng.tables
@@ -77,7 +107,10 @@ def main():
                              dev)
     res["slerp"] = per_call(lambda: o.slerp(eng.Xd[B:2 * B], eng.Xd[0:B], eng.Xd[2 * B:3 * B]), dev)
     res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[2 * nP:], 10.0, eng.metrics[1:2]), dev)
-    res["full step (graph)"] = per_call(eng._one_step, dev, n=5, reps=20)
+    res["full step (graph, side lanes)"] = per_call(eng._one_step, dev, n=5, reps=20)
+    lanes, eng.lanes = eng.lanes, None
+    res["full step (graph, one stream)"] = per_call(eng._one_step, dev, n=5, reps=20)
+    eng.lanes = lanes
     for k, v in res.items():
         print(f"{v:9.2f} us  {k}")
 
