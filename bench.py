@@ -71,12 +71,14 @@ def main():
     rt.initialize()
     for ep in range(args.warmup):
         rt.run_round(ep)
+    rt.flush_writes()
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for ep in range(args.warmup, args.warmup + args.steps):
         rt.round_times.append(rt.run_round(ep))
+    rt.flush_writes()       # every timed round's CSV is on disk inside the timed region
     if device.type == "cuda":
         torch.cuda.synchronize(device)
     comm.barrier()

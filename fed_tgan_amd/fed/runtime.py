@@ -72,6 +72,7 @@ class FedConfig:
     backend: str = "auto"                   # engine ops: auto | hip | torch
     write_csv: bool = True
     csv_writer: str = "auto"                # auto | native | pandas
+    async_csv: bool = True                  # write each epoch CSV in the background (overlaps next round)
     seed: int = 0
     engine: EngineConfig = dataclasses.field(default_factory=EngineConfig)
     ckpt_every: int = 0
@@ -144,6 +145,7 @@ class FedRuntime:
         self.is_client = comm.is_client
         self.name = cfg.spec.name
         self.n_sample = cfg.n_sample or cfg.spec.n_sample
+        self._writer = None
         self.timer = PhaseTimer(sync=True)    # device-synchronised phase boundaries (3 per round)
         self.round_times: List[float] = []
         self.start_epoch = 0
@@ -308,6 +310,20 @@ class FedRuntime:
         return d
 
     def write_epoch_csv(self, values: np.ndarray, epoch: int):
+        if self.cfg.async_csv:
+            if self._writer is None:
+                from ..utils.csvio import AsyncTableWriter
+                self._writer = AsyncTableWriter()
+            self._writer.submit(self._write_epoch_csv, values, epoch)
+            return os.path.join(self.result_dir(), f"{self.name}_synthesis_epoch_{epoch}.csv")
+        return self._write_epoch_csv(values, epoch)
+
+    def flush_writes(self):
+        """Block until every submitted epoch CSV is on disk."""
+        if self._writer is not None:
+            self._writer.flush()
+
+    def _write_epoch_csv(self, values: np.ndarray, epoch: int):
         path = os.path.join(self.result_dir(), f"{self.name}_synthesis_epoch_{epoch}.csv")
         use_native = self.cfg.csv_writer in ("auto", "native") and self.csv_cols is not None
         if use_native:
@@ -349,6 +365,7 @@ class FedRuntime:
                                         **self.timer.last()})
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
                 self.save_checkpoint(ep + 1)
+        self.flush_writes()
         if self.is_fed:
             self.write_timestamps()
             if cfg.dump_real:

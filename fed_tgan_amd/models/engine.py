@@ -369,7 +369,9 @@ class CTGANEngine:
             return _ext(x, kp), _ext(W, kp)
         return x, W
 
-    def _g_forward(self, H, logits, training: bool, nhat=True):
+    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0):
+        """Residual stack + output layer; with ``act_out`` the activation is fused onto the
+        output GEMM (tanh / Gumbel-softmax into act_out, Philox stream ``stream_id``)."""
         o = self.ops
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
@@ -380,7 +382,10 @@ class CTGANEngine:
                              self.bn_mean[i], self.bn_invstd[i], self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
                              training, self.cfg.bn_momentum, self.cfg.bn_eps)
         x, W = self._kpad(H, 0, self.p["G.out.W"])
-        o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
+        if act_out is None:
+            o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
+        else:
+            o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id)
 
     def _d_forward(self, rows: slice, stream_base: int, X=None):
         o = self.ops
@@ -431,8 +436,7 @@ class CTGANEngine:
         o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], self.Xd[B:2 * B], self.Dd,
                        self.col, self.opt, step_counter=self.stepD, metrics=self.metrics, zero_metrics=True,
                        stream_id=1)
-        self._g_forward(self.H, self.logits, training=True)
-        o.activate(self.logits, self.Xd[0:B, :self.Dd], self.spans, self.cfg.tau, stream_id=2)
+        self._g_forward(self.H, self.logits, training=True, act_out=self.Xd[0:B, :self.Dd], stream_id=2)
         o.slerp(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], stream_id=3)
 
     def _d_update(self):
@@ -474,8 +478,7 @@ class CTGANEngine:
         o, B = self.ops, self.B
         o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xg, None, self.Dd,
                        self.col, self.opt, step_counter=self.stepG, stream_id=11)
-        self._g_forward(self.H, self.logits, training=True)
-        o.activate(self.logits, self.Xg[:, :self.Dd], self.spans, self.cfg.tau, stream_id=12)
+        self._g_forward(self.H, self.logits, training=True, act_out=self.Xg[:, :self.Dd], stream_id=12)
 
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""

@@ -40,6 +40,15 @@ def _splitk(M: int, N: int, K: int, kc: int = 128) -> int:
     return int(max(1, min(want, bursts, cap_ws)))
 
 
+def _effective_splits(K: int, sk: int, kc: int) -> int:
+    """The split count launch_gemm actually runs: K slices are rounded up to whole bursts."""
+    if sk <= 1:
+        return 1
+    kchunk = -(-max(K, 1) // sk)
+    kchunk = -(-kchunk // kc) * kc
+    return -(-max(K, 1) // kchunk)
+
+
 class HipOps:
     name = "hip"
 
@@ -94,10 +103,12 @@ class HipOps:
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
              slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5):
+        """C = epi(alpha op(A) op(B) + beta C + bias)."""
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
-        sk = self.split_override or _splitk(M, N, K, 64 if self.f32 else 128)
+        kc = 64 if self.f32 else 128
+        sk = _effective_splits(K, self.split_override or _splitk(M, N, K, kc), kc)
         ws = None
         if sk > 1:
             ws = self._workspace(sk * M * N)
@@ -109,6 +120,8 @@ class HipOps:
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5):
         if training:
+            # (fusing the split-K reduction into this BN launch was measured slower: the BN grid
+            # has only cols/16 workgroups to pull the slabs -- profiles/README.md)
             self.gemm(x, W, abuf, tb=True, bias=b)
             self.L.bn_relu_train(abuf, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps))
         else:
@@ -146,6 +159,11 @@ class HipOps:
     def activate(self, logits, out, spans, tau=0.2, stream_id=0):
         st, w, k, ci, el = self._span_tables(spans)
         self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16)
+
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0):
+        """logits = x W^T + b; out = activate(logits)."""
+        self.gemm(x, W, logits, tb=True, bias=b)
+        self.activate(logits, out, spans, tau, stream_id)
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
         st, w, k, ci, el = self._span_tables(spans, cond_spans)

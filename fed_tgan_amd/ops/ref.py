@@ -145,6 +145,10 @@ class TorchOps:
             dbias.copy_(da.sum(0))
 
     # ------------------------------------------------------------------ activations
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0):
+        self.gemm(x, W, logits, tb=True, bias=b)
+        self.activate(logits, out, spans, tau, stream_id=stream_id)
+
     def activate(self, logits, out, spans, tau=0.2, stream_id=0):
         """spans: list of (start, width, kind) host tuples (kind 0 tanh, 1 gumbel-softmax)."""
         for s, w, k in spans:

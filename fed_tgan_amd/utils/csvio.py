@@ -79,3 +79,28 @@ def write_table(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequ
     kinds_py = [KIND_FLOAT if k == KIND_NONNEG else k for k in kinds]
     with open(path, "wb") as f:
         f.write(format_table_py(values, names, kinds_py, vocabs, empty_minus_one=[k == KIND_NONNEG for k in kinds]))
+
+
+class AsyncTableWriter:
+    """Writes epoch tables on one background thread so formatting + file IO of round ``r``
+    overlaps the GPU training of round ``r + 1`` (the native formatter releases the GIL).
+    Writes complete in submission order; :meth:`flush` waits for all of them and re-raises
+    the first failure."""
+
+    def __init__(self):
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="csv-writer")
+        self._pending = []
+
+    def submit(self, fn, *args, **kwargs):
+        self._pending.append(self._pool.submit(fn, *args, **kwargs))
+        self._pending = [f for f in self._pending if not f.done() or f.exception() is not None]
+
+    def flush(self):
+        pending, self._pending = self._pending, []
+        for f in pending:
+            f.result()
+
+    def close(self):
+        self.flush()
+        self._pool.shutdown(wait=True)
