@@ -114,15 +114,18 @@ def fed_config_from_args(args):
                      engine=EngineConfig(batch_size=args.batch_size, precision=args.precision),
                      ckpt_every=args.ckpt_every, resume=args.resume, verbose=not args.quiet,
                      metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
+                     e_interval=args.E_interval,
                      dump_real=args.dump_real, async_csv=not args.sync_csv)
 
 
-def pick_device(rank: int, colocated: bool, backend: str) -> torch.device:
+def pick_device(rank: int, colocated: bool, backend: str, mode: str = "fedavg") -> torch.device:
     if backend == "torch" or not torch.cuda.is_available():
         return torch.device("cpu")
     n = torch.cuda.device_count()
     local = int(os.environ.get("LOCAL_RANK", rank))
-    idx = local % n if colocated else max(local - 1, 0) % n
+    # dedicated federator: it shares GPU 0 with client 1, except in MD-GAN mode where it runs the
+    # generator for every client and gets a GPU of its own (RCCL needs one rank per device)
+    idx = local % n if (colocated or mode == "mdgan") else max(local - 1, 0) % n
     torch.cuda.set_device(idx)
     return torch.device("cuda", idx)
 
@@ -130,19 +133,24 @@ def pick_device(rank: int, colocated: bool, backend: str) -> torch.device:
 def run_rank(rank: int, args) -> None:
     """One process of the federation (the reference ``run()``, `Server/dtds/distributed.py:838-891`)."""
     from .fed.runtime import FedRuntime
+    from .fed.mdgan import MDGANRuntime
     from .parallel.comm import Comm
     world = args.world_size
     colocated = args.colocated
-    device = pick_device(rank, colocated, args.backend)
+    device = pick_device(rank, colocated, args.backend, args.mode)
     if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
         torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
     client_ranks = list(range(world)) if colocated else list(range(1, world))
     data_backend = args.data_backend
     if data_backend == "auto":
-        data_backend = "nccl" if (device.type == "cuda" and colocated) else "gloo"
+        if args.mode == "mdgan":
+            data_backend = "nccl" if (device.type == "cuda" and world <= torch.cuda.device_count()) else "gloo"
+        else:
+            data_backend = "nccl" if (device.type == "cuda" and colocated) else "gloo"
     comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
     try:
-        rt = FedRuntime(fed_config_from_args(args), comm, device, federator=0)
+        cls = MDGANRuntime if args.mode == "mdgan" else FedRuntime
+        rt = cls(fed_config_from_args(args), comm, device, federator=0)
         rt.initialize()
         rt.fit()
         comm.barrier()

@@ -82,6 +82,7 @@ class FedConfig:
     metrics_log: Optional[str] = None
     drop_client_prob: float = 0.0           # fault injection: a client misses a round with this probability
     mode: str = "fedavg"                    # fedavg | mdgan
+    e_interval: int = 1                     # fedavg: local epochs per aggregation; mdgan: D-swap period
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
 
 
@@ -344,7 +345,10 @@ class FedRuntime:
                 self.engine.train_epoch(self.cfg.use_graph)
         self._epoch_done = epoch + 1
         with self.timer.phase("aggregate", self.device):
-            self.aggregate(alive if self.cfg.drop_client_prob > 0 else None)
+            # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
+            # local epochs between aggregations (1 = aggregate every round, the reference behaviour)
+            if (epoch + 1) % max(int(self.cfg.e_interval), 1) == 0:
+                self.aggregate(alive if self.cfg.drop_client_prob > 0 else None)
         with self.timer.phase("sample_dump", self.device):
             self.sample_round(epoch)
         if self.device.type == "cuda":
@@ -352,13 +356,17 @@ class FedRuntime:
         dt = time.time() - t0
         return dt
 
+    def round_losses(self):
+        """(loss_d, loss_g) of the last step, as the federator reports them."""
+        return self.engine.losses() if self.is_client else (float("nan"), float("nan"))
+
     def fit(self):
         cfg = self.cfg
         for ep in range(self.start_epoch, cfg.epochs):
             dt = self.run_round(ep)
             self.round_times.append(dt)
             if self.is_fed:
-                ld, lg = self.engine.losses() if self.is_client else (float("nan"), float("nan"))
+                ld, lg = self.round_losses()
                 _log(cfg, self.rank, f"EPOCH {ep}: loss_d:{ld:>6.2f}   loss_g:{lg:>6.2f}   round time: {dt:.3f} sec")
                 if self.metrics is not None:
                     self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,

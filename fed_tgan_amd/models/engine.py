@@ -482,6 +482,12 @@ class CTGANEngine:
 
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
+        self._g_dlogits()
+        self._g_backward()
+        self._g_adam()
+
+    def _g_dlogits(self):
+        """G loss (-mean D(fake) + cond CE) back to the generator's logits: self.dlogits."""
         o, B, nP = self.ops, self.B, self.nP
         L = len(self.ddims)
         fk = slice(0, nP)
@@ -493,6 +499,10 @@ class CTGANEngine:
         dx = self.gbuf.view(B, self.Din)
         o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
                      self.opt, self.dlogits, self.metrics[3:4], self.cfg.tau)
+
+    def _g_backward(self):
+        """self.dlogits -> G parameter gradients (self.gradG), through the saved forward buffers."""
+        o = self.ops
         # generator backward: the dH chain on the main lane, weight gradients on side lanes
         Lg = len(self.gdims)
         with self._lane(1):
@@ -516,21 +526,56 @@ class CTGANEngine:
                 x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
                 o.gemm(self.da[i], x, dW, ta=True)
         self._join(1, 2, 3)
+
+    def _g_adam(self):
         b1, b2 = self.cfg.betas
-        o.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
-               self.cfg.l2scale, last_in_step=True)
+        self.ops.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
+                      self.cfg.l2scale, last_in_step=True)
+
+    # ================================================================= split roles (MD-GAN)
+    G_BUFFERS = ("H", "abuf", "nhat", "bn_mean", "bn_invstd", "da", "logits", "dlogits", "dH")
+
+    def new_g_buffers(self) -> Dict[str, object]:
+        """A private set of the generator's forward/backward buffers (one per remote client batch
+        on an MD-GAN server, so K batches can be in flight between forward and backward)."""
+        dev, B = self.device, self.B
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        return {"H": _padded_rows(B, self.Hw, dev), "abuf": [z(B, g) for g in self.gdims],
+                "nhat": [z(B, g) for g in self.gdims], "bn_mean": [z(g) for g in self.gdims],
+                "bn_invstd": [z(g) for g in self.gdims], "da": [z(B, g) for g in self.gdims],
+                "logits": _padded_rows(B, self.Dd, dev), "dlogits": _padded_rows(B, self.Dd, dev),
+                "dH": _padded_rows(B, self.Hw, dev)}
+
+    @contextlib.contextmanager
+    def use_g_buffers(self, bufs: Dict[str, object]):
+        saved = {k: getattr(self, k) for k in self.G_BUFFERS}
+        for k in self.G_BUFFERS:
+            setattr(self, k, bufs[k])
+        try:
+            yield
+        finally:
+            for k, v in saved.items():
+                setattr(self, k, v)
+
+    def g_input_view(self, H=None) -> torch.Tensor:
+        """The generator input block [z | c] of an H buffer (written by the sampler)."""
+        return (self.H if H is None else H)[:, self.off[0]:]
 
     def _one_step(self):
         if hasattr(self.ops, "begin_step"):
             self.ops.begin_step(self)
-        # the G phase's sampling + generator forward only depends on G (unchanged by the D
-        # step), so it runs on lane 3 while the D update runs on the main lane
-        self._d_prepare()
-        with self._lane(3):
-            self._g_prepare()
-        self._d_update()
-        self._join(3)
-        self._g_update()
+        if self.lanes is None:      # the reference order: D step, then G step
+            self._d_step()
+            self._g_step()
+        else:
+            # the G phase's sampling + generator forward only depends on G (unchanged by the D
+            # step), so it runs on lane 3 while the D update runs on the main lane
+            self._d_prepare()
+            with self._lane(3):
+                self._g_prepare()
+            self._d_update()
+            self._join(3)
+            self._g_update()
         if hasattr(self.ops, "end_step"):
             self.ops.end_step(self)
 

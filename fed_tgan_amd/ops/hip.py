@@ -51,6 +51,7 @@ def _effective_splits(K: int, sk: int, kc: int) -> int:
 
 class HipOps:
     name = "hip"
+    adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
 
     def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16"):
         self.L = native.require()

@@ -24,6 +24,7 @@ EPI_RELU = 3
 
 
 class TorchOps:
+    adam_counts_steps = True     # eager Adam bumps its step counter (the HIP sampler does it there)
     name = "torch"
 
     # ------------------------------------------------------------------ GEMM

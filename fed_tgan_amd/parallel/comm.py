@@ -41,6 +41,7 @@ class Comm:
         self.timeout = datetime.timedelta(seconds=timeout_s)
         self.ctrl = None
         self.data = None
+        self.p2p = None
         self.initialized = False
         if world_size > 1 and init:
             self._init(ip, port)
@@ -171,6 +172,38 @@ class Comm:
                 dist.recv(host, src=src, group=self.ctrl)
                 flat.copy_(host)
         return flat
+
+    # ------------------------------------------------------------------ point to point (MD-GAN)
+    def init_p2p(self):
+        """Collective (every rank): the point-to-point group of the split (MD-GAN) mode -- RCCL over
+        all ranks when the data plane is RCCL, else the gloo control plane."""
+        if self.world_size == 1:
+            self.p2p = None
+        elif self.data_backend == "nccl":
+            self.p2p = dist.new_group(ranks=list(range(self.world_size)), backend="nccl", timeout=self.timeout)
+        else:
+            self.p2p = self.ctrl
+        return self.p2p
+
+    def exchange(self, sends: Sequence[tuple] = (), recvs: Sequence[tuple] = ()):
+        """Batched point-to-point: ``sends`` = [(tensor, dst)], ``recvs`` = [(tensor, src)]; all
+        posted together, returns when every transfer is complete.  Over gloo, device tensors are
+        staged through host memory; over RCCL they move GPU to GPU (xGMI)."""
+        if not sends and not recvs:
+            return
+        nccl = self.data_backend == "nccl"
+        host = (lambda t: t) if nccl else (lambda t: t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t)
+        s_bufs = [(host(t.contiguous()), d) for t, d in sends]
+        r_bufs = [(t if (nccl or t.device.type == "cpu") and t.is_contiguous() else
+                   torch.empty(t.shape, dtype=t.dtype, device=t.device if nccl else "cpu"), t, src)
+                  for t, src in recvs]
+        ops = [dist.P2POp(dist.isend, b, d, group=self.p2p) for b, d in s_bufs]
+        ops += [dist.P2POp(dist.irecv, b, src, group=self.p2p) for b, _, src in r_bufs]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for b, t, _ in r_bufs:
+            if b is not t:
+                t.copy_(b)
 
     def destroy(self):
         if self.initialized and dist.is_initialized():

@@ -113,3 +113,9 @@ def test_cli_reference_topology_gloo(tmp_path):
     sim = pd.read_csv(tmp_path / "Intrusion_statistical_similarity_analysis.csv")
     assert list(sim.columns) == ["Epoch_No.", "Avg_JSD", "Avg_WD", "time_stamp"]
     assert sim["Avg_JSD"].between(0, 1).all() and np.isfinite(sim["Avg_WD"]).all()
+
+
+def test_local_epochs_between_aggregations(tmp_path):
+    """-E_interval 2: clients train two local epochs between weighted aggregations."""
+    rt = run_local_emulation(_cfg(tmp_path, epochs=3, e_interval=2), 2, backend="torch", device=torch.device("cpu"))
+    assert len(rt.round_times) == 3
