@@ -152,15 +152,8 @@ class MDGANRuntime(FedRuntime):
     # ------------------------------------------------------------------ rounds
     def run_round(self, epoch: int) -> float:
         dt = self._run_round(epoch)
-        # every rank joins: the clients' last-step D / G losses, averaged for the server's log
-        m = self.engine.metrics.detach().cpu().double() if self.is_client else torch.zeros(4, dtype=torch.float64)
-        self.comm.all_reduce_cpu(m)
-        self._md_losses = m / max(self.comm.n_clients, 1)
+        self._sync_losses()
         return dt
-
-    def round_losses(self):
-        m = self._md_losses
-        return float(m[0] + m[1]), float(m[2] + m[3])
 
     def _run_round(self, epoch: int) -> float:
         t0 = time.time()

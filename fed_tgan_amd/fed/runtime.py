@@ -147,6 +147,7 @@ class FedRuntime:
         self.name = cfg.spec.name
         self.n_sample = cfg.n_sample or cfg.spec.n_sample
         self._writer = None
+        self._losses = None
         self.timer = PhaseTimer(sync=True)    # device-synchronised phase boundaries (3 per round)
         self.round_times: List[float] = []
         self.start_epoch = 0
@@ -354,10 +355,24 @@ class FedRuntime:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = time.time() - t0
+        self._sync_losses()
         return dt
+
+    def _sync_losses(self):
+        """Collective when the federator holds no data: the clients' last-step losses, averaged."""
+        c = self.comm
+        if c.world_size == 1 or self.federator in c.client_ranks:
+            self._losses = None
+            return
+        m = self.engine.metrics.detach().cpu().double() if self.is_client else torch.zeros(4, dtype=torch.float64)
+        c.all_reduce_cpu(m)
+        self._losses = m / max(c.n_clients, 1)
 
     def round_losses(self):
         """(loss_d, loss_g) of the last step, as the federator reports them."""
+        m = getattr(self, "_losses", None)
+        if m is not None:
+            return float(m[0] + m[1]), float(m[2] + m[3])
         return self.engine.losses() if self.is_client else (float("nan"), float("nan"))
 
     def fit(self):
