@@ -62,6 +62,18 @@ def stat_sim(real: pd.DataFrame, fake: pd.DataFrame, cat_cols: Sequence[str]) ->
     return float(np.mean(jsd)) if jsd else float("nan"), float(np.mean(wd)) if wd else float("nan")
 
 
+def column_similarity(real: pd.DataFrame, fake: pd.DataFrame, cat_cols: Sequence[str]) -> pd.DataFrame:
+    """Per-column table behind :func:`stat_sim`: JSD for categorical, normalised W1 for continuous."""
+    cat_cols = set(cat_cols or [])
+    rows = []
+    for col in real.columns:
+        if col in cat_cols:
+            rows.append([col, "categorical", "JSD", column_jsd(real[col], fake[col])])
+        else:
+            rows.append([col, "continuous", "WD", column_wd(real[col], fake[col])])
+    return pd.DataFrame(rows, columns=["column", "type", "metric", "value"])
+
+
 def stat_sim_normalize(real_path: str, fake_path: str, cat_cols=None) -> Tuple[float, float]:
     """Path-based entry point with the reference signature."""
     return stat_sim(pd.read_csv(real_path), pd.read_csv(fake_path), cat_cols or [])

@@ -187,6 +187,28 @@ class VGMTransformer:
     def get_information(self):
         return self.bank, self.components, self.meta
 
+    # --------------------------------------------------------------------- persistence
+    def to_dict(self) -> dict:
+        """Plain-Python state (loadable with ``torch.load(..., weights_only=True)`` / JSON)."""
+        def py(v):
+            if isinstance(v, (list, tuple)):
+                return [py(x) for x in v]
+            if isinstance(v, np.generic):
+                return v.item()
+            return v
+        meta = [{k: py(v) for k, v in m.items()} for m in self.meta]
+        return {"n_clusters": self.n_clusters, "eps": self.eps, "meta": meta, "bank": self.bank.to_dict(),
+                "components": np.asarray(self.components, dtype=bool).tolist()}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "VGMTransformer":
+        t = cls(int(d["n_clusters"]), float(d["eps"]))
+        t.meta = [dict(m) for m in d["meta"]]
+        t.bank = VGMBank.from_dict(d["bank"])
+        t.components = np.asarray(d["components"], dtype=bool)
+        t._build_info()
+        return t
+
     def set_model(self, bank: VGMBank, components: np.ndarray) -> None:
         self.bank = bank
         self.components = np.asarray(components, dtype=bool)

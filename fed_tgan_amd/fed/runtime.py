@@ -82,6 +82,7 @@ class FedConfig:
     metrics_log: Optional[str] = None
     drop_client_prob: float = 0.0           # fault injection: a client misses a round with this probability
     mode: str = "fedavg"                    # fedavg | mdgan
+    grad_flow: bool = False                 # record per-layer mean |grad| each round (utils/gradflow.py)
     e_interval: int = 1                     # fedavg: local epochs per aggregation; mdgan: D-swap period
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
 
@@ -148,6 +149,10 @@ class FedRuntime:
         self.n_sample = cfg.n_sample or cfg.spec.n_sample
         self._writer = None
         self._losses = None
+        self.gradflow = None
+        if cfg.grad_flow and comm.is_client and comm.client_index == 0:
+            from ..utils.gradflow import GradFlow
+            self.gradflow = GradFlow()
         self.timer = PhaseTimer(sync=True)    # device-synchronised phase boundaries (3 per round)
         self.round_times: List[float] = []
         self.start_epoch = 0
@@ -344,6 +349,8 @@ class FedRuntime:
         with self.timer.phase("train", self.device):
             if self.is_client and alive[c.client_index]:
                 self.engine.train_epoch(self.cfg.use_graph)
+                if self.gradflow is not None:
+                    self.gradflow.update(self.engine)
         self._epoch_done = epoch + 1
         with self.timer.phase("aggregate", self.device):
             # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
@@ -389,6 +396,11 @@ class FedRuntime:
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
                 self.save_checkpoint(ep + 1)
         self.flush_writes()
+        if self.gradflow is not None:
+            d = os.path.join(cfg.out_dir, "reports")
+            os.makedirs(d, exist_ok=True)
+            self.gradflow.save_csv(os.path.join(d, "grad_flow.csv"))
+            self.gradflow.plot(d)
         if self.is_fed:
             self.write_timestamps()
             if cfg.dump_real:

@@ -64,7 +64,8 @@ class CTGANSynthesizer(BaseSynthesizer):
                            batch_size=self.batch_size, l2scale=self.l2scale, precision=self.precision)
         self.engine = CTGANEngine(self.transformer.layout, cfg, self.device, backend=self.backend, seed=self.seed)
         self.engine.set_training_data(enc)
-        self.engine.set_generation_tables(CondTables.from_encoded(enc, self.transformer.layout), self.transformer)
+        self._cond_counts = CondTables.span_counts(enc, self.transformer.layout)
+        self.engine.set_generation_tables(CondTables(self.transformer.layout, self._cond_counts), self.transformer)
         for i in range(self.epochs):
             t = time.time()
             self.engine.train_epoch()
@@ -82,9 +83,28 @@ class CTGANSynthesizer(BaseSynthesizer):
         return self.engine.generate_encoded(n).cpu().numpy()
 
     def save(self, path: str):
-        """Model bundle (the reference's unused ``save_model``, `Server/dtds/distributed.py:560-563`)."""
-        torch.save({"G": self.engine.g_state_dict(), "D": self.engine.d_state_dict(),
-                    "layout": self.transformer.output_info, "bank": self.transformer.bank.to_dict(),
-                    "components": self.transformer.components.tolist(), "meta": self.transformer.meta,
-                    "config": {"embedding_dim": self.embedding_dim, "gen_dim": self.gen_dim, "dis_dim": self.dis_dim,
-                               "batch_size": self.batch_size}}, path)
+        """Model bundle (the reference's unused ``save_model``, `Server/dtds/distributed.py:560-563`,
+        pickles ``[G, cond, transformer, batch_size, embedding_dim]``).  Here: plain tensors and
+        Python containers only, so :meth:`load` reads it with ``weights_only=True``."""
+        eng = self.engine
+        torch.save({"G": eng.g_state_dict(), "D": eng.d_state_dict(), "transformer": self.transformer.to_dict(),
+                    "cond_counts": torch.as_tensor(self._cond_counts),
+                    "config": {"embedding_dim": self.embedding_dim, "gen_dim": list(self.gen_dim),
+                               "dis_dim": list(self.dis_dim), "batch_size": self.batch_size, "l2scale": self.l2scale,
+                               "epochs": self.epochs}}, path)
+
+    @classmethod
+    def load(cls, path: str, device: Optional[str] = None, backend: str = "auto") -> "CTGANSynthesizer":
+        blob = torch.load(path, map_location="cpu", weights_only=True)
+        c = blob["config"]
+        syn = cls(embedding_dim=c["embedding_dim"], gen_dim=c["gen_dim"], dis_dim=c["dis_dim"], l2scale=c["l2scale"],
+                  batch_size=c["batch_size"], epochs=c["epochs"], device=device, backend=backend, verbose=False)
+        syn.transformer = VGMTransformer.from_dict(blob["transformer"])
+        cfg = EngineConfig(embedding_dim=syn.embedding_dim, gen_dims=syn.gen_dim, dis_dims=syn.dis_dim,
+                           batch_size=syn.batch_size, l2scale=syn.l2scale, precision=syn.precision)
+        syn.engine = CTGANEngine(syn.transformer.layout, cfg, syn.device, backend=backend)
+        syn.engine.load_g_state_dict(blob["G"])
+        syn.engine.load_d_state_dict(blob["D"])
+        syn._cond_counts = blob["cond_counts"].numpy()
+        syn.engine.set_generation_tables(CondTables(syn.transformer.layout, syn._cond_counts), syn.transformer)
+        return syn
