@@ -142,7 +142,8 @@ void launch_sample(const SampleArgs& a, hipStream_t stream) {
 //   element-parallel: Gumbel-perturbed logits (or tanh) into an LDS row image
 //   span-parallel   : one lane per softmax span reduces (max, sum) from LDS
 //   element-parallel: normalise and store
-constexpr int ACT_WAVES = 4;
+constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
+constexpr size_t LDS_BYTES = 160 * 1024;
 
 struct ActSmem {
   int* elem;    // [D]  element -> span
@@ -150,7 +151,7 @@ struct ActSmem {
   int* start;   // [S]
   int* width;   // [S]
   int* cidx;    // [S]
-  float* rows;  // [ACT_WAVES][D + 2S]
+  float* rows;  // [waves][D + 2S]
 };
 
 __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float* smem) {
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   extern __shared__ float act_smem[];
   const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int r = blockIdx.x * ACT_WAVES + wv;
+  const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
   if (r >= rows) return;
   const int D = sp.dim, S = sp.n_span;
   float* v = t.rows + (size_t)wv * (D + 2 * S);
@@ -215,15 +216,31 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   }
 }
 
-static size_t act_smem_bytes(const SpanTables& sp) {
-  return (size_t)(sp.dim + 4 * sp.n_span) * sizeof(int) + (size_t)ACT_WAVES * (sp.dim + 2 * sp.n_span) * sizeof(float);
+static size_t act_smem_bytes(const SpanTables& sp, int waves) {
+  return (size_t)(sp.dim + 4 * sp.n_span) * sizeof(int) + (size_t)waves * (sp.dim + 2 * sp.n_span) * sizeof(float);
+}
+
+// wide tables (hundreds of columns, thousands of spans) get fewer rows per workgroup so the
+// tables + row images still fit the 160 KiB LDS
+static int act_waves(const SpanTables& sp) {
+  for (int w = ACT_WAVES; w > 1; w /= 2)
+    if (act_smem_bytes(sp, w) <= LDS_BYTES) return w;
+  return 1;
+}
+
+template <typename K>
+static void allow_big_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024) hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(activate_kernel, dim3((rows + ACT_WAVES - 1) / ACT_WAVES), dim3(ACT_WAVES * 64),
-                     act_smem_bytes(sp), stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id);
+  const int nw = act_waves(sp);
+  const size_t lds = act_smem_bytes(sp, nw);
+  allow_big_lds(activate_kernel, lds);
+  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id);
 }
 
 // backward of the activation + fused conditional cross-entropy, one wave per row
@@ -236,7 +253,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
   extern __shared__ float act_smem[];
   const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int r = blockIdx.x * ACT_WAVES + wv;
+  const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
   if (r >= rows) return;
   const int D = sp.dim, S = sp.n_span;
   float* gy = t.rows + (size_t)wv * (D + 2 * S);
@@ -300,12 +317,14 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
                        hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + ACT_WAVES - 1) / ACT_WAVES), dim3(ACT_WAVES * 64),
-                     act_smem_bytes(sp), stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
+  const int nw = act_waves(sp);
+  const size_t lds = act_smem_bytes(sp, nw);
+  allow_big_lds(act_bwd_ce_kernel, lds);
+  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
                      1.f / tau, loss);
 }
 
-size_t activation_smem_bytes(const SpanTables& sp) { return act_smem_bytes(sp); }
+size_t activation_smem_bytes(const SpanTables& sp) { return act_smem_bytes(sp, act_waves(sp)); }
 
 // ============================================================================ gradient penalty pieces
 // one wave per row

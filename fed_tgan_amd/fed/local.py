@@ -16,6 +16,7 @@ from typing import Any, List, Optional
 import torch
 
 from ..parallel.comm import Comm
+from ..utils.devsync import device_sync
 
 
 class LocalGroup:
@@ -90,7 +91,7 @@ class ThreadComm(Comm):
     def weighted_all_reduce(self, flat, weight: float):
         """sum_i w_i * flat_i: every rank posts (buffer, weight); rank 0 accumulates on the device."""
         if flat.is_cuda:
-            torch.cuda.synchronize(flat.device)
+            device_sync(flat.device)
         self.g.slots[self.rank] = (flat, float(weight))
         self.g.wait()
         if self.rank == 0:
@@ -99,12 +100,12 @@ class ThreadComm(Comm):
                 if w != 0.0:
                     acc.add_(buf, alpha=w)
             if flat.is_cuda:
-                torch.cuda.synchronize(flat.device)
+                device_sync(flat.device)
             self.g.result = acc
         self.g.wait()
         flat.copy_(self.g.result)
         if flat.is_cuda:
-            torch.cuda.synchronize(flat.device)
+            device_sync(flat.device)
         self.g.wait()
         return flat
 

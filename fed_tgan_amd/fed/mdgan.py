@@ -53,6 +53,7 @@ import numpy as np
 import torch
 
 from .runtime import FedRuntime, _log
+from ..utils.devsync import device_sync
 
 
 class MDGANRuntime(FedRuntime):
@@ -110,7 +111,7 @@ class MDGANRuntime(FedRuntime):
         c.exchange(sends=[(eng.g_input_view(), self.federator)])
         c.exchange(recvs=[(eng.logits, self.federator)])
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            device_sync(self.device)
         return time.perf_counter() - t0
 
     def _client_step(self):
@@ -172,7 +173,7 @@ class MDGANRuntime(FedRuntime):
         with self.timer.phase("sample_dump", self.device):
             self.sample_round(epoch)
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            device_sync(self.device)
         return time.time() - t0
 
     def fit(self):

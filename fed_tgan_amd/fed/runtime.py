@@ -52,6 +52,7 @@ from ..models.engine import CTGANEngine, EngineConfig
 from ..models.samplers import CondTables
 from ..parallel.comm import Comm
 from ..utils.metrics import MetricsLog, PhaseTimer
+from ..utils.devsync import device_sync
 from .stats import (aggregation_weights, continuous_client_distances, merge_categorical_metas,
                     normalise_over_clients, uniform_weights, wasserstein_1d)
 
@@ -360,7 +361,7 @@ class FedRuntime:
         with self.timer.phase("sample_dump", self.device):
             self.sample_round(epoch)
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            device_sync(self.device)
         dt = time.time() - t0
         self._sync_losses()
         return dt

@@ -598,6 +598,11 @@ class CTGANEngine:
         self.train_steps(self.steps_per_epoch, use_graph)
 
     def _capture(self):
+        from ..utils.devsync import CAPTURE_LOCK
+        with CAPTURE_LOCK:      # no device-wide sync from another client thread meanwhile
+            self._capture_locked()
+
+    def _capture_locked(self):
         # warm up on a side stream (allocator / lazy init), then capture one step
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))

@@ -13,6 +13,7 @@ import time
 from typing import Dict
 
 import torch
+from .devsync import device_sync
 
 
 class PhaseTimer:
@@ -24,13 +25,13 @@ class PhaseTimer:
     @contextlib.contextmanager
     def phase(self, name: str, device=None):
         if self.sync and device is not None and getattr(device, "type", "") == "cuda":
-            torch.cuda.synchronize(device)
+            device_sync(device)
         t = time.perf_counter()
         try:
             yield
         finally:
             if self.sync and device is not None and getattr(device, "type", "") == "cuda":
-                torch.cuda.synchronize(device)
+                device_sync(device)
             dt = time.perf_counter() - t
             self.totals[name] = self.totals.get(name, 0.0) + dt
             self._last[name] = dt
