@@ -312,6 +312,47 @@ void write_csv(const std::string& path, const Tensor& values, std::vector<std::s
   fedtgan::write_csv_file(path, values.data_ptr<double>(), values.size(0), cols, names, k, voc, (int)threads);
 }
 
+void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Tensor& col_kind, const Tensor& col_pos,
+                const Tensor& col_aux, const Tensor& col_span, const Tensor& col_lut_n, const Tensor& consts, const Tensor& means,
+                const Tensor& prec, const Tensor& stds, const Tensor& vrank, const Tensor& lut, int64_t seed,
+                int64_t stream) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.stride(1) == 1, "vgm_encode: x");
+  check_f32_2d(out, "out");
+  TORCH_CHECK(opt.is_cuda() && opt.scalar_type() == at::kInt && opt.is_contiguous() && opt.size(0) == x.size(0),
+              "vgm_encode: opt");
+  const int64_t n_cols = x.size(1);
+  for (const Tensor* t : {&col_kind, &col_pos, &col_aux, &col_span, &col_lut_n})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() == n_cols && t->is_contiguous(),
+                "vgm_encode: column tables");
+  for (const Tensor* t : {&consts, &means, &prec, &stds})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == vrank.numel(),
+                "vgm_encode: bank tables");
+  TORCH_CHECK(vrank.scalar_type() == at::kInt && lut.scalar_type() == at::kInt && lut.is_contiguous(), "vgm_encode");
+  fedtgan::VgmEncodeArgs a{};
+  a.x = x.data_ptr<double>();
+  a.ldx = (int)x.stride(0);
+  a.n_rows = (int)x.size(0);
+  a.n_cols = (int)n_cols;
+  a.out = fp(out);
+  a.ldo = ld_of(out);
+  a.opt = opt.data_ptr<int>();
+  a.n_span = (int)opt.size(1);
+  a.col_kind = col_kind.data_ptr<int>();
+  a.col_pos = col_pos.data_ptr<int>();
+  a.col_aux = col_aux.data_ptr<int>();
+  a.col_span = col_span.data_ptr<int>();
+  a.col_lut_n = col_lut_n.data_ptr<int>();
+  a.consts = consts.data_ptr<float>();
+  a.means = means.data_ptr<float>();
+  a.prec = prec.data_ptr<float>();
+  a.stds = stds.data_ptr<float>();
+  a.vrank = vrank.data_ptr<int>();
+  a.lut = lut.data_ptr<int>();
+  a.seed = (uint64_t)seed;
+  a.stream = (uint32_t)stream;
+  fedtgan::launch_vgm_encode(a, cur_stream());
+}
+
 std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
 }  // namespace
@@ -351,6 +392,10 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def("rng_bump(Tensor(a!) ctr) -> ()");
   m.def(
+      "vgm_encode(Tensor x, Tensor(a!) out, Tensor(b!) opt, Tensor col_kind, Tensor col_pos, Tensor col_aux, "
+      "Tensor col_span, Tensor col_lut_n, Tensor consts, Tensor means, Tensor prec, Tensor stds, Tensor vrank, Tensor lut, int seed, "
+      "int stream) -> ()");
+  m.def(
       "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
       "int threads) -> ()");
   m.def("py_float(float x) -> str", &py_float);
@@ -370,6 +415,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("adam", &adam);
   m.impl("sample_decode", &sample_decode);
   m.impl("rng_bump", &rng_bump);
+  m.impl("vgm_encode", &vgm_encode);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CPU, m) { m.impl("write_csv", &write_csv); }

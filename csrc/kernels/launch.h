@@ -131,4 +131,28 @@ void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
 
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream);
 
+// VGM encode (kernels/vgm.hip): one thread per (row, column) cell of the label-encoded table
+struct VgmEncodeArgs {
+  const double* x;      // [n_rows, ldx] label codes / continuous values
+  int ldx, n_rows, n_cols;
+  float* out;           // [n_rows, ldo] encoded matrix (zero-filled by the caller)
+  int ldo;
+  int* opt;             // [n_rows, n_span] option index per conditional span
+  int n_span;
+  const int* col_kind;  // 0 continuous, 1 categorical
+  const int* col_pos;   // output column of the alpha / first one-hot slot
+  const int* col_aux;   // continuous: bank row; categorical: LUT offset
+  const int* col_span;  // conditional span of the column's one-hot
+  const int* col_lut_n; // categorical: LUT length (codes are clamped into it)
+  const float* consts;  // [n_cont, 10] constant part of the weighted log prob
+  const float* means;   // [n_cont, 10]
+  const float* prec;    // [n_cont, 10] precision Cholesky (1 / sigma)
+  const float* stds;    // [n_cont, 10]
+  const int* vrank;     // [n_cont, 10] position among the valid modes, -1 if invalid
+  const int* lut;       // categorical code -> option position
+  uint64_t seed;
+  uint32_t stream;
+};
+void launch_vgm_encode(const VgmEncodeArgs& a, hipStream_t stream);
+
 }  // namespace fedtgan

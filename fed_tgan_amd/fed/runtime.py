@@ -83,6 +83,7 @@ class FedConfig:
     metrics_log: Optional[str] = None
     drop_client_prob: float = 0.0           # fault injection: a client misses a round with this probability
     mode: str = "fedavg"                    # fedavg | mdgan
+    device_encode: bool = True              # GPU: VGM-encode with the HIP kernel (csrc/kernels/vgm.hip)
     grad_flow: bool = False                 # record per-layer mean |grad| each round (utils/gradflow.py)
     e_interval: int = 1                     # fedavg: local epochs per aggregation; mdgan: D-swap period
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
@@ -237,7 +238,7 @@ class FedRuntime:
                                                   self.components)
         lay = self.transformer.layout
         if self.is_client:
-            self.train_matrix = self.transformer.transform(self.encoded, np.random.default_rng(cfg.seed + self.rank))
+            self.train_matrix = self._encode_training_table()
         # ---- D. weights
         if cfg.aggregation == "uniform":
             self.weights = uniform_weights(c.n_clients)
@@ -248,7 +249,8 @@ class FedRuntime:
         maxw = int(lay.cond_width.max()) if lay.n_col else 0
         cnt = torch.zeros(lay.n_col, maxw, dtype=torch.float64)
         if self.is_client:
-            cnt += torch.as_tensor(CondTables.span_counts(self.train_matrix, lay))
+            cnt += torch.as_tensor(self.train_matrix.counts if hasattr(self.train_matrix, "counts")
+                                   else CondTables.span_counts(self.train_matrix, lay))
         c.all_reduce_cpu(cnt)
         self.gen_cond = CondTables(lay, cnt.numpy())
         # ---- engine + F. initial weights
@@ -266,6 +268,18 @@ class FedRuntime:
         self.csv_cols = csv_columns(merged, self.vocabs) if not spec.date_dic else None
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
+
+    def _encode_training_table(self):
+        """VGM-encode the local table: on the GPU with the HIP kernel (matrix and row lists stay
+        resident), else with the numpy reference path."""
+        cfg = self.cfg
+        if self.device.type == "cuda" and cfg.backend in ("auto", "hip") and cfg.device_encode:
+            from ..features.encode_gpu import encode_on_device
+            try:
+                return encode_on_device(self.transformer, self.encoded, self.device, seed=cfg.seed * 131 + self.rank)
+            except ValueError:
+                pass   # e.g. non-integer category codes: host path below
+        return self.transformer.transform(self.encoded, np.random.default_rng(cfg.seed + self.rank))
 
     def _global_gmm(self, banks: List[VGMBank], rows: List[int]):
         return federate_gmm(banks, rows, self.cfg, self.device)

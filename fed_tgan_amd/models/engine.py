@@ -311,22 +311,31 @@ class CTGANEngine:
         self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
 
     # ================================================================= data
-    def set_training_data(self, encoded: np.ndarray, rows: RowIndex | None = None, cond: CondTables | None = None):
+    def set_training_data(self, encoded, rows: RowIndex | None = None, cond: CondTables | None = None):
+        """encoded: the host matrix [N, data_dim], or a ``DeviceEncoded`` from the HIP encoder
+        (matrix, row lists and counts already on the device)."""
         lay = self.layout
-        rows = rows or RowIndex(encoded, lay)
-        cond = cond or CondTables.from_encoded(encoded, lay)
         dev = self.device
-        t = {
-            "data": torch.as_tensor(np.ascontiguousarray(encoded, dtype=np.float32), device=dev),
+        dev_enc = hasattr(encoded, "opt") and hasattr(encoded, "rows")
+        if dev_enc:
+            cond = cond or CondTables(lay, encoded.counts)
+            rt = encoded.rows
+            t = {"data": encoded.data.to(dev), "row_offset": rt["row_offset"].to(dev),
+                 "row_count": rt["row_count"].to(dev), "rows": rt["rows"].to(dev)}
+        else:
+            rows = rows or RowIndex(encoded, lay)
+            cond = cond or CondTables.from_encoded(encoded, lay)
+            t = {"data": torch.as_tensor(np.ascontiguousarray(encoded, dtype=np.float32), device=dev),
+                 "row_offset": torch.as_tensor(rows.offset, dtype=torch.int64, device=dev),
+                 "row_count": torch.as_tensor(rows.count, dtype=torch.int64, device=dev),
+                 "rows": torch.as_tensor(rows.rows, dtype=torch.int64, device=dev)}
+        t.update({
             "cdf_log": torch.as_tensor(cond.cdf_log, dtype=torch.float32, device=dev),
             "cdf_emp": torch.as_tensor(cond.cdf_emp, dtype=torch.float32, device=dev),
             "cond_offset": torch.as_tensor(lay.cond_offset, dtype=torch.int32, device=dev),
             "cond_width": torch.as_tensor(lay.cond_width, dtype=torch.int32, device=dev),
             "cond_start": torch.as_tensor(lay.cond_start, dtype=torch.int32, device=dev),
-            "row_offset": torch.as_tensor(rows.offset, dtype=torch.int64, device=dev),
-            "row_count": torch.as_tensor(rows.count, dtype=torch.int64, device=dev),
-            "rows": torch.as_tensor(rows.rows, dtype=torch.int64, device=dev),
-        }
+        })
         self.n_rows = len(encoded)
         self.tables = t
         self.steps_per_epoch = len(encoded) // self.B

@@ -292,3 +292,43 @@ def test_sample_decode_deterministic_argmax(hip):
     torch.cuda.synchronize()
     ref = tr.inverse_transform(X[:rows])
     assert np.allclose(out.cpu().numpy(), ref, rtol=1e-4, atol=1e-3)
+
+
+def test_vgm_encode_matches_host(hip):
+    """HIP VGM encode vs the numpy transform: exact categorical one-hots, exact alpha for the
+    drawn mode, mode frequencies = mean posterior, and device row lists = host RowIndex."""
+    from fed_tgan_amd.features.encode_gpu import encode_on_device
+    from fed_tgan_amd.features.transformer import CONTINUOUS
+    from fed_tgan_amd.models.samplers import CondTables, RowIndex
+    from helpers import small_table
+    _, _, _, _, _, enc, tr, X = small_table(4000, 3)
+    d = encode_on_device(tr, enc, DEV, seed=7)
+    torch.cuda.synchronize()
+    D = d.data.cpu().numpy()
+    assert D.shape == X.shape
+    probs = tr.mode_probs(enc)                                 # [N, n_cont, K]
+    pos, c = 0, 0
+    for j, m in enumerate(tr.meta):
+        if m["type"] == CONTINUOUS:
+            valid = np.nonzero(tr.components[c])[0]
+            nv = len(valid)
+            oh = D[:, pos + 1:pos + 1 + nv]
+            assert np.all(oh.sum(1) == 1.0)
+            k = valid[oh.argmax(1)]
+            mu, sd = tr.bank.means[c][k], tr.bank.stds[c][k]
+            alpha = np.clip((enc[:, j] - mu) / (4 * sd), -0.99, 0.99)
+            assert np.allclose(D[:, pos], alpha, atol=2e-5)
+            freq = oh.mean(0)
+            expect = probs[:, c, valid].mean(0)
+            assert np.abs(freq - expect).max() < 0.03, (j, freq, expect)
+            pos += 1 + nv
+            c += 1
+        else:
+            w = int(m["size"])
+            assert np.array_equal(D[:, pos:pos + w], X[:, pos:pos + w])
+            pos += w
+    host_rows = RowIndex(D, tr.layout)
+    assert np.array_equal(d.rows["row_count"].cpu().numpy(), host_rows.count)
+    assert np.array_equal(d.rows["row_offset"].cpu().numpy(), host_rows.offset)
+    assert np.array_equal(d.rows["rows"].cpu().numpy(), host_rows.rows)
+    assert np.array_equal(d.counts, CondTables.span_counts(D, tr.layout))
