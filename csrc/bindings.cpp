@@ -353,6 +353,45 @@ void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Ten
   fedtgan::launch_vgm_encode(a, cur_stream());
 }
 
+fedtgan::VgmFitArgs fit_args(const Tensor& x, const Tensor& n_rows, const Tensor& means, const Tensor& partial,
+                             int64_t rows_per_block, int64_t nv) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.stride(1) == 1, "vgm fit: x");
+  TORCH_CHECK(n_rows.is_cuda() && n_rows.scalar_type() == at::kInt && n_rows.numel() == x.size(0), "vgm fit: n_rows");
+  TORCH_CHECK(means.scalar_type() == at::kDouble && means.is_contiguous() && means.numel() == x.size(0) * 10,
+              "vgm fit: [n_cols, 10] tables");
+  TORCH_CHECK(rows_per_block > 0, "vgm fit: rows_per_block");
+  const int64_t chunks = (x.size(1) + rows_per_block - 1) / rows_per_block;
+  TORCH_CHECK(partial.scalar_type() == at::kDouble && partial.is_contiguous() &&
+                  partial.numel() == x.size(0) * chunks * nv, "vgm fit: partial must be [n_cols, chunks, ", nv, "]");
+  fedtgan::VgmFitArgs a{};
+  a.x = x.data_ptr<double>();
+  a.ldx = (int)x.stride(0);
+  a.n_cols = (int)x.size(0);
+  a.max_rows = (int)x.size(1);
+  a.rows_per_block = (int)rows_per_block;
+  a.n_rows = n_rows.data_ptr<int>();
+  a.means = means.data_ptr<double>();
+  a.partial = partial.data_ptr<double>();
+  return a;
+}
+
+void vgm_estep(const Tensor& x, const Tensor& n_rows, const Tensor& consts, const Tensor& means, const Tensor& prec,
+               const Tensor& partial, int64_t rows_per_block) {
+  auto a = fit_args(x, n_rows, means, partial, rows_per_block, 31);
+  TORCH_CHECK(consts.scalar_type() == at::kDouble && consts.is_contiguous() && consts.numel() == means.numel() &&
+                  prec.scalar_type() == at::kDouble && prec.is_contiguous() && prec.numel() == means.numel(),
+              "vgm_estep: tables");
+  a.consts = consts.data_ptr<double>();
+  a.prec = prec.data_ptr<double>();
+  fedtgan::launch_vgm_estep(a, cur_stream());
+}
+
+void kmeans_step(const Tensor& x, const Tensor& n_rows, const Tensor& centers, const Tensor& partial,
+                 int64_t rows_per_block) {
+  auto a = fit_args(x, n_rows, centers, partial, rows_per_block, 30);
+  fedtgan::launch_kmeans_step(a, cur_stream());
+}
+
 std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
 }  // namespace
@@ -392,6 +431,10 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def("rng_bump(Tensor(a!) ctr) -> ()");
   m.def(
+      "vgm_estep(Tensor x, Tensor n_rows, Tensor consts, Tensor means, Tensor prec, Tensor(a!) partial, "
+      "int rows_per_block) -> ()");
+  m.def("kmeans_step(Tensor x, Tensor n_rows, Tensor centers, Tensor(a!) partial, int rows_per_block) -> ()");
+  m.def(
       "vgm_encode(Tensor x, Tensor(a!) out, Tensor(b!) opt, Tensor col_kind, Tensor col_pos, Tensor col_aux, "
       "Tensor col_span, Tensor col_lut_n, Tensor consts, Tensor means, Tensor prec, Tensor stds, Tensor vrank, Tensor lut, int seed, "
       "int stream) -> ()");
@@ -416,6 +459,8 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("sample_decode", &sample_decode);
   m.impl("rng_bump", &rng_bump);
   m.impl("vgm_encode", &vgm_encode);
+  m.impl("vgm_estep", &vgm_estep);
+  m.impl("kmeans_step", &kmeans_step);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CPU, m) { m.impl("write_csv", &write_csv); }

@@ -155,4 +155,17 @@ struct VgmEncodeArgs {
 };
 void launch_vgm_encode(const VgmEncodeArgs& a, hipStream_t stream);
 
+// Batched 1-D DP-GMM fit passes (kernels/vgm_fit.hip)
+struct VgmFitArgs {
+  const double* x;       // [n_cols, ldx] centred column data (row r valid for r < n_rows[col])
+  int ldx, n_cols, max_rows, rows_per_block;
+  const int* n_rows;     // [n_cols]
+  const double* consts;  // [n_cols, 10] E-step: constant part of the weighted log prob
+  const double* means;   // [n_cols, 10] E-step: posterior means; k-means: centres
+  const double* prec;    // [n_cols, 10] E-step: precision Cholesky
+  double* partial;       // [n_cols, chunks, 31] (E-step) or [n_cols, chunks, 30] (k-means)
+};
+void launch_vgm_estep(const VgmFitArgs& a, hipStream_t stream);
+void launch_kmeans_step(const VgmFitArgs& a, hipStream_t stream);
+
 }  // namespace fedtgan

@@ -20,6 +20,13 @@ Columns may have different lengths (padded + masked).  Results are returned as a
 :class:`~fed_tgan_amd.features.gmm.VGMBank`.  The fit is statistically equivalent to
 sklearn's (same objective, same init family); it is not bitwise identical because the
 k-means seeding draws differ.
+
+The data passes -- the E-step's responsibilities + sufficient statistics (sum r, sum r x,
+sum r x^2, sum r log r) and the k-means assignment + sums -- run as the HIP kernels of
+``csrc/kernels/vgm_fit.hip`` on a GPU (one read of the data per iteration, fp64), or as
+torch ops on the CPU (the reference implementation of the same statistics).  The M-step,
+lower bound and convergence bookkeeping are [n_cols, K]-sized torch ops shared by both.
+Data are centred per column first (prior mean 0), and the means shifted back at the end.
 """
 from __future__ import annotations
 
@@ -46,13 +53,12 @@ def _pad(columns: Sequence[np.ndarray], device, dtype):
     return X, W
 
 
-def kmeans_1d(X: torch.Tensor, W: torch.Tensor, k: int, gen: torch.Generator, iters: int = 300) -> torch.Tensor:
-    """Batched 1-D k-means (k-means++ seeding, Lloyd). X, W: [n_cols, N]. Returns labels [n_cols, N]."""
+def _kmeans_seed(X: torch.Tensor, W: torch.Tensor, k: int, gen: torch.Generator) -> torch.Tensor:
+    """k-means++ seeding, batched over columns. X, W: [n_cols, N]. Returns centres [n_cols, k]."""
     nc, N = X.shape
     dev = X.device
     counts = W.sum(1)
     centers = torch.zeros(nc, k, dtype=X.dtype, device=dev)
-    # first center: uniform among valid rows
     u = torch.rand(nc, generator=gen, device=dev, dtype=X.dtype)
     idx = torch.clamp((u * counts).long(), max=N - 1)
     centers[:, 0] = X.gather(1, idx.view(-1, 1)).view(-1)
@@ -64,33 +70,86 @@ def kmeans_1d(X: torch.Tensor, W: torch.Tensor, k: int, gen: torch.Generator, it
         pick = torch.searchsorted(cdf.contiguous(), u.contiguous()).clamp(max=N - 1)
         centers[:, c] = X.gather(1, pick).view(-1)
         d2 = torch.minimum(d2, (X - centers[:, c:c + 1]) ** 2 * W)
-    tol = 1e-4 * ((X - (X * W).sum(1, keepdim=True) / counts.view(-1, 1)) ** 2 * W).sum(1) / counts
-    labels = None
-    for _ in range(iters):
-        dist = (X.unsqueeze(2) - centers.unsqueeze(1)) ** 2          # [nc, N, k]
-        labels = dist.argmin(2)
+    return centers
+
+
+class _TorchPasses:
+    """Data passes as torch ops ([n_cols, N, K] intermediates; the CPU path and the oracle)."""
+
+    def __init__(self, X, W):
+        self.X, self.W = X, W
+
+    def kmeans(self, centers):
+        X, W = self.X, self.W
+        k = centers.shape[1]
+        labels = ((X.unsqueeze(2) - centers.unsqueeze(1)) ** 2).argmin(2)
         oh = torch.nn.functional.one_hot(labels, k).to(X.dtype) * W.unsqueeze(2)
-        cnt = oh.sum(1)
-        new = (oh * X.unsqueeze(2)).sum(1) / cnt.clamp_min(1e-300)
-        new = torch.where(cnt > 0, new, centers)
+        xe = X.unsqueeze(2)
+        return oh.sum(1), (oh * xe).sum(1), (oh * xe * xe).sum(1)
+
+    def estep(self, const, means, pc):
+        X, W = self.X, self.W
+        y = (X.unsqueeze(2) - means.unsqueeze(1)) * pc.unsqueeze(1)
+        wlp = const.unsqueeze(1) - 0.5 * y * y
+        log_resp = wlp - torch.logsumexp(wlp, dim=2, keepdim=True)
+        r = torch.exp(log_resp) * W.unsqueeze(2)
+        xe = X.unsqueeze(2)
+        return r.sum(1), (r * xe).sum(1), (r * xe * xe).sum(1), (r * log_resp).sum((1, 2))
+
+
+class _HipPasses:
+    """Data passes as the HIP kernels (one fp64 read of the data per pass)."""
+
+    RPB = 4096   # rows per workgroup
+
+    def __init__(self, X, W):
+        from ..ops import native
+        self.L = native.require()
+        self.X = X.contiguous()
+        self.n = W.sum(1).to(torch.int32)
+        self.chunks = -(-X.shape[1] // self.RPB)
+
+    def kmeans(self, centers):
+        nc, k = centers.shape
+        part = torch.zeros(nc, self.chunks, 3 * k, dtype=torch.float64, device=self.X.device)
+        self.L.kmeans_step(self.X, self.n, centers.contiguous(), part, self.RPB)
+        tot = part.sum(1)
+        return tot[:, :k], tot[:, k:2 * k], tot[:, 2 * k:]
+
+    def estep(self, const, means, pc):
+        nc, k = means.shape
+        part = torch.zeros(nc, self.chunks, 3 * k + 1, dtype=torch.float64, device=self.X.device)
+        self.L.vgm_estep(self.X, self.n, const.contiguous(), means.contiguous(), pc.contiguous(), part, self.RPB)
+        tot = part.sum(1)
+        return tot[:, :k], tot[:, k:2 * k], tot[:, 2 * k:3 * k], tot[:, 3 * k]
+
+
+def kmeans_1d(X: torch.Tensor, W: torch.Tensor, k: int, gen: torch.Generator, iters: int = 300,
+              passes=None) -> torch.Tensor:
+    """Batched 1-D k-means (k-means++ seeding, Lloyd). X, W: [n_cols, N]. Returns centres [n_cols, k]."""
+    passes = passes or _TorchPasses(X, W)
+    counts = W.sum(1)
+    centers = _kmeans_seed(X, W, k, gen)
+    tol = 1e-4 * ((X - (X * W).sum(1, keepdim=True) / counts.view(-1, 1)) ** 2 * W).sum(1) / counts
+    for _ in range(iters):
+        cnt, sums, _ = passes.kmeans(centers)
+        new = torch.where(cnt > 0, sums / cnt.clamp_min(1e-300), centers)
         shift = ((new - centers) ** 2).sum(1)
         centers = new
         if bool((shift <= tol).all()):
             break
-    dist = (X.unsqueeze(2) - centers.unsqueeze(1)) ** 2
-    return dist.argmin(2)
+    return centers
 
 
 class _State:
     pass
 
 
-def _m_step(X, W, resp, pri):
-    eps10 = 10 * torch.finfo(X.dtype).eps
-    r = resp * W.unsqueeze(2)
-    nk = r.sum(1) + eps10                                              # [nc, k]
-    xk = (r * X.unsqueeze(2)).sum(1) / nk
-    sk = (r * (X.unsqueeze(2) - xk.unsqueeze(1)) ** 2).sum(1) / nk + REG_COVAR
+def _m_step(nk_raw, sx, sxx, pri, eps10):
+    """Variational M-step from the sufficient statistics ([n_cols, K])."""
+    nk = nk_raw + eps10
+    xk = sx / nk
+    sk = (sxx - 2.0 * xk * sx + xk * xk * nk_raw).clamp_min(0.0) / nk + REG_COVAR
     s = _State()
     # stick-breaking Beta posteriors
     s.a = 1.0 + nk
@@ -105,20 +164,16 @@ def _m_step(X, W, resp, pri):
     return s
 
 
-def _weighted_log_prob(X, s):
+def _log_prob_const(s):
     dsum = torch.digamma(s.a + s.b)
     logw = torch.digamma(s.a) - dsum
     cum = torch.cumsum(torch.digamma(s.b) - dsum, 1)
     logw = logw + torch.cat([torch.zeros_like(cum[:, :1]), cum[:, :-1]], 1)
-    const = (logw - 0.5 * math.log(2 * math.pi) + torch.log(s.pc) - 0.5 * torch.log(s.dof)
-             + 0.5 * (math.log(2.0) + torch.digamma(0.5 * s.dof) - 1.0 / s.beta))
-    y = (X.unsqueeze(2) - s.means.unsqueeze(1)) * s.pc.unsqueeze(1)
-    return const.unsqueeze(1) - 0.5 * y * y
+    return (logw - 0.5 * math.log(2 * math.pi) + torch.log(s.pc) - 0.5 * torch.log(s.dof)
+            + 0.5 * (math.log(2.0) + torch.digamma(0.5 * s.dof) - 1.0 / s.beta))
 
 
-def _lower_bound(log_resp, W, s):
-    resp = torch.exp(log_resp)
-    ent = -(resp * log_resp * W.unsqueeze(2)).sum((1, 2))
+def _lower_bound(ent, s):
     logdet = torch.log(s.pc) - 0.5 * torch.log(s.dof)
     log_wishart = -(s.dof * logdet + s.dof * 0.5 * math.log(2.0) + torch.lgamma(0.5 * s.dof)).sum(1)
     betaln = torch.lgamma(s.a) + torch.lgamma(s.b) - torch.lgamma(s.a + s.b)
@@ -127,30 +182,35 @@ def _lower_bound(log_resp, W, s):
 
 
 def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int | None = None, device=None,
-                  max_iter: int = MAX_ITER, tol: float = TOL) -> VGMBank:
+                  max_iter: int = MAX_ITER, tol: float = TOL, use_hip: bool | None = None) -> VGMBank:
     dev = torch.device(device) if device is not None else torch.device("cpu")
     dt = torch.float64
     X, W = _pad(columns, dev, dt)
     gen = torch.Generator(device=dev)
     gen.manual_seed(int(seed) if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)).item()))
     counts = W.sum(1)
+    shift = (X * W).sum(1) / counts                       # centre every column (prior mean 0)
+    X = (X - shift.unsqueeze(1)) * W
+    if use_hip is None:
+        use_hip = dev.type == "cuda" and n_clusters == 10
+    passes = _HipPasses(X, W) if use_hip else _TorchPasses(X, W)
     pri = _State()
     pri.wprior = WEIGHT_PRIOR
     pri.beta0 = 1.0
     pri.nu0 = 1.0
-    pri.m0 = (X * W).sum(1) / counts
-    pri.cov0 = ((X - pri.m0.unsqueeze(1)) ** 2 * W).sum(1) / (counts - 1).clamp_min(1)
-    labels = kmeans_1d(X, W, n_clusters, gen)
-    resp = torch.nn.functional.one_hot(labels, n_clusters).to(dt)
-    s = _m_step(X, W, resp, pri)
+    pri.m0 = torch.zeros_like(counts)
+    pri.cov0 = (X ** 2 * W).sum(1) / (counts - 1).clamp_min(1)
+    eps10 = 10 * torch.finfo(dt).eps
+    # init: hard k-means responsibilities -> first M-step
+    centers = kmeans_1d(X, W, n_clusters, gen, passes=passes)
+    s = _m_step(*passes.kmeans(centers), pri, eps10)
     lb = torch.full((X.shape[0],), -float("inf"), dtype=dt, device=dev)
     active = torch.ones(X.shape[0], dtype=torch.bool, device=dev)
     fields = ("a", "b", "beta", "means", "dof", "cov", "pc")
     for _ in range(max_iter):
-        wlp = _weighted_log_prob(X, s)
-        log_resp = wlp - torch.logsumexp(wlp, dim=2, keepdim=True)
-        ns = _m_step(X, W, torch.exp(log_resp), pri)
-        new_lb = _lower_bound(log_resp, W, ns)
+        nk, sx, sxx, rlr = passes.estep(_log_prob_const(s), s.means, s.pc)
+        ns = _m_step(nk, sx, sxx, pri, eps10)
+        new_lb = _lower_bound(-rlr, ns)
         for f in fields:
             cur, nv = getattr(s, f), getattr(ns, f)
             setattr(s, f, torch.where(active.unsqueeze(1), nv, cur))
@@ -160,5 +220,5 @@ def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int
         if not bool(active.any()):
             break
     cpu = lambda t: t.detach().cpu().numpy().astype(np.float64)  # noqa: E731
-    return VGMBank(wc_a=cpu(s.a), wc_b=cpu(s.b), mean_precision=cpu(s.beta), means=cpu(s.means), dof=cpu(s.dof),
-                   covariances=cpu(s.cov))
+    return VGMBank(wc_a=cpu(s.a), wc_b=cpu(s.b), mean_precision=cpu(s.beta),
+                   means=cpu(s.means + shift.unsqueeze(1)), dof=cpu(s.dof), covariances=cpu(s.cov))

@@ -332,3 +332,16 @@ def test_vgm_encode_matches_host(hip):
     assert np.array_equal(d.rows["row_offset"].cpu().numpy(), host_rows.offset)
     assert np.array_equal(d.rows["rows"].cpu().numpy(), host_rows.rows)
     assert np.array_equal(d.counts, CondTables.span_counts(D, tr.layout))
+
+
+def test_vgm_fit_hip_passes_match_torch(hip):
+    """The HIP E-step / k-means passes give the same fit as the torch passes (same seeding)."""
+    from fed_tgan_amd.features.vgm_fit import fit_vgm_torch
+    rng = np.random.default_rng(0)
+    cols = [np.concatenate([rng.normal(0, 1, 3000), rng.normal(8, 0.5, 2000)]), rng.exponential(3, 4500),
+            rng.normal(100, 10, 5000), np.round(rng.lognormal(2, 1, 4000))]
+    a = fit_vgm_torch(cols, seed=1, device=DEV, use_hip=True)
+    b = fit_vgm_torch(cols, seed=1, device=DEV, use_hip=False)
+    for f in ("wc_a", "wc_b", "mean_precision", "means", "dof", "covariances"):
+        np.testing.assert_allclose(getattr(a, f), getattr(b, f), rtol=1e-5, atol=1e-7, err_msg=f)
+    np.testing.assert_allclose(a.weights, b.weights, atol=1e-6)
