@@ -90,7 +90,17 @@ class TablePreprocessor:
         self.output_name = f"{self.file_name}_{self.synthesizer_used}-{timestamp_token()}"
 
         self.integer_columns = detect_integer_columns(frame)
-        df = frame.replace(r" ", np.nan).fillna(EMPTY)
+        # blanks -> NaN -> "empty" (`file_generator.py:115-116`), column by column: numeric columns
+        # without NaNs are untouched, so only object columns and NaN-holding ones are rewritten
+        df = frame.copy()
+        for c in df.columns:
+            col = df[c]
+            if col.dtype == object:
+                col = col.where(col != " ", np.nan)
+            if col.isna().any():
+                df[c] = col.astype(object).where(col.notna(), EMPTY)
+            elif col is not df[c]:
+                df[c] = col
         categorical = list(categorical_list) + [d for d in self.date_columns if d not in categorical_list]
         untouched = set(categorical) | set(self.date_columns)
         for c in df.columns:

@@ -24,13 +24,14 @@ class CategoryVocab:
 
     # --- LabelEncoder-compatible surface -------------------------------------------------
     def transform(self, values: Sequence) -> np.ndarray:
-        vals = np.asarray([str(v) for v in values], dtype=object)
-        # object arrays of python str sort consistently with sorted()
-        idx = np.searchsorted(self.classes_, vals)
-        idx = np.clip(idx, 0, len(self.classes_) - 1)
-        bad = self.classes_[idx] != vals
-        if np.any(bad):
-            raise ValueError(f"y contains previously unseen labels: {sorted(set(vals[bad].tolist()))[:5]}")
+        import pandas as pd
+        vals = pd.Series(values, dtype=object) if not isinstance(values, pd.Series) else values
+        if vals.dtype != object or not all(isinstance(v, str) for v in vals.iloc[:64]):
+            vals = vals.astype(str)
+        idx = pd.Index(self.classes_).get_indexer(vals.to_numpy(dtype=object))   # hash lookup
+        if np.any(idx < 0):
+            bad = vals.to_numpy(dtype=object)[idx < 0]
+            raise ValueError(f"y contains previously unseen labels: {sorted(set(bad.tolist()))[:5]}")
         return idx.astype(np.int64)
 
     def inverse_transform(self, codes: Sequence) -> np.ndarray:
