@@ -81,6 +81,12 @@ class ThreadComm(Comm):
     def max_float(self, x: float) -> float:
         return max(self.all_gather_object(float(x)))
 
+    def gather_rows(self, t, counts, ranks, dst: int = 0):
+        parts = self.all_gather_object(t.cpu())
+        if self.rank != dst:
+            return None
+        return torch.cat([parts[r][:n] for r, n in zip(ranks, counts)])
+
     def gather_bytes(self, payload, dst: int = 0):
         out = self.all_gather_object(payload)
         return out if self.rank == dst else None

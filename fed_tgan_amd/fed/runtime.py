@@ -312,16 +312,18 @@ class FedRuntime:
         colocated = self.federator in c.client_ranks
         samplers = c.client_ranks if colocated else [self.federator]
         share = None
-        if self.rank in samplers:
-            k = samplers.index(self.rank)
-            per = [self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0)
-                   for i in range(len(samplers))]
-            vals = self.engine.generate_decoded(per[k]).cpu().numpy()
-            share = vals
-        if len(samplers) > 1:
-            parts = c.gather_bytes(share, dst=self.federator)
+        per = [self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0)
+               for i in range(len(samplers))]
+        if len(samplers) == 1:
+            if self.rank in samplers:
+                share = self.engine.generate_decoded(per[0]).cpu().numpy()
+        else:
+            # every client decodes its share on its GPU; one gather to the federator (RCCL over
+            # xGMI when the data plane is RCCL), one device-to-host copy there
+            vals = self.engine.generate_decoded(per[samplers.index(self.rank)])
+            rows = c.gather_rows(vals, per, samplers, dst=self.federator)
             if self.is_fed:
-                share = np.concatenate([parts[r] for r in samplers], axis=0)
+                share = rows.numpy()
         if self.is_fed and self.cfg.write_csv:
             self.write_epoch_csv(share, epoch)
         return share if self.is_fed else None

@@ -133,6 +133,28 @@ class Comm:
         return out
 
     # ------------------------------------------------------------------ data plane
+    def gather_rows(self, t: torch.Tensor, counts: Sequence[int], ranks: Sequence[int], dst: int = 0):
+        """Row-concatenate the [counts[i], C] tensors of ``ranks`` (in order) on ``dst``.
+
+        With an RCCL data plane the device tensors move GPU to GPU over xGMI (padded to the
+        largest share, one ``gather``) and ``dst`` copies the result to the host once; the
+        gloo path gathers host tensors.  Returns the host tensor on ``dst``, None elsewhere."""
+        if self.world_size == 1:
+            return t.cpu()
+        nccl = self.data_backend == "nccl"
+        width = t.shape[1]
+        m = max(counts)
+        buf = torch.zeros(m, width, dtype=t.dtype, device=t.device if nccl else "cpu")
+        buf[:t.shape[0]] = t if nccl else t.cpu()
+        group = self.data if nccl else self.ctrl
+        gl = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))] if self.rank == dst else None
+        dist.gather(buf, gl, dst=dst, group=group)
+        if self.rank != dst:
+            return None
+        order = dist.get_process_group_ranks(group) if group is not dist.group.WORLD else list(range(self.world_size))
+        parts = {r: g for r, g in zip(order, gl)}
+        return torch.cat([parts[r][:n] for r, n in zip(ranks, counts)]).cpu()
+
     def weighted_all_reduce(self, flat: torch.Tensor, weight: float) -> torch.Tensor:
         """flat <- sum_i w_i * flat_i over the data group (in place).
 

@@ -119,3 +119,13 @@ def test_local_epochs_between_aggregations(tmp_path):
     """-E_interval 2: clients train two local epochs between weighted aggregations."""
     rt = run_local_emulation(_cfg(tmp_path, epochs=3, e_interval=2), 2, backend="torch", device=torch.device("cpu"))
     assert len(rt.round_times) == 3
+
+
+def test_cli_colocated_two_ranks(tmp_path):
+    """-colocated (the MI355X layout, every rank a client): weighted all-reduce + sharded sampling
+    gathered to rank 0, here over gloo with two processes; uneven shares (501 rows)."""
+    r = _run_cli(["-world_size", "2", "-colocated", "-epochs", "2", "-backend", "torch", "-synthetic_rows", "1000",
+                  "-n_sample", "501", "-batch_size", "100", "-out_dir", str(tmp_path), "-quiet"], cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    df = pd.read_csv(tmp_path / "Intrusion_result" / "Intrusion_synthesis_epoch_1.csv")
+    assert df.shape == (501, 42)
