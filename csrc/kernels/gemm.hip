@@ -30,6 +30,7 @@
 //   EPI_RELU            out = max(v, 0)
 //   EPI_BN_EVAL_RELU    out = relu((v - rm) * rsqrt(rv + eps) * gamma + beta)   (eval BatchNorm)
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "launch.h"
@@ -71,20 +72,28 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
 // With a 16-B aligned base, a leading dimension and a vector extent divisible by 4 ("vec"),
 // every load is a 16-B global_load_dwordx4 (one CU pulls several times more bytes per
 // instruction than with dword loads); otherwise every element is a clamped dword load.
-// Out-of-range elements are zeroed after all loads of the burst have been issued.
+// Out-of-range elements are zeroed when the burst is staged into LDS, so nothing waits on a
+// burst's loads before its turn comes (PIPE bursts stay in flight).
 template <int KC, bool ROWMAJ>
 struct Chunk {
   static constexpr int NV = KC / 16;
   f32x4 v[NV];
+  int r0, rmax, k0, kmax;   // bounds of the burst: out-of-range elements are zeroed at staging
 
-  // vec: wave-uniform -- base 16-B aligned, ld % 4 == 0 and the vector extent (kmax for ROWMAJ,
-  // rmax otherwise) % 4 == 0, so every float4 is entirely inside or entirely outside the
-  // operand and its address can simply be clamped; the two paths are straight-line code.
-  __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0, int rmax, int k0, int kmax,
-                                       bool vec) {
+  // Issue the burst's loads (and nothing that waits on them, so the burst stays in flight).
+  // VEC (a kernel template parameter, so each variant is straight-line code and the compiler's
+  // load-counter waits stay exact): base 16-B aligned, ld % 4 == 0 and the vector extent (kmax
+  // for ROWMAJ, rmax otherwise) % 4 == 0, so every float4 is entirely inside or entirely
+  // outside the operand and its address can simply be clamped.
+  template <bool VEC>
+  __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0_, int rmax_, int k0_, int kmax_) {
+    r0 = r0_;
+    rmax = rmax_;
+    k0 = k0_;
+    kmax = kmax_;
     const int t = threadIdx.x;
     if constexpr (ROWMAJ) {
-      if (vec) {
+      if constexpr (VEC) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
           const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
@@ -101,16 +110,8 @@ struct Chunk {
           for (int e = 0; e < 4; ++e) v[i][e] = row[min(k + e, kmax - 1)];
         }
       }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
-        const int k = k0 + 4 * (t % (KC / 4));
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (rr >= rmax || k + e >= kmax) v[i][e] = 0.f;
-      }
     } else {
-      if (vec) {
+      if constexpr (VEC) {
 #pragma unroll
         for (int i = 0; i < NV / 2; ++i) {
           const int rr = min(r0 + 4 * (t % 16), rmax - 4);
@@ -133,17 +134,17 @@ struct Chunk {
           }
         }
       }
-#pragma unroll
-      for (int i = 0; i < NV / 2; ++i) {
-        const int rr = r0 + 4 * (t % 16);
-        const int k = k0 + 2 * (t / 16 + 16 * i);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (rr + e >= rmax || k >= kmax) v[2 * i][e] = 0.f;
-          if (rr + e >= rmax || k + 1 >= kmax) v[2 * i + 1][e] = 0.f;
-        }
-      }
     }
+  }
+
+  // element (i, e) of this thread -> in range?
+  __device__ __forceinline__ bool ok_rm(int i, int e) const {
+    const int t = threadIdx.x;
+    return r0 + t / (KC / 4) + (NT / (KC / 4)) * i < rmax && k0 + 4 * (t % (KC / 4)) + e < kmax;
+  }
+  __device__ __forceinline__ bool ok_cm(int i, int half, int e) const {
+    const int t = threadIdx.x;
+    return r0 + 4 * (t % 16) + e < rmax && k0 + 2 * (t / 16 + 16 * i) + half < kmax;
   }
 
   // bf16 image [row][KC + 8]
@@ -153,8 +154,10 @@ struct Chunk {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
-        *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) =
-            uint2{pack_bf16x2(v[i][0], v[i][1]), pack_bf16x2(v[i][2], v[i][3])};
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = ok_rm(i, e) ? v[i][e] : 0.f;
+        *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
       }
     } else {
 #pragma unroll
@@ -162,7 +165,8 @@ struct Chunk {
         const int rq = t % 16, kp = t / 16 + 16 * i;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          *reinterpret_cast<uint32_t*>(&s[(4 * rq + e) * (KC + 8) + 2 * kp]) = pack_bf16x2(v[2 * i][e], v[2 * i + 1][e]);
+          *reinterpret_cast<uint32_t*>(&s[(4 * rq + e) * (KC + 8) + 2 * kp]) =
+              pack_bf16x2(ok_cm(i, 0, e) ? v[2 * i][e] : 0.f, ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f);
       }
     }
   }
@@ -175,7 +179,7 @@ struct Chunk {
       for (int i = 0; i < NV; ++i) {
         const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) s[r * (KC + 1) + 4 * q + e] = v[i][e];
+        for (int e = 0; e < 4; ++e) s[r * (KC + 1) + 4 * q + e] = ok_rm(i, e) ? v[i][e] : 0.f;
       }
     } else {
 #pragma unroll
@@ -183,8 +187,8 @@ struct Chunk {
         const int rq = t % 16, kp = t / 16 + 16 * i;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          s[(4 * rq + e) * (KC + 1) + 2 * kp] = v[2 * i][e];
-          s[(4 * rq + e) * (KC + 1) + 2 * kp + 1] = v[2 * i + 1][e];
+          s[(4 * rq + e) * (KC + 1) + 2 * kp] = ok_cm(i, 0, e) ? v[2 * i][e] : 0.f;
+          s[(4 * rq + e) * (KC + 1) + 2 * kp + 1] = ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f;
         }
       }
     }
@@ -193,13 +197,16 @@ struct Chunk {
 
 template <bool F32>
 struct Cfg {
+  // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
+  // with 135 KB of LDS raised the per-workgroup rate of long-K GEMMs by 1.36x but cost more on
+  // the short-K ones -- padding waste and one workgroup per CU -- so the step got slower.)
   static constexpr int KC = F32 ? 64 : 128;
   static constexpr int LD = F32 ? KC + 1 : KC + 8;            // LDS row stride (elements)
   static constexpr int ESZ = F32 ? 4 : 2;
   static constexpr int STAGE = (BM + BN) * LD * ESZ;          // bytes per stage (A image + B image)
 };
 
-template <bool TA, bool TB, bool F32>
+template <bool TA, bool TB, bool F32, bool VEC>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   using C = Cfg<F32>;
   constexpr int KC = C::KC;
@@ -219,8 +226,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
 
   // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> staged [m][k]; k-contiguous in memory iff !TA
   // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged [n][k]; k-contiguous in memory iff TB
+  // one register slot: burst i+1's loads are issued before burst i is multiplied out of LDS
   Chunk<KC, !TA> ca;
   Chunk<KC, TB> cb;
+  auto issue = [&](int k0) {
+    ca.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
+    cb.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
+  };
   auto stage = [&](int st) {
     unsigned char* base = smem + st * C::STAGE;
     if constexpr (F32) {
@@ -231,27 +243,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
       cb.store_bf16(reinterpret_cast<uint16_t*>(base) + BM * C::LD);
     }
   };
-
-  // 16-B operand loads (see Chunk::load); the vector extent is K for k-contiguous operands
-  // (every split boundary is a multiple of KC), the row count otherwise
-  const bool va = ((uintptr_t)g.a % 16 == 0) && (g.lda % 4 == 0) && ((TA ? g.M : g.K) % 4 == 0);
-  const bool vb = ((uintptr_t)g.b % 16 == 0) && (g.ldb % 4 == 0) && ((TB ? g.K : g.N) % 4 == 0);
-  int buf = 0;
-  if (kb < ke) {
-    ca.load(g.a, g.lda, m0, g.M, kb, ke, va);
-    cb.load(g.b, g.ldb, n0, g.N, kb, ke, vb);
-    stage(0);
-  }
-  __syncthreads();
-  for (int k0 = kb; k0 < ke; k0 += KC) {
-    const bool more = k0 + KC < ke;
-    if (more) {  // next burst in flight while this chunk is multiplied
-      ca.load(g.a, g.lda, m0, g.M, k0 + KC, ke, va);
-      cb.load(g.b, g.ldb, n0, g.N, k0 + KC, ke, vb);
-    }
-    const int kvalid = min(KC, ke - k0);
+  auto compute = [&](int st, int kvalid) {
     if constexpr (F32) {
-      const float* A = reinterpret_cast<const float*>(smem + buf * C::STAGE);
+      const float* A = reinterpret_cast<const float*>(smem + st * C::STAGE);
       const float* B = A + BM * C::LD;
       const int nsteps = (kvalid + 3) / 4;
       for (int s4 = 0; s4 < nsteps; ++s4) {
@@ -268,7 +262,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
     } else {
-      const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + buf * C::STAGE);
+      const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + st * C::STAGE);
       const uint16_t* B = A + BM * C::LD;
       const int nsteps = (kvalid + 31) / 32;
       for (int s = 0; s < nsteps; ++s) {
@@ -284,9 +278,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (more) stage(buf ^ 1);
+  };
+  // per burst: stage the landed burst into LDS buffer st, issue the next burst, multiply.  One
+  // barrier per burst: buffer st was last read two bursts ago, before the previous barrier.
+  int st = 0;
+  issue(kb);
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+    stage(st);
     __syncthreads();
-    buf ^= 1;
+    if (k0 + KC < ke) issue(k0 + KC);
+    compute(st, min(KC, ke - k0));
+    st ^= 1;
   }
 
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
@@ -348,16 +350,28 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
   g.kchunk = kchunk;
   dim3 grid(tn, tm, g.splitk), block(NT);
-#define FEDTGAN_GEMM_DISPATCH(F)                                                                         \
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F>), grid, block, 0, stream, g);       \
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F>), grid, block, 0, stream, g); \
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F>), grid, block, 0, stream, g);   \
-  else hipLaunchKernelGGL((gemm_kernel<true, true, F>), grid, block, 0, stream, g);
+  // 16-B operand loads (see Chunk::load) when both operands allow them; the vector extent is K
+  // for k-contiguous operands (every split boundary is a multiple of KC), the row count otherwise
+  const bool va = ((uintptr_t)g.a % 16 == 0) && (g.lda % 4 == 0) && ((g.ta ? g.M : g.K) % 4 == 0);
+  const bool vb = ((uintptr_t)g.b % 16 == 0) && (g.ldb % 4 == 0) && ((g.tb ? g.K : g.N) % 4 == 0);
+  const bool vec = va && vb;
+#define FEDTGAN_GEMM_LAYOUTS(F, V)                                                                           \
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V>), grid, block, 0, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V>), grid, block, 0, stream, g); \
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V>), grid, block, 0, stream, g);   \
+  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V>), grid, block, 0, stream, g);
+#define FEDTGAN_GEMM_DISPATCH(F) \
+  if (vec) {                     \
+    FEDTGAN_GEMM_LAYOUTS(F, true)  \
+  } else {                       \
+    FEDTGAN_GEMM_LAYOUTS(F, false) \
+  }
   if (g.f32) {
     FEDTGAN_GEMM_DISPATCH(true)
   } else {
     FEDTGAN_GEMM_DISPATCH(false)
   }
+#undef FEDTGAN_GEMM_LAYOUTS
 #undef FEDTGAN_GEMM_DISPATCH
   if (grid.z > 1) {
     const size_t total = (size_t)g.M * g.N;
