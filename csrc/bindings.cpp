@@ -43,7 +43,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
           const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
-          const optional<Tensor>& bn_rv, double bn_eps, bool f32) {
+          const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
+          const optional<Tensor>& head_v, const optional<Tensor>& head_a) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -89,6 +90,17 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.rng_ctr = ctr_ptr(rng_ctr);
   g.rng_stream = (uint32_t)stream;
   g.f32 = f32 ? 1 : 0;
+  if (head_a.has_value() && head_a->defined()) {
+    TORCH_CHECK(epi == fedtgan::EPI_LRELU_DROPOUT, "gemm: the head seed needs the LeakyReLU+dropout epilogue");
+    check_f32_2d(*head_a, "head_a");
+    TORCH_CHECK(head_a->size(0) == M && head_a->size(1) == N, "gemm: head_a shape");
+    TORCH_CHECK(head_coef.has_value() && head_coef->numel() == M && head_coef->is_contiguous() && head_v.has_value() &&
+                    head_v->numel() == N && head_v->is_contiguous(), "gemm: head coef [M] / v [N]");
+    g.head_a = fp(*head_a);
+    g.ldha = ld_of(*head_a);
+    g.head_coef = cfp(*head_coef);
+    g.head_v = cfp(*head_v);
+  }
   fedtgan::launch_gemm(g, cur_stream());
 }
 
@@ -214,13 +226,45 @@ void d_head(const Tensor& d, const Tensor& ms, const Tensor& v, const Tensor& e,
                          ld_of(a), (int)rows, (int)cols, fp(loss), cur_stream());
 }
 
+void colsum_ex(at::TensorList srcs, const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
+               const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
+               const c10::List<optional<Tensor>>& dot_out) {
+  const size_t n = srcs.size();
+  TORCH_CHECK(n <= 8 && outs.size() == n && w.size() == n && dot_v.size() == n && dot_e.size() == n &&
+                  dot_out.size() == n, "colsum_ex: up to 8 jobs, one entry per job in every list");
+  std::vector<fedtgan::ColsumJob> jobs;
+  for (size_t i = 0; i < n; ++i) {
+    check_f32_2d(srcs[i], "colsum src");
+    const int64_t rows = srcs[i].size(0), cols = srcs[i].size(1);
+    fedtgan::ColsumJob j{cfp(srcs[i]), ld_of(srcs[i]), (int)rows, (int)cols, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const optional<Tensor> o = outs[i], wi = w[i], dv = dot_v[i], de = dot_e[i], dout = dot_out[i];
+    if (o.has_value() && o->defined()) {
+      TORCH_CHECK(o->numel() == cols && o->is_contiguous(), "colsum_ex: out");
+      j.out = fp(*o);
+    }
+    if (wi.has_value() && wi->defined()) {
+      TORCH_CHECK(wi->numel() == rows && wi->is_contiguous(), "colsum_ex: row weights");
+      j.w = cfp(*wi);
+    }
+    if (dv.has_value() && dv->defined()) {
+      TORCH_CHECK(dv->numel() == cols && dv->is_contiguous() && dout.has_value() && dout->defined(), "colsum_ex: dot");
+      j.dot_v = cfp(*dv);
+      j.dot_out = fp(*dout);
+      if (de.has_value() && de->defined()) j.dot_e = cfp(*de);
+    }
+    jobs.push_back(j);
+  }
+  fedtgan::launch_colsum(jobs.data(), (int)jobs.size(), cur_stream());
+}
+
 void colsum(at::TensorList srcs, at::TensorList outs) {
   TORCH_CHECK(srcs.size() == outs.size() && srcs.size() <= 8, "colsum: up to 8 jobs");
   std::vector<fedtgan::ColsumJob> jobs;
   for (size_t i = 0; i < srcs.size(); ++i) {
     check_f32_2d(srcs[i], "colsum src");
     TORCH_CHECK(outs[i].numel() == srcs[i].size(1) && outs[i].is_contiguous(), "colsum: out");
-    jobs.push_back({cfp(srcs[i]), ld_of(srcs[i]), (int)srcs[i].size(0), (int)srcs[i].size(1), fp(outs[i])});
+    jobs.push_back({cfp(srcs[i]), ld_of(srcs[i]), (int)srcs[i].size(0), (int)srcs[i].size(1), fp(outs[i]), nullptr,
+                    nullptr, nullptr, nullptr});
   }
   fedtgan::launch_colsum(jobs.data(), (int)jobs.size(), cur_stream());
 }
@@ -400,7 +444,8 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
-      "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32) -> ()");
+      "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
+      "Tensor? head_v, Tensor(e!)? head_a) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
@@ -417,6 +462,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "d_head(Tensor d, Tensor ms, Tensor v, Tensor e, Tensor coef, Tensor wloss, Tensor(a!) y, Tensor(b!) a, "
       "Tensor(c!) loss) -> ()");
   m.def("colsum(Tensor[] srcs, Tensor(a!)[] outs) -> ()");
+  m.def("colsum_ex(Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, Tensor?[] dot_e, Tensor?[] dot_out) -> ()");
   m.def(
       "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
       "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps) -> ()");
@@ -453,6 +499,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("gp_scale", &gp_scale);
   m.impl("d_head", &d_head);
   m.impl("colsum", &colsum);
+  m.impl("colsum_ex", &colsum_ex);
   m.impl("bn_relu_train", &bn_relu_train);
   m.impl("bn_relu_bwd", &bn_relu_bwd);
   m.impl("adam", &adam);

@@ -439,17 +439,26 @@ __global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch 
   const int c = blockIdx.x * CS_COLS + (threadIdx.x % CS_COLS);
   const int grp = threadIdx.x / CS_COLS;
   if ((int)(blockIdx.x * CS_COLS) >= jb.cols) return;
+  const int cc = min(c, jb.cols - 1);
   float s = 0.f;
-  if (c < jb.cols) {
 #pragma unroll 8
-    for (int r = grp; r < jb.rows; r += CS_GROUPS) s += jb.a[(size_t)r * jb.lda + c];
-  }
+  for (int r = grp; r < jb.rows; r += CS_GROUPS) s += (jb.w ? jb.w[r] : 1.f) * jb.a[(size_t)r * jb.lda + cc];
   part[grp][threadIdx.x % CS_COLS] = s;
   __syncthreads();
-  if (grp == 0 && c < jb.cols) {
+  if (grp == 0) {   // one wave: the block's 64 columns
     float t = 0.f;
     for (int i = 0; i < CS_GROUPS; ++i) t += part[i][threadIdx.x];
-    jb.out[c] = t;
+    if (c < jb.cols && jb.out) jb.out[c] = t;
+    if (jb.dot_v) {
+      float d = c < jb.cols ? t * jb.dot_v[c] : 0.f;
+      if (blockIdx.x == 0 && jb.dot_e) {   // + e * sum_r w[r], once per job
+        float ws = 0.f;
+        for (int r = threadIdx.x; r < jb.rows; r += 64) ws += jb.w ? jb.w[r] : 1.f;
+        d += wave_sum(ws) * (threadIdx.x == 0 ? jb.dot_e[0] : 0.f);
+      }
+      d = wave_sum(d);
+      if (threadIdx.x == 0) atomicAdd(jb.dot_out, d);
+    }
   }
 }
 

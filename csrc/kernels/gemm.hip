@@ -51,6 +51,7 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
     const float keep = (u01(r.x) >= g.p_drop) ? 1.f / (1.f - g.p_drop) : 0.f;
     const float f = s * keep;
     g.ms[(size_t)m * g.ldms + n] = f;
+    if (g.head_a) g.head_a[(size_t)m * g.ldha + n] = g.head_coef[m] * g.head_v[n] * f;
     return v * f;
   } else if (epi == EPI_MASK) {
     return v * g.ms[(size_t)m * g.ldms + n];

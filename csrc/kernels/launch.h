@@ -15,6 +15,13 @@ struct GemmArgs {
   float* c;
   const float* bias;
   float* ms;   // EPI_MASK: read; EPI_LRELU_DROPOUT: written (slope * keep / (1 - p))
+  // EPI_LRELU_DROPOUT on D's last hidden layer (nullable): also write the backward seed of that
+  // layer, head_a[m, n] = head_coef[m] * head_v[n] * (slope * keep / (1 - p))  (the D head's
+  // A_{L-1} = coef * v * MS_{L-1}, which needs no reduction)
+  const float* head_coef;
+  const float* head_v;
+  float* head_a;
+  int ldha;
   float* ws;   // split-K partial slabs [splitk][M][N]
   int M, N, K;
   int lda, ldb, ldc, ldms;
@@ -92,10 +99,17 @@ void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const flo
                    const float* coef, const float* wloss, float* y, float* a, int lda, int rows, int cols, float* loss,
                    hipStream_t stream);
 
+// out[c] = sum_r w[r] a[r, c] (w nullable = 1; out nullable); with dot_v, additionally
+// *dot_out += sum_c dot_v[c] * (that column sum) + dot_e[0] * sum_r w[r]  (the WGAN loss
+// sum_r w[r] (d_r . v + e) of the D head, folded into the bias-gradient launch)
 struct ColsumJob {
   const float* a;
   int lda, rows, cols;
   float* out;
+  const float* w;
+  const float* dot_v;
+  const float* dot_e;
+  float* dot_out;
 };
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 

@@ -130,6 +130,7 @@ class MDGANRuntime(FedRuntime):
         o.activate(eng.logits, eng.Xg[:, :eng.Dd], eng.spans, eng.cfg.tau, stream_id=12)
         eng._g_dlogits()
         self.comm.exchange(sends=[(eng.dlogits, self.federator)])
+        eng._g_loss_metric()
         if hasattr(o, "ctr"):
             o.L.rng_bump(o.ctr)                      # fresh Philox streams for the next step
 

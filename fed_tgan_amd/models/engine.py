@@ -396,14 +396,31 @@ class CTGANEngine:
         else:
             o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id)
 
-    def _d_forward(self, rows: slice, stream_base: int, X=None):
+    def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None):
+        """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
+        writes the head's backward seed A_{L-1} = coef * v * MS_{L-1} (no separate head launch;
+        the head's WGAN value is folded into a later column-sum launch, see _wgan_job)."""
         o = self.ops
         inp = (self.X if X is None else X)[rows]
-        for i in range(len(self.ddims)):
+        L = len(self.ddims)
+        for i in range(L):
+            head = None
+            if coef is not None and i == L - 1:
+                head = (coef, self.p["D.out.W"].view(-1), self.A[L - 1][rows])
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][rows], tb=True, bias=self.p[f"D.{i}.b"], epi=EPI_LRELU_DROPOUT,
                    ms=self.ms[i][rows], slope=self.cfg.lrelu_slope, p_drop=self.cfg.dropout_p,
-                   stream_id=stream_base + i)
+                   stream_id=stream_base + i, head=head)
             inp = self.dl[i][rows]
+
+    def _g_loss_metric(self):
+        """The G-phase WGAN value alone (split roles: the client has no generator backward)."""
+        src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
+        self.ops.colsum_many([src], [out], weights=[w], dots=[dot])
+
+    def _wgan_job(self, rows: slice, wloss, loss_out):
+        """colsum job computing loss_out += sum_r wloss[r] (D(x_r) - ...) = sum_r wloss[r](d_r . v + e)."""
+        L = len(self.ddims)
+        return self.dl[L - 1][rows], None, wloss, (self.p["D.out.W"].view(-1), self.p["D.out.b"], loss_out)
 
     def _a_chain(self, rows: slice):
         o = self.ops
@@ -454,9 +471,7 @@ class CTGANEngine:
         L = len(self.ddims)
         allr = slice(0, 3 * nP)
         I = slice(2 * nP, 3 * nP)
-        self._d_forward(allr, stream_base=4)
-        o.d_head(self.dl[L - 1], self.ms[L - 1], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coef3,
-                 self.wloss3, self.y, self.A[L - 1], self.metrics[0:1])
+        self._d_forward(allr, stream_base=4, coef=self.coef3)
         self._a_chain(allr)
         # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
         o.gemm(self.A[0][I], self.p["D.0.W"], self.gbuf)
@@ -472,8 +487,12 @@ class CTGANEngine:
             inp = self.dl[i][I]
             prev = self.dl[i]
         fr = slice(0, 2 * nP)
-        o.colsum_many([self.A[i][fr] for i in range(L)], [self.g[f"D.{i}.b"] for i in range(L)])
-        o.gemm(self.dl[L - 1], self.coef3.view(-1, 1), self.g["D.out.W"].view(-1, 1), ta=True)
+        # bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN loss value, one launch.
+        # (dl[L-1][I] holds R_{L-1} by now: coef = 1 there gives dpen/dv; wloss = 0 there.)
+        src, out, w, dot = self._wgan_job(allr, self.wloss3, self.metrics[0:1])
+        o.colsum_many([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src],
+                      [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out],
+                      weights=[None] * L + [self.coef3, w], dots=[None] * (L + 1) + [dot])
         self._join(1, 2)
         # d(loss)/d(e_out) = sum of the +-1/n_packs seeds = 0 (stays zero from allocation)
         b1, b2 = self.cfg.betas
@@ -500,9 +519,7 @@ class CTGANEngine:
         o, B, nP = self.ops, self.B, self.nP
         L = len(self.ddims)
         fk = slice(0, nP)
-        self._d_forward(fk, stream_base=14, X=self.XgP)
-        o.d_head(self.dl[L - 1][fk], self.ms[L - 1][fk], self.p["D.out.W"].view(-1), self.p["D.out.b"], self.coefg,
-                 self.coefg, self.y[fk], self.A[L - 1][fk], self.metrics[2:3])
+        self._d_forward(fk, stream_base=14, X=self.XgP, coef=self.coefg)
         self._a_chain(fk)
         o.gemm(self.A[0][fk], self.p["D.0.W"], self.gbuf)            # d(-mean D)/dX, packed
         dx = self.gbuf.view(B, self.Din)
@@ -517,7 +534,9 @@ class CTGANEngine:
         with self._lane(1):
             x, dW = self._kpad(self.H, 0, self.g["G.out.W"])
             o.gemm(self.dlogits, x, dW, ta=True)
-            o.colsum_many([self.dlogits], [self.g["G.out.b"]])
+            # G.out bias grad + the G-phase WGAN value (-mean D(fake)) in one launch
+            src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
+            o.colsum_many([self.dlogits, src], [self.g["G.out.b"], out], weights=[None, w], dots=[None, dot])
         top = self.off[0]
         if Lg:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])

@@ -103,8 +103,9 @@ class HipOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5):
-        """C = epi(alpha op(A) op(B) + beta C + bias)."""
+             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None):
+        """C = epi(alpha op(A) op(B) + beta C + bias).  head = (coef [M], v [N], A_out [M, N]):
+        with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed)."""
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
@@ -116,7 +117,7 @@ class HipOps:
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
-                    float(bn_eps), self.f32)
+                    float(bn_eps), self.f32, *(head or (None, None, None)))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5):
@@ -185,7 +186,16 @@ class HipOps:
             raise NotImplementedError
         self.L.colsum([a], [out])
 
-    def colsum_many(self, srcs, outs):
+    def colsum_many(self, srcs, outs, weights=None, dots=None):
+        """out_i = sum_r w_i[r] src_i[r, :] (out_i may be None); dots[i] = (v, e, loss): loss +=
+        sum_r w_i[r] (src_i[r] . v + e) in the same launch (the WGAN term of the D head)."""
+        if weights is not None or dots is not None:
+            n = len(srcs)
+            weights = weights or [None] * n
+            dots = dots or [None] * n
+            self.L.colsum_ex(list(srcs), list(outs), list(weights), [d[0] if d else None for d in dots],
+                             [d[1] if d else None for d in dots], [d[2] if d else None for d in dots])
+            return
         self.L.colsum(list(srcs), list(outs))
 
     # ------------------------------------------------------------------ optimizer

@@ -29,7 +29,7 @@ class TorchOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0):
+             slope=0.2, p_drop=0.5, stream_id=0, head=None):
         """c = epi(alpha * op(a) @ op(b) + beta * c + bias)."""
         A = a.t() if ta else a
         B = b.t() if tb else b
@@ -45,6 +45,9 @@ class TorchOps:
             s = torch.where(acc > 0, torch.ones_like(acc), torch.full_like(acc, slope))
             ms.copy_(s * keep)
             acc = acc * ms
+            if head is not None:      # D head seed: A_{L-1} = coef * v * MS_{L-1}
+                coef, v, a_out = head
+                a_out.copy_(coef.view(-1, 1) * v.view(1, -1) * ms)
         elif epi == EPI_MASK:
             acc = acc * ms
         elif epi == EPI_RELU:
@@ -217,9 +220,16 @@ class TorchOps:
         else:
             out.mul_(beta).add_(a.sum(0))
 
-    def colsum_many(self, srcs, outs):
-        for a, o in zip(srcs, outs):
-            o.copy_(a.sum(0))
+    def colsum_many(self, srcs, outs, weights=None, dots=None):
+        n = len(srcs)
+        for a, o, w, d in zip(srcs, outs, weights or [None] * n, dots or [None] * n):
+            s = (a * w.view(-1, 1)).sum(0) if w is not None else a.sum(0)
+            if o is not None:
+                o.copy_(s)
+            if d is not None:
+                v, e, loss = d
+                wsum = w.sum() if w is not None else torch.tensor(float(a.shape[0]), device=a.device)
+                loss.add_((s * v.view(-1)).sum() + e.view(-1)[0] * wsum)
 
     # ------------------------------------------------------------------ optimizer
     def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False):

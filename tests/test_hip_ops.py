@@ -345,3 +345,30 @@ def test_vgm_fit_hip_passes_match_torch(hip):
     for f in ("wc_a", "wc_b", "mean_precision", "means", "dof", "covariances"):
         np.testing.assert_allclose(getattr(a, f), getattr(b, f), rtol=1e-5, atol=1e-7, err_msg=f)
     np.testing.assert_allclose(a.weights, b.weights, atol=1e-6)
+
+
+def test_gemm_head_seed_and_weighted_colsum(hip):
+    """The D head folded into other launches: the last layer's LeakyReLU+dropout epilogue writes
+    A_{L-1} = coef v^T * MS, and the bias-gradient launch computes weighted column sums and the
+    WGAN value sum_r w_r (d_r . v + e)."""
+    M, N, K = 150, 256, 300
+    a, b = mat(M, K, seed=40), mat(N, K, seed=41)
+    bias = mat(1, N, seed=42).view(-1).contiguous()
+    coef = mat(M, 1, seed=43).view(-1).contiguous()
+    v = mat(N, 1, seed=44).view(-1).contiguous()
+    out, ms, A = (torch.zeros(M, N, device=DEV) for _ in range(3))
+    hip.gemm(a, b, out, tb=True, bias=bias, epi=1, ms=ms, head=(coef, v, A))
+    torch.cuda.synchronize()
+    assert torch.allclose(A, coef.view(-1, 1) * v.view(1, -1) * ms, atol=1e-6, rtol=1e-6)
+    w = mat(M, 1, seed=45).view(-1).contiguous()
+    e = torch.tensor([0.3], device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    og = torch.zeros(N, device=DEV)
+    plain = torch.zeros(N, device=DEV)
+    hip.colsum_many([out, out, out], [og, None, plain], weights=[w, w, None], dots=[None, (v, e, loss), None])
+    torch.cuda.synchronize()
+    s = (out.double() * w.double().view(-1, 1)).sum(0)
+    assert torch.allclose(og.double(), s, atol=1e-3, rtol=1e-4)
+    assert torch.allclose(plain.double(), out.double().sum(0), atol=1e-3, rtol=1e-4)
+    ref = (s * v.double()).sum() + 0.3 * w.double().sum()
+    assert abs(loss.item() - ref.item()) < 1e-3 * (1 + abs(ref.item()))
