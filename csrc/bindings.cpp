@@ -168,14 +168,31 @@ fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Ten
 }
 
 void activate(const Tensor& logits, const Tensor& out, const Tensor& start, const Tensor& width, const Tensor& kind,
-              const Tensor& cidx, const Tensor& elem, double tau, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+              const Tensor& cidx, const Tensor& elem, double tau, int64_t seed, const Tensor& rng_ctr, int64_t stream,
+              const optional<Tensor>& slerp_real, const optional<Tensor>& slerp_out, int64_t slerp_cols,
+              int64_t slerp_stream) {
   check_f32_2d(logits, "logits");
   check_f32_2d(out, "out");
   TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) >= logits.size(1), "activate: shapes");
   TORCH_CHECK(elem.numel() == logits.size(1), "activate: elem_span must cover every data column");
+  fedtgan::SlerpFuse sl{};
+  if (slerp_real.has_value() && slerp_real->defined()) {
+    TORCH_CHECK(slerp_out.has_value() && slerp_out->defined(), "activate: slerp needs an output");
+    check_f32_2d(*slerp_real, "slerp real");
+    check_f32_2d(*slerp_out, "slerp out");
+    TORCH_CHECK(ld_of(*slerp_real) == ld_of(*slerp_out) && ld_of(*slerp_real) == ld_of(out), "activate: slerp strides");
+    TORCH_CHECK(slerp_real->size(0) == out.size(0) && slerp_out->size(0) == out.size(0) &&
+                    slerp_real->size(1) == slerp_cols && slerp_out->size(1) == slerp_cols &&
+                    slerp_cols >= logits.size(1) && slerp_cols <= ld_of(out), "activate: slerp shapes");
+    sl.real = cfp(*slerp_real);
+    sl.out = fp(*slerp_out);
+    sl.ld = ld_of(out);
+    sl.cols = (int)slerp_cols;
+    sl.stream = (uint32_t)slerp_stream;
+  }
   fedtgan::launch_activate(cfp(logits), ld_of(logits), fp(out), ld_of(out), (int)logits.size(0),
                            spans_of(start, width, kind, cidx, elem), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
-                           (uint32_t)stream, cur_stream());
+                           (uint32_t)stream, sl, cur_stream());
 }
 
 void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, const Tensor& start, const Tensor& width,
@@ -452,7 +469,8 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor(f!)? step_bump, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def(
       "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, Tensor elem, "
-      "float tau, int seed, Tensor rng_ctr, int stream) -> ()");
+      "float tau, int seed, Tensor rng_ctr, int stream, Tensor? slerp_real, Tensor(b!)? slerp_out, int slerp_cols, "
+      "int slerp_stream) -> ()");
   m.def(
       "act_bwd_ce(Tensor dact, Tensor act, Tensor logits, Tensor start, Tensor width, Tensor kind, Tensor cidx, "
       "Tensor elem, Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");

@@ -142,6 +142,22 @@ void launch_sample(const SampleArgs& a, hipStream_t stream) {
 //   element-parallel: Gumbel-perturbed logits (or tanh) into an LDS row image
 //   span-parallel   : one lane per softmax span reduces (max, sum) from LDS
 //   element-parallel: normalise and store
+// slerp weights of the reference's `slerp` (`Server/dtds/synthesizers/ctgan.py:231-237`), linear
+// fallback when the angle degenerates; shared by the fused activation and the standalone kernel
+__device__ __forceinline__ void slerp_weights(float saa, float sbb, float sab, float alpha, float& wa, float& wb) {
+  float cosw = sab / (sqrtf(saa) * sqrtf(sbb));
+  cosw = fminf(1.f, fmaxf(-1.f, cosw));
+  const float om = acosf(cosw);
+  const float so = sinf(om);
+  if (so < 1e-6f) {
+    wa = 1.f - alpha;
+    wb = alpha;
+  } else {
+    wa = sinf((1.f - alpha) * om) / so;
+    wb = sinf(alpha * om) / so;
+  }
+}
+
 constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
 constexpr size_t LDS_BYTES = 160 * 1024;
 
@@ -177,7 +193,8 @@ __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float*
 __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* __restrict__ logits, int ldl,
                                                                   float* __restrict__ out, int ldo, int rows,
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
-                                                                  const uint64_t* ctr, uint32_t stream_id) {
+                                                                  const uint64_t* ctr, uint32_t stream_id,
+                                                                  SlerpFuse sl) {
   extern __shared__ float act_smem[];
   const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -193,8 +210,13 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   const uint64_t base = (uint64_t)r << 20;
   for (int j = lane; j < D; j += 64) {
     const float xv = x[j];
-    if (t.kind[t.elem[j]] == 0) y[j] = tanhf(xv);
-    else v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
+    if (t.kind[t.elem[j]] == 0) {
+      const float th = tanhf(xv);
+      y[j] = th;
+      v[j] = th;    // (read back by the fused slerp; tanh elements have no softmax input)
+    } else {
+      v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -212,8 +234,32 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   __builtin_amdgcn_wave_barrier();
   for (int j = lane; j < D; j += 64) {
     const int s = t.elem[j];
-    if (t.kind[s] != 0) y[j] = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
+    if (t.kind[s] != 0) {
+      const float o = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
+      y[j] = o;
+      v[j] = o;     // each lane re-reads only its own elements below
+    }
   }
+  if (sl.real == nullptr) return;
+  // fused slerp(real_r, fake_r) of the gradient penalty (one launch less per step): the fake row
+  // is this row's activation (LDS, j < D) followed by its conditional columns (global)
+  const float* a = sl.real + (size_t)r * sl.ld;
+  float saa = 0.f, sbb = 0.f, sab = 0.f;
+  for (int j = lane; j < sl.cols; j += 64) {
+    const float ra = a[j], fb = j < D ? v[j] : y[j];
+    saa += ra * ra;
+    sbb += fb * fb;
+    sab += ra * fb;
+  }
+  saa = wave_sum(saa);
+  sbb = wave_sum(sbb);
+  sab = wave_sum(sab);
+  RngArgs srng{seed, ctr, sl.stream};
+  const float alpha = u01(rng4(srng, step, (uint64_t)r).x);
+  float wa, wb;
+  slerp_weights(saa, sbb, sab, alpha, wa, wb);
+  float* o = sl.out + (size_t)r * sl.ld;
+  for (int j = lane; j < sl.cols; j += 64) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
 }
 
 static size_t act_smem_bytes(const SpanTables& sp, int waves) {
@@ -235,12 +281,12 @@ static void allow_big_lds(K kernel, size_t bytes) {
 }
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
-                     uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream) {
+                     uint64_t seed, const uint64_t* ctr, uint32_t stream_id, SlerpFuse sl, hipStream_t stream) {
   if (rows == 0) return;
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(activate_kernel, lds);
-  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id);
+  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl);
 }
 
 // backward of the activation + fused conditional cross-entropy, one wave per row
@@ -345,13 +391,8 @@ __global__ __launch_bounds__(256) void slerp_kernel(const float* __restrict__ re
   const uint64_t step = ctr ? *ctr : 0ull;
   RngArgs rng{seed, ctr, stream_id};
   const float alpha = u01(rng4(rng, step, (uint64_t)r).x);
-  float cosw = sab / (sqrtf(saa) * sqrtf(sbb));
-  cosw = fminf(1.f, fmaxf(-1.f, cosw));
-  const float om = acosf(cosw);
-  const float so = sinf(om);
   float wa, wb;
-  if (so < 1e-6f) { wa = 1.f - alpha; wb = alpha; }
-  else { wa = sinf((1.f - alpha) * om) / so; wb = sinf(alpha * om) / so; }
+  slerp_weights(saa, sbb, sab, alpha, wa, wb);
   float* o = out + (size_t)r * ld;
   for (int i = lane; i < cols; i += 64) o[i] = wa * a[i] + wb * b[i];
 }

@@ -82,8 +82,15 @@ struct SpanTables {
 
 size_t activation_smem_bytes(const SpanTables& sp);   // dynamic LDS of the activation kernels
 
+// optional slerp(real, fake) fused onto the activation of the fake rows (real == nullptr: off)
+struct SlerpFuse {
+  const float* real;   // [rows, ld] real rows
+  float* out;          // [rows, ld] interpolates
+  int ld, cols;        // cols = data_dim + n_opt (the fake row continues past the activation)
+  uint32_t stream;
+};
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
-                     uint64_t seed, const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
+                     uint64_t seed, const uint64_t* ctr, uint32_t stream_id, SlerpFuse sl, hipStream_t stream);
 
 void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, const float* logits, int ldl, SpanTables sp,
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,

@@ -378,7 +378,7 @@ class CTGANEngine:
             return _ext(x, kp), _ext(W, kp)
         return x, W
 
-    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0):
+    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None):
         """Residual stack + output layer; with ``act_out`` the activation is fused onto the
         output GEMM (tanh / Gumbel-softmax into act_out, Philox stream ``stream_id``)."""
         o = self.ops
@@ -394,7 +394,8 @@ class CTGANEngine:
         if act_out is None:
             o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
         else:
-            o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id)
+            o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
+                              slerp=slerp)
 
     def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None):
         """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
@@ -462,8 +463,9 @@ class CTGANEngine:
         o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], self.Xd[B:2 * B], self.Dd,
                        self.col, self.opt, step_counter=self.stepD, metrics=self.metrics, zero_metrics=True,
                        stream_id=1)
-        self._g_forward(self.H, self.logits, training=True, act_out=self.Xd[0:B, :self.Dd], stream_id=2)
-        o.slerp(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], stream_id=3)
+        # activation of the fake rows + slerp(real, fake) for the gradient penalty in one launch
+        self._g_forward(self.H, self.logits, training=True, act_out=self.Xd[0:B, :self.Dd], stream_id=2,
+                        slerp=(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], 3))
 
     def _d_update(self):
         """D forward on the stacked rows, WGAN + GP backward, D Adam step."""

@@ -158,14 +158,23 @@ class HipOps:
                       int(stream_id) * 16)
 
     # ------------------------------------------------------------------ activations
-    def activate(self, logits, out, spans, tau=0.2, stream_id=0):
+    def activate(self, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
+        """Per-span tanh / Gumbel-softmax.  slerp = (real, fake_full, interp, stream_id): also
+        interp = slerp(real, fake_full) in the same launch (fake_full = out's rows continued by
+        their conditional columns)."""
         st, w, k, ci, el = self._span_tables(spans)
-        self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16)
+        if slerp is None:
+            sr, so, cols, ss = None, None, 0, 0
+        else:
+            sr, fake_full, so, sid = slerp
+            cols, ss = int(fake_full.shape[1]), int(sid) * 16
+        self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16, sr, so,
+                        cols, ss)
 
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0):
-        """logits = x W^T + b; out = activate(logits)."""
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
+        """logits = x W^T + b; out = activate(logits) (optionally + the fused slerp)."""
         self.gemm(x, W, logits, tb=True, bias=b)
-        self.activate(logits, out, spans, tau, stream_id)
+        self.activate(logits, out, spans, tau, stream_id, slerp=slerp)
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
         st, w, k, ci, el = self._span_tables(spans, cond_spans)

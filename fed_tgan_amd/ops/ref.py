@@ -149,9 +149,12 @@ class TorchOps:
             dbias.copy_(da.sum(0))
 
     # ------------------------------------------------------------------ activations
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0):
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
         self.gemm(x, W, logits, tb=True, bias=b)
         self.activate(logits, out, spans, tau, stream_id=stream_id)
+        if slerp is not None:
+            real, fake_full, interp, sid = slerp
+            self.slerp(real, fake_full, interp, stream_id=sid)
 
     def activate(self, logits, out, spans, tau=0.2, stream_id=0):
         """spans: list of (start, width, kind) host tuples (kind 0 tanh, 1 gumbel-softmax)."""

@@ -372,3 +372,21 @@ def test_gemm_head_seed_and_weighted_colsum(hip):
     assert torch.allclose(plain.double(), out.double().sum(0), atol=1e-3, rtol=1e-4)
     ref = (s * v.double()).sum() + 0.3 * w.double().sum()
     assert abs(loss.item() - ref.item()) < 1e-3 * (1 + abs(ref.item()))
+
+
+def test_activate_with_fused_slerp_matches_standalone(hip):
+    """The slerp fused onto the fake rows' activation = activation, then the standalone slerp
+    kernel (same Philox stream, same weights)."""
+    tr, X, spans, cond = _spans()
+    B, Dd = 256, tr.layout.data_dim
+    Din = Dd + 40
+    logits = mat(B, Dd, seed=50)
+    xd = mat(3 * B, Din, seed=51)          # [fake | real | interp] blocks; fake cond columns random
+    fake, real, interp = xd[0:B], xd[B:2 * B], xd[2 * B:]
+    xd2 = xd.clone()
+    hip.activate(logits, fake[:, :Dd], spans, 0.2, stream_id=2, slerp=(real, fake, interp, 3))
+    hip.activate(logits, xd2[0:B, :Dd], spans, 0.2, stream_id=2)
+    hip.slerp(xd2[B:2 * B], xd2[0:B], xd2[2 * B:], stream_id=3)
+    torch.cuda.synchronize()
+    assert torch.equal(fake, xd2[0:B])
+    assert torch.allclose(interp, xd2[2 * B:], atol=2e-6, rtol=1e-5)
