@@ -44,7 +44,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
           const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
-          const optional<Tensor>& head_v, const optional<Tensor>& head_a) {
+          const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -90,6 +90,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.rng_ctr = ctr_ptr(rng_ctr);
   g.rng_stream = (uint32_t)stream;
   g.f32 = f32 ? 1 : 0;
+  TORCH_CHECK(tile == 32 || tile == 64, "gemm: tile must be 32 or 64");
+  g.tile = (int)tile;
   if (head_a.has_value() && head_a->defined()) {
     TORCH_CHECK(epi == fedtgan::EPI_LRELU_DROPOUT, "gemm: the head seed needs the LeakyReLU+dropout epilogue");
     check_f32_2d(*head_a, "head_a");
@@ -462,7 +464,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
-      "Tensor? head_v, Tensor(e!)? head_a) -> ()");
+      "Tensor? head_v, Tensor(e!)? head_a, int tile) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

@@ -40,7 +40,7 @@ namespace fedtgan {
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int BM = 64, BN = 64, NT = 256;
+constexpr int NT = 256;
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
   const int epi = g.epi;
@@ -75,9 +75,10 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
 // instruction than with dword loads); otherwise every element is a clamped dword load.
 // Out-of-range elements are zeroed when the burst is staged into LDS, so nothing waits on a
 // burst's loads before its turn comes (PIPE bursts stay in flight).
-template <int KC, bool ROWMAJ>
+template <int KC, bool ROWMAJ, int R>
 struct Chunk {
-  static constexpr int NV = KC / 16;
+  static constexpr int NV = R * KC / (4 * NT);   // float4 per thread
+  static constexpr int RQ = R / 4;               // row quads (row-contiguous operands)
   f32x4 v[NV];
   int r0, rmax, k0, kmax;   // bounds of the burst: out-of-range elements are zeroed at staging
 
@@ -115,16 +116,16 @@ struct Chunk {
       if constexpr (VEC) {
 #pragma unroll
         for (int i = 0; i < NV / 2; ++i) {
-          const int rr = min(r0 + 4 * (t % 16), rmax - 4);
-          const int k = k0 + 2 * (t / 16 + 16 * i);
+          const int rr = min(r0 + 4 * (t % RQ), rmax - 4);
+          const int k = k0 + 2 * (t / RQ + (NT / RQ) * i);
           v[2 * i] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k, kmax - 1) * ld + rr);
           v[2 * i + 1] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k + 1, kmax - 1) * ld + rr);
         }
       } else {
 #pragma unroll
         for (int i = 0; i < NV / 2; ++i) {
-          const int rr = r0 + 4 * (t % 16);
-          const int k = k0 + 2 * (t / 16 + 16 * i);
+          const int rr = r0 + 4 * (t % RQ);
+          const int k = k0 + 2 * (t / RQ + (NT / RQ) * i);
           const float* l0 = p + (size_t)min(k, kmax - 1) * ld;
           const float* l1 = p + (size_t)min(k + 1, kmax - 1) * ld;
 #pragma unroll
@@ -145,7 +146,7 @@ struct Chunk {
   }
   __device__ __forceinline__ bool ok_cm(int i, int half, int e) const {
     const int t = threadIdx.x;
-    return r0 + 4 * (t % 16) + e < rmax && k0 + 2 * (t / 16 + 16 * i) + half < kmax;
+    return r0 + 4 * (t % RQ) + e < rmax && k0 + 2 * (t / RQ + (NT / RQ) * i) + half < kmax;
   }
 
   // bf16 image [row][KC + 8]
@@ -163,7 +164,7 @@ struct Chunk {
     } else {
 #pragma unroll
       for (int i = 0; i < NV / 2; ++i) {
-        const int rq = t % 16, kp = t / 16 + 16 * i;
+        const int rq = t % RQ, kp = t / RQ + (NT / RQ) * i;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           *reinterpret_cast<uint32_t*>(&s[(4 * rq + e) * (KC + 8) + 2 * kp]) =
@@ -185,7 +186,7 @@ struct Chunk {
     } else {
 #pragma unroll
       for (int i = 0; i < NV / 2; ++i) {
-        const int rq = t % 16, kp = t / 16 + 16 * i;
+        const int rq = t % RQ, kp = t / RQ + (NT / RQ) * i;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           s[(4 * rq + e) * (KC + 1) + 2 * kp] = ok_cm(i, 0, e) ? v[2 * i][e] : 0.f;
@@ -196,7 +197,7 @@ struct Chunk {
   }
 };
 
-template <bool F32>
+template <bool F32, int TM, int TN>
 struct Cfg {
   // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
   // with 135 KB of LDS raised the per-workgroup rate of long-K GEMMs by 1.36x but cost more on
@@ -204,32 +205,35 @@ struct Cfg {
   static constexpr int KC = F32 ? 64 : 128;
   static constexpr int LD = F32 ? KC + 1 : KC + 8;            // LDS row stride (elements)
   static constexpr int ESZ = F32 ? 4 : 2;
-  static constexpr int STAGE = (BM + BN) * LD * ESZ;          // bytes per stage (A image + B image)
+  static constexpr int STAGE = (TM + TN) * LD * ESZ;          // bytes per stage (A image + B image)
 };
 
-template <bool TA, bool TB, bool F32, bool VEC>
+// TM x TN output tile (64x64, or 32x32 for short-K GEMMs that would otherwise need split-K):
+// 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
-  using C = Cfg<F32>;
+  using C = Cfg<F32, TM, TN>;
   constexpr int KC = C::KC;
+  constexpr int MI = TM / 32, NJ = TN / 32, WM = TM / 2, WN = TN / 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::STAGE];
 
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
   const int kb = blockIdx.z * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
 
-  f32x4 acc[2][2];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> staged [m][k]; k-contiguous in memory iff !TA
   // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged [n][k]; k-contiguous in memory iff TB
   // one register slot: burst i+1's loads are issued before burst i is multiplied out of LDS
-  Chunk<KC, !TA> ca;
-  Chunk<KC, TB> cb;
+  Chunk<KC, !TA, TM> ca;
+  Chunk<KC, TB, TN> cb;
   auto issue = [&](int k0) {
     ca.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
     cb.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
@@ -238,45 +242,45 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
     unsigned char* base = smem + st * C::STAGE;
     if constexpr (F32) {
       ca.store_f32(reinterpret_cast<float*>(base));
-      cb.store_f32(reinterpret_cast<float*>(base) + BM * C::LD);
+      cb.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
     } else {
       ca.store_bf16(reinterpret_cast<uint16_t*>(base));
-      cb.store_bf16(reinterpret_cast<uint16_t*>(base) + BM * C::LD);
+      cb.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
     }
   };
   auto compute = [&](int st, int kvalid) {
     if constexpr (F32) {
       const float* A = reinterpret_cast<const float*>(smem + st * C::STAGE);
-      const float* B = A + BM * C::LD;
+      const float* B = A + TM * C::LD;
       const int nsteps = (kvalid + 3) / 4;
       for (int s4 = 0; s4 < nsteps; ++s4) {
         const int kk = 4 * s4 + (lane >> 4);
-        float af[2], bfv[2];
+        float af[MI], bfv[NJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          af[i] = A[(wm * 32 + i * 16 + (lane & 15)) * C::LD + kk];
-          bfv[i] = B[(wn * 32 + i * 16 + (lane & 15)) * C::LD + kk];
-        }
+        for (int i = 0; i < MI; ++i) af[i] = A[(wm * WM + i * 16 + (lane & 15)) * C::LD + kk];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < NJ; ++j) bfv[j] = B[(wn * WN + j * 16 + (lane & 15)) * C::LD + kk];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
       }
     } else {
       const uint16_t* A = reinterpret_cast<const uint16_t*>(smem + st * C::STAGE);
-      const uint16_t* B = A + BM * C::LD;
+      const uint16_t* B = A + TM * C::LD;
       const int nsteps = (kvalid + 31) / 32;
       for (int s = 0; s < nsteps; ++s) {
-        bf16x8 af[2], bfr[2];
+        bf16x8 af[MI], bfr[NJ];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * 32 + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
-          bfr[i] = *reinterpret_cast<const bf16x8*>(&B[(wn * 32 + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
-        }
+        for (int i = 0; i < MI; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * WM + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < NJ; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&B[(wn * WN + j * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
   };
@@ -294,13 +298,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
 
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * WN + j * 16 + (lane & 15);
         if (m >= g.M || n >= g.N) continue;
         const float v0 = acc[i][j][r];
         if (gridDim.z > 1) {
@@ -339,12 +343,13 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
   }
 }
 
-int gemm_kc(int f32) { return f32 ? Cfg<true>::KC : Cfg<false>::KC; }
+int gemm_kc(int f32) { return f32 ? Cfg<true, 64, 64>::KC : Cfg<false, 64, 64>::KC; }
 
 void launch_gemm(GemmArgs g, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0) return;
   const int KC = gemm_kc(g.f32);
-  const int tm = (g.M + BM - 1) / BM, tn = (g.N + BN - 1) / BN;
+  const int T = g.tile == 32 ? 32 : 64;   // square output tile
+  const int tm = (g.M + T - 1) / T, tn = (g.N + T - 1) / T;
   if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
   int kchunk = (std::max(g.K, 1) + g.splitk - 1) / g.splitk;
   kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
@@ -356,22 +361,29 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   const bool va = ((uintptr_t)g.a % 16 == 0) && (g.lda % 4 == 0) && ((g.ta ? g.M : g.K) % 4 == 0);
   const bool vb = ((uintptr_t)g.b % 16 == 0) && (g.ldb % 4 == 0) && ((g.tb ? g.K : g.N) % 4 == 0);
   const bool vec = va && vb;
-#define FEDTGAN_GEMM_LAYOUTS(F, V)                                                                           \
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V>), grid, block, 0, stream, g);       \
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V>), grid, block, 0, stream, g); \
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V>), grid, block, 0, stream, g);   \
-  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V>), grid, block, 0, stream, g);
+#define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, 0, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT>), grid, block, 0, stream, g); \
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT>), grid, block, 0, stream, g);   \
+  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT>), grid, block, 0, stream, g);
+#define FEDTGAN_GEMM_TILES(F, V)       \
+  if (T == 32) {                       \
+    FEDTGAN_GEMM_LAYOUTS(F, V, 32)     \
+  } else {                             \
+    FEDTGAN_GEMM_LAYOUTS(F, V, 64)     \
+  }
 #define FEDTGAN_GEMM_DISPATCH(F) \
   if (vec) {                     \
-    FEDTGAN_GEMM_LAYOUTS(F, true)  \
+    FEDTGAN_GEMM_TILES(F, true)  \
   } else {                       \
-    FEDTGAN_GEMM_LAYOUTS(F, false) \
+    FEDTGAN_GEMM_TILES(F, false) \
   }
   if (g.f32) {
     FEDTGAN_GEMM_DISPATCH(true)
   } else {
     FEDTGAN_GEMM_DISPATCH(false)
   }
+#undef FEDTGAN_GEMM_TILES
 #undef FEDTGAN_GEMM_LAYOUTS
 #undef FEDTGAN_GEMM_DISPATCH
   if (grid.z > 1) {

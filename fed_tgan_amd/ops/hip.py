@@ -21,23 +21,33 @@ import torch
 from . import native
 
 EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 4
-TILE = 64
+
+
+def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
+    """(output tile, split-K factor) for the burst GEMM (one K-burst = ``kc`` values per row).
+
+    Measured on MI355X (profiles/gemm_split_sweep_r1.txt): a split costs an epilogue launch
+    (~4.6 us) and 64x64 tiles leave most CUs idle on these skinny shapes, so
+      * >= 256 64x64 tiles: 64x64, no split (the grid already covers the chip);
+      * short K (<= 8 bursts): 32x32 tiles, no split (4x the workgroups, no epilogue) --
+        e.g. 500x256x432: 5.5 us vs 7.7 us for 64x64 split 4;
+      * long K: 32x32 tiles split ~512 workgroups deep (one CU pulls only ~60-100 GB/s), at
+        most 2 bursts per split, fp32 slabs capped at ~6 MB.
+    """
+    t64 = -(-M // 64) * -(-N // 64)
+    t32 = -(-M // 32) * -(-N // 32)
+    bursts = -(-K // kc)
+    if t64 >= 256:
+        return 64, 1
+    if bursts <= 8:
+        return 32, 1
+    cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
+    return 32, int(max(1, min(-(-512 // t32), -(-bursts // 2), cap_ws)))
 
 
 def _splitk(M: int, N: int, K: int, kc: int = 128) -> int:
-    """Split-K factor for the burst GEMM (one K-burst = ``kc`` values per operand row).
-
-    One workgroup only pulls ~60-100 GB/s from L2 / Infinity Cache, so a GEMM with few output
-    tiles spreads its K range over many CUs: aim for ~256-384 workgroups, at most ~2 bursts per
-    split, and cap the fp32 partial slabs (splits * M * N * 4 B) at ~6 MB.
-    """
-    tiles = ((M + TILE - 1) // TILE) * ((N + TILE - 1) // TILE)
-    bursts = -(-K // kc)
-    if bursts <= 1 or tiles >= 256:
-        return 1
-    want = max(-(-320 // tiles), -(-bursts // 2))
-    cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
-    return int(max(1, min(want, bursts, cap_ws)))
+    """Split factor of the plan (kept for callers that only need the split)."""
+    return _plan(M, N, K, kc)[1]
 
 
 def _effective_splits(K: int, sk: int, kc: int) -> int:
@@ -62,6 +72,7 @@ class HipOps:
         self.seed = int(seed) & ((1 << 62) - 1)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=device)
         self.split_override = None   # int: force the split-K factor (tuning / microbenchmarks)
+        self.tile_override = None    # 32 | 64: force the output tile (tuning / microbenchmarks)
         self.lane = 0          # set by the engine while it issues work on a side stream
         self._ws: Dict[int, torch.Tensor] = {}
         self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
@@ -110,14 +121,16 @@ class HipOps:
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
         kc = 64 if self.f32 else 128
-        sk = _effective_splits(K, self.split_override or _splitk(M, N, K, kc), kc)
+        tile, sk = _plan(M, N, K, kc)
+        tile = self.tile_override or tile
+        sk = _effective_splits(K, self.split_override or sk, kc)
         ws = None
         if sk > 1:
             ws = self._workspace(sk * M * N)
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
-                    float(bn_eps), self.f32, *(head or (None, None, None)))
+                    float(bn_eps), self.f32, *(head or (None, None, None)), int(tile))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5):

@@ -37,9 +37,12 @@ def hip32():
     return HipOps(DEV, seed=1234, precision="fp32")
 
 
+@pytest.mark.parametrize("tile", [64, 32])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
-@pytest.mark.parametrize("M,N,K", [(150, 256, 6240), (50, 6240, 256), (500, 323, 941), (7, 5, 3), (256, 430, 500)])
-def test_gemm_layouts(hip, hip32, ta, tb, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(150, 256, 6240), (50, 6240, 256), (500, 323, 941), (7, 5, 3), (256, 430, 500),
+                                   (500, 256, 432)])
+def test_gemm_layouts(hip, hip32, ta, tb, M, N, K, tile):
+    hip.tile_override = hip32.tile_override = tile
     a = mat(*((K, M) if ta else (M, K)), seed=1)
     b = mat(*((N, K) if tb else (K, N)), seed=2)
     bias = mat(N, seed=3)
@@ -57,6 +60,7 @@ def test_gemm_layouts(hip, hip32, ta, tb, M, N, K):
     c32 = torch.zeros(M, N, device=DEV)
     hip32.gemm(a, b, c32, ta=ta, tb=tb, bias=bias)
     torch.cuda.synchronize()
+    hip.tile_override = hip32.tile_override = None
     assert (c32.double() - ref32).abs().max().item() < 2e-6 * K + 1e-5
 
 

@@ -61,33 +61,36 @@ def main():
         return step_only(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
     shapes = {
-        "G0 fwd 500x256x(E+C) NT": (eng.H[:, eng.off[0]:], eng.p["G.0.W"], eng.abuf[0], False, True),
-        "G1 fwd 500x256x(E+C+256) NT": (eng.H[:, eng.off[1]:], eng.p["G.1.W"], eng.abuf[1], False, True),
-        "Gout fwd 500xDdxHw NT": (eng.H, eng.p["G.out.W"], eng.logits, False, True),
+        "G0 fwd 500x256x(E+C) NT": (*eng._kpad(eng.H, eng.off[0], eng.p["G.0.W"]), eng.abuf[0], False, True),
+        "G1 fwd 500x256x(E+C+256) NT": (*eng._kpad(eng.H, eng.off[1], eng.p["G.1.W"]), eng.abuf[1], False, True),
+        "Gout fwd 500xDdxHw NT": (*eng._kpad(eng.H, 0, eng.p["G.out.W"]), eng.logits, False, True),
         "D0 fwd 150x256xK1 NT": (eng.X, eng.p["D.0.W"], eng.dl[0], False, True),
         "D1 fwd 150x256x256 NT": (eng.dl[0], eng.p["D.1.W"], eng.dl[1], False, True),
         "A chain 150x256x256 NN": (eng.A[1], eng.p["D.1.W"], eng.A[0], False, False),
         "gp g 50xK1x256 NN": (eng.A[0][:nP], eng.p["D.0.W"], eng.gbuf, False, False),
         "dV0 256xK1x150 TN": (eng.A[0], eng.X, eng.g["D.0.W"], True, False),
-        "dWout DdxHwx500 TN": (eng.dlogits, eng.H, eng.g["G.out.W"], True, False),
+        "dWout DdxHwx500 TN": (eng.dlogits, *eng._kpad(eng.H, 0, eng.g["G.out.W"]), True, False),
         "dH 500x512xDd NN": (eng.dlogits, eng.p["G.out.W"][:, :eng.off[0]], eng.dH[:, :eng.off[0]], False, False),
         "R0 50x256xK1 NT": (eng.X[2 * nP:], eng.p["D.0.W"], eng.dl[0][2 * nP:], False, True),
-        "dW1 256x(E+C+256)x500 TN": (eng.da[1], eng.H[:, eng.off[1]:], eng.g["G.1.W"], True, False),
+        "dW1 256x(E+C+256)x500 TN": (eng.da[1], *eng._kpad(eng.H, eng.off[1], eng.g["G.1.W"]), True, False),
     }
     if args.split_sweep:
         for name, (a, b, c, ta, tb) in shapes.items():
             K = a.shape[0] if ta else a.shape[1]
             kc = 64 if o.f32 else 128
             bursts = -(-K // kc)
-            row = []
-            for sk in [0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48]:
-                if sk > bursts:
-                    break
-                o.split_override = sk or None
-                us = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
-                row.append(f"{'auto' if sk == 0 else sk}:{us:.1f}")
+            for tile in (64, 32):
+                o.tile_override = tile
+                row = []
+                for sk in [0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48]:
+                    if sk > bursts:
+                        break
+                    o.split_override = sk or None
+                    us = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
+                    row.append(f"{'auto' if sk == 0 else sk}:{us:.1f}")
+                print(f"{name:28s} t{tile} " + "  ".join(row), flush=True)
             o.split_override = None
-            print(f"{name:28s} " + "  ".join(row), flush=True)
+            o.tile_override = None
         return
     for name, (a, b, c, ta, tb) in shapes.items():
         res[name] = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
