@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--sync-csv", action="store_true", help="write each epoch CSV inside its round")
     args = ap.parse_args()
 
     from fed_tgan_amd.data.schema import intrusion_spec
@@ -66,7 +67,7 @@ def main():
     spec = intrusion_spec()
     cfg = FedConfig(spec=spec, epochs=args.warmup + args.steps, synthetic_rows=args.rows, out_dir=out,
                     n_sample=args.n_sample, backend=args.backend, gmm_backend=args.gmm, seed=0,
-                    verbose=not args.quiet)
+                    verbose=not args.quiet, async_csv=not args.sync_csv)
     rt = FedRuntime(cfg, comm, device)
     rt.initialize()
     for ep in range(args.warmup):

@@ -85,6 +85,7 @@ class EngineConfig:
     bn_eps: float = 1e-5
     gen_chunk: int = 8192
     precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
+    graph_unroll: int = 8       # GPU: training steps captured per hipGraph (fewer graph launches)
     streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
 
 
@@ -142,8 +143,7 @@ class CTGANEngine:
         self.tables: Dict[str, torch.Tensor] = {}
         self.gen_tables = None
         self._gen_bufs = None
-        self.graph = None
-        self.graph_steps = 0
+        self.graphs: Dict[int, object] = {}    # steps per graph -> captured hipGraph
         self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
 
@@ -339,7 +339,7 @@ class CTGANEngine:
         self.n_rows = len(encoded)
         self.tables = t
         self.steps_per_epoch = len(encoded) // self.B
-        self.graph = None
+        self.graphs = {}
 
     def set_generation_tables(self, cond: CondTables, transformer):
         """Tables for sample_zero + fused decode (transformer: a fitted VGMTransformer)."""
@@ -615,10 +615,18 @@ class CTGANEngine:
         if use_graph is None:
             use_graph = self.device.type == "cuda"
         if use_graph:
-            if self.graph is None:
-                self._capture()
-            for _ in range(n):
-                self.graph.replay()
+            # U steps per graph launch (the per-launch gap between graphs is paid n/U times)
+            U = max(1, int(self.cfg.graph_unroll))
+            left = n
+            if left >= U:
+                g = self.graphs.get(U) or self._capture(U)
+                for _ in range(left // U):
+                    g.replay()
+                left %= U
+            if left:
+                g1 = self.graphs.get(1) or self._capture(1)
+                for _ in range(left):
+                    g1.replay()
         else:
             for _ in range(n):
                 self._one_step()
@@ -627,12 +635,12 @@ class CTGANEngine:
     def train_epoch(self, use_graph: bool | None = None):
         self.train_steps(self.steps_per_epoch, use_graph)
 
-    def _capture(self):
+    def _capture(self, steps: int = 1):
         from ..utils.devsync import CAPTURE_LOCK
         with CAPTURE_LOCK:      # no device-wide sync from another client thread meanwhile
-            self._capture_locked()
+            return self._capture_locked(steps)
 
-    def _capture_locked(self):
+    def _capture_locked(self, steps: int = 1):
         # warm up on a side stream (allocator / lazy init), then capture one step
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -647,8 +655,15 @@ class CTGANEngine:
             dst.copy_(src)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
-            self._one_step()
-        self.graph = g
+            for _ in range(steps):      # every step re-reads the device RNG/step counters
+                self._one_step()
+        self.graphs[steps] = g
+        return g
+
+    @property
+    def graph(self):
+        """The one-step graph, if captured (inspection / tests)."""
+        return self.graphs.get(1)
 
     def losses(self) -> Tuple[float, float]:
         m = self.metrics.detach().cpu().numpy()
