@@ -103,7 +103,7 @@ def main():
             "higher_is_better": False, "scaling": "weak",
             "vs_baseline": round(sec_per_epoch / BASELINE_SEC_PER_EPOCH, 6),
             "dtype": cfg.engine.precision if rt.engine.ops.name == "hip" else "fp32",
-            "data": "synthetic (Intrusion schema, 40000 rows per client)",
+            "data": f"synthetic (Intrusion schema, {args.rows} rows per client; random-init weights)",
             "config": {"model": "Fed-TGAN CTGAN (G 256x256 residual+BN, D 256x256 pack10, WGAN-GP slerp)",
                        "global_batch": 500 * world, "seq_len": None, "parallelism": f"fed{world}",
                        "rows_per_client": args.rows, "n_sample": args.n_sample,
