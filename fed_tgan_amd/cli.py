@@ -83,6 +83,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-batch_size", type=int, default=500)
     p.add_argument("-timeout", type=float, default=600.0)
     p.add_argument("-dump_real", action="store_true", help="write the synthetic client shards under out_dir/data/raw")
+    p.add_argument("-profile_dir", default=None, help="export a torch.profiler Chrome trace of round 1 here")
     p.add_argument("-grad_flow", action="store_true", help="write reports/grad_flow.{csv,png} (client 0)")
     p.add_argument("-sync_csv", action="store_true",
                    help="write each epoch CSV inside its round (reference timing) instead of in the background")
@@ -115,7 +116,7 @@ def fed_config_from_args(args):
                      engine=EngineConfig(batch_size=args.batch_size, precision=args.precision),
                      ckpt_every=args.ckpt_every, resume=args.resume, verbose=not args.quiet,
                      metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
-                     e_interval=args.E_interval, grad_flow=args.grad_flow,
+                     e_interval=args.E_interval, grad_flow=args.grad_flow, profile_dir=args.profile_dir,
                      dump_real=args.dump_real, async_csv=not args.sync_csv)
 
 

@@ -86,6 +86,8 @@ class FedConfig:
     device_encode: bool = True              # GPU: VGM-encode with the HIP kernel (csrc/kernels/vgm.hip)
     grad_flow: bool = False                 # record per-layer mean |grad| each round (utils/gradflow.py)
     e_interval: int = 1                     # fedavg: local epochs per aggregation; mdgan: D-swap period
+    profile_dir: Optional[str] = None       # export a torch.profiler trace of round `profile_epoch`
+    profile_epoch: int = 1
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
 
 
@@ -392,6 +394,16 @@ class FedRuntime:
         c.all_reduce_cpu(m)
         self._losses = m / max(c.n_clients, 1)
 
+    def _profiled_round(self, epoch: int) -> float:
+        """One round under torch.profiler (host ops + HIP kernels), exported as a Chrome trace."""
+        from torch.profiler import ProfilerActivity, profile
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.device.type == "cuda" else [])
+        os.makedirs(self.cfg.profile_dir, exist_ok=True)
+        with profile(activities=acts, record_shapes=False) as prof:
+            dt = self.run_round(epoch)
+        prof.export_chrome_trace(os.path.join(self.cfg.profile_dir, f"trace_rank{self.rank}_epoch{epoch}.json"))
+        return dt
+
     def round_losses(self):
         """(loss_d, loss_g) of the last step, as the federator reports them."""
         m = getattr(self, "_losses", None)
@@ -402,7 +414,10 @@ class FedRuntime:
     def fit(self):
         cfg = self.cfg
         for ep in range(self.start_epoch, cfg.epochs):
-            dt = self.run_round(ep)
+            if cfg.profile_dir and ep == cfg.profile_epoch:
+                dt = self._profiled_round(ep)
+            else:
+                dt = self.run_round(ep)
             self.round_times.append(dt)
             if self.is_fed:
                 ld, lg = self.round_losses()

@@ -129,3 +129,9 @@ def test_cli_colocated_two_ranks(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     df = pd.read_csv(tmp_path / "Intrusion_result" / "Intrusion_synthesis_epoch_1.csv")
     assert df.shape == (501, 42)
+
+
+def test_profiled_round_exports_trace(tmp_path):
+    cfg = _cfg(tmp_path, epochs=2, profile_dir=str(tmp_path / "prof"))
+    run_local_emulation(cfg, 1, backend="torch", device=torch.device("cpu"))
+    assert (tmp_path / "prof" / "trace_rank0_epoch1.json").stat().st_size > 0
