@@ -83,6 +83,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-batch_size", type=int, default=500)
     p.add_argument("-timeout", type=float, default=600.0)
     p.add_argument("-dump_real", action="store_true", help="write the synthetic client shards under out_dir/data/raw")
+    p.add_argument("-heartbeat", type=float, default=0.0,
+                   help="per-round monitored barrier: fail fast (naming the dead ranks) after this many seconds")
     p.add_argument("-profile_dir", default=None, help="export a torch.profiler Chrome trace of round 1 here")
     p.add_argument("-grad_flow", action="store_true", help="write reports/grad_flow.{csv,png} (client 0)")
     p.add_argument("-sync_csv", action="store_true",
@@ -117,6 +119,7 @@ def fed_config_from_args(args):
                      ckpt_every=args.ckpt_every, resume=args.resume, verbose=not args.quiet,
                      metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
                      e_interval=args.E_interval, grad_flow=args.grad_flow, profile_dir=args.profile_dir,
+                     heartbeat_s=args.heartbeat,
                      dump_real=args.dump_real, async_csv=not args.sync_csv)
 
 

@@ -81,6 +81,9 @@ class ThreadComm(Comm):
     def max_float(self, x: float) -> float:
         return max(self.all_gather_object(float(x)))
 
+    def heartbeat(self, timeout_s: float):
+        self.g.wait()
+
     def gather_rows(self, t, counts, ranks, dst: int = 0):
         parts = self.all_gather_object(t.cpu())
         if self.rank != dst:

@@ -86,6 +86,7 @@ class FedConfig:
     device_encode: bool = True              # GPU: VGM-encode with the HIP kernel (csrc/kernels/vgm.hip)
     grad_flow: bool = False                 # record per-layer mean |grad| each round (utils/gradflow.py)
     e_interval: int = 1                     # fedavg: local epochs per aggregation; mdgan: D-swap period
+    heartbeat_s: float = 0.0                # >0: per-round monitored barrier naming dead ranks
     profile_dir: Optional[str] = None       # export a torch.profiler trace of round `profile_epoch`
     profile_epoch: int = 1
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
@@ -418,6 +419,11 @@ class FedRuntime:
                 dt = self._profiled_round(ep)
             else:
                 dt = self.run_round(ep)
+            fault = os.environ.get("FEDTGAN_FAULT_EXIT")   # "rank:epoch" -- test hook: that rank dies
+            if fault and fault == f"{self.rank}:{ep}":
+                os._exit(3)
+            if cfg.heartbeat_s > 0:
+                self.comm.heartbeat(cfg.heartbeat_s)
             self.round_times.append(dt)
             if self.is_fed:
                 ld, lg = self.round_losses()

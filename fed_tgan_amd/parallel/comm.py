@@ -103,6 +103,14 @@ class Comm:
         if self.world_size > 1:
             dist.barrier(group=self.ctrl)
 
+    def heartbeat(self, timeout_s: float):
+        """Failure detection: a monitored gloo barrier over the control plane.  If a rank does not
+        arrive within ``timeout_s`` every live rank raises, naming the missing ranks (instead of
+        hanging until the process-group timeout)."""
+        if self.world_size > 1:
+            dist.monitored_barrier(group=self.ctrl, timeout=datetime.timedelta(seconds=timeout_s),
+                                   wait_all_ranks=True)
+
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         """Broadcast a tensor over the control plane (device tensors are staged through host memory)."""
         if self.world_size == 1:

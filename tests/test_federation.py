@@ -135,3 +135,16 @@ def test_profiled_round_exports_trace(tmp_path):
     cfg = _cfg(tmp_path, epochs=2, profile_dir=str(tmp_path / "prof"))
     run_local_emulation(cfg, 1, backend="torch", device=torch.device("cpu"))
     assert (tmp_path / "prof" / "trace_rank0_epoch1.json").stat().st_size > 0
+
+
+@pytest.mark.slow
+def test_heartbeat_names_a_dead_rank(tmp_path):
+    """Failure detection: rank 1 dies after its first round; with -heartbeat the survivors fail
+    fast with an error naming rank 1 instead of waiting out the process-group timeout."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", FEDTGAN_FAULT_EXIT="1:0")
+    r = subprocess.run([sys.executable, "-m", "dtds.distributed", "-world_size", "2", "-colocated", "-epochs", "3",
+                        "-backend", "torch", "-synthetic_rows", "1000", "-n_sample", "200", "-batch_size", "100",
+                        "-heartbeat", "5", "-out_dir", str(tmp_path), "-quiet"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "1" in r.stderr and ("monitoredBarrier" in r.stderr or "process 1" in r.stderr.lower()), r.stderr[-2000:]
