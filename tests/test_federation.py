@@ -139,12 +139,24 @@ def test_profiled_round_exports_trace(tmp_path):
 
 @pytest.mark.slow
 def test_heartbeat_names_a_dead_rank(tmp_path):
-    """Failure detection: rank 1 dies after its first round; with -heartbeat the survivors fail
-    fast with an error naming rank 1 instead of waiting out the process-group timeout."""
+    """Failure detection: rank 1 (its own process, reference-style explicit -rank launch) dies
+    after its first round; with -heartbeat, rank 0 fails fast with a monitored-barrier error
+    naming rank 1 instead of waiting out the process-group timeout."""
+    import socket
+    import time
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = str(so.getsockname()[1])
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", FEDTGAN_FAULT_EXIT="1:0")
-    r = subprocess.run([sys.executable, "-m", "dtds.distributed", "-world_size", "2", "-colocated", "-epochs", "3",
-                        "-backend", "torch", "-synthetic_rows", "1000", "-n_sample", "200", "-batch_size", "100",
-                        "-heartbeat", "5", "-out_dir", str(tmp_path), "-quiet"], cwd=ROOT, env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode != 0
-    assert "1" in r.stderr and ("monitoredBarrier" in r.stderr or "process 1" in r.stderr.lower()), r.stderr[-2000:]
+    args = ["-world_size", "2", "-colocated", "-epochs", "3", "-backend", "torch", "-synthetic_rows", "1000",
+            "-n_sample", "200", "-batch_size", "100", "-heartbeat", "5", "-out_dir", str(tmp_path), "-quiet",
+            "-ip", "127.0.0.1", "-port", port]
+    procs = [subprocess.Popen([sys.executable, "-m", "dtds.distributed", "-rank", str(r)] + args, cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in (0, 1)]
+    t0 = time.time()
+    out0, err0 = procs[0].communicate(timeout=300)
+    procs[1].communicate(timeout=60)
+    assert procs[1].returncode == 3
+    assert procs[0].returncode != 0
+    assert "monitoredBarrier" in err0 and "1" in err0, err0[-2000:]
+    assert time.time() - t0 < 240
