@@ -27,6 +27,18 @@ void check_f32_2d(const Tensor& t, const char* name) {
 
 int ld_of(const Tensor& t) { return (int)(t.size(0) <= 1 ? std::max<int64_t>(t.size(1), 1) : t.stride(0)); }
 
+// May a GEMM operand be read with 16-B loads?  Base 16-B aligned, ld % 4 == 0, and every row's
+// contiguous extent rounded up to a multiple of 4 fits in ld and -- for the last row -- inside
+// the tensor's storage (reads past the logical edge hit padding or the next row, which staging
+// zeroes; never memory outside the storage).
+bool vec_ok(const Tensor& t) {
+  const int64_t ld = ld_of(t);
+  const int64_t ext4 = (t.size(1) + 3) / 4 * 4;
+  if (reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 != 0 || ld % 4 != 0 || ext4 > ld) return false;
+  const int64_t storage = (int64_t)(t.storage().nbytes() / sizeof(float));
+  return t.storage_offset() + (t.size(0) - 1) * ld + ext4 <= storage;
+}
+
 float* fp(const Tensor& t) { return t.data_ptr<float>(); }
 const float* cfp(const Tensor& t) { return t.data_ptr<float>(); }
 template <typename T>
@@ -91,6 +103,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.rng_stream = (uint32_t)stream;
   g.f32 = f32 ? 1 : 0;
   TORCH_CHECK(tile == 32 || tile == 64, "gemm: tile must be 32 or 64");
+  g.vec = (vec_ok(a) && vec_ok(b)) ? 1 : 0;
   g.tile = (int)tile;
   if (head_a.has_value() && head_a->defined()) {
     TORCH_CHECK(epi == fedtgan::EPI_LRELU_DROPOUT, "gemm: the head seed needs the LeakyReLU+dropout epilogue");

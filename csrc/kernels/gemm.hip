@@ -84,9 +84,10 @@ struct Chunk {
 
   // Issue the burst's loads (and nothing that waits on them, so the burst stays in flight).
   // VEC (a kernel template parameter, so each variant is straight-line code and the compiler's
-  // load-counter waits stay exact): base 16-B aligned, ld % 4 == 0 and the vector extent (kmax
-  // for ROWMAJ, rmax otherwise) % 4 == 0, so every float4 is entirely inside or entirely
-  // outside the operand and its address can simply be clamped.
+  // load-counter waits stay exact; decided on the host from the tensor's storage): base 16-B
+  // aligned, ld % 4 == 0, and every row's contiguous extent rounded up to 4 still lies inside its
+  // ld-long storage row -- so a float4 may run past the logical edge (into padding that staging
+  // zeroes) but never past the storage, and its start is clamped to ceil4(extent) - 4.
   template <bool VEC>
   __device__ __forceinline__ void load(const float* __restrict__ p, int ld, int r0_, int rmax_, int k0_, int kmax_) {
     r0 = r0_;
@@ -99,7 +100,7 @@ struct Chunk {
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
           const int rr = r0 + t / (KC / 4) + (NT / (KC / 4)) * i;
-          const int k = min(k0 + 4 * (t % (KC / 4)), kmax - 4);
+          const int k = min(k0 + 4 * (t % (KC / 4)), ((kmax + 3) & ~3) - 4);
           v[i] = *reinterpret_cast<const f32x4*>(p + (size_t)min(rr, rmax - 1) * ld + k);
         }
       } else {
@@ -116,7 +117,7 @@ struct Chunk {
       if constexpr (VEC) {
 #pragma unroll
         for (int i = 0; i < NV / 2; ++i) {
-          const int rr = min(r0 + 4 * (t % RQ), rmax - 4);
+          const int rr = min(r0 + 4 * (t % RQ), ((rmax + 3) & ~3) - 4);
           const int k = k0 + 2 * (t / RQ + (NT / RQ) * i);
           v[2 * i] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k, kmax - 1) * ld + rr);
           v[2 * i + 1] = *reinterpret_cast<const f32x4*>(p + (size_t)min(k + 1, kmax - 1) * ld + rr);
@@ -356,11 +357,7 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
   g.kchunk = kchunk;
   dim3 grid(tn, tm, g.splitk), block(NT);
-  // 16-B operand loads (see Chunk::load) when both operands allow them; the vector extent is K
-  // for k-contiguous operands (every split boundary is a multiple of KC), the row count otherwise
-  const bool va = ((uintptr_t)g.a % 16 == 0) && (g.lda % 4 == 0) && ((g.ta ? g.M : g.K) % 4 == 0);
-  const bool vb = ((uintptr_t)g.b % 16 == 0) && (g.ldb % 4 == 0) && ((g.tb ? g.K : g.N) % 4 == 0);
-  const bool vec = va && vb;
+  const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
   if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, 0, stream, g);       \
   else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT>), grid, block, 0, stream, g); \

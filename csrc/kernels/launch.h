@@ -39,6 +39,7 @@ struct GemmArgs {
   const uint64_t* rng_ctr;
   uint32_t rng_stream;
   int splitk, kchunk;
+  int vec;     // 1: both operands may be read with 16-B loads (see gemm.hip Chunk::load)
   int tile;    // output tile edge: 64 (default) or 32 (4x the workgroups, for short-K GEMMs)
   int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
 };

@@ -394,3 +394,26 @@ def test_activate_with_fused_slerp_matches_standalone(hip):
     torch.cuda.synchronize()
     assert torch.equal(fake, xd2[0:B])
     assert torch.allclose(interp, xd2[2 * B:], atol=2e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(500, 325, 943), (150, 254, 6263), (37, 61, 150)])
+def test_gemm_padded_views_use_vector_loads(hip, ta, tb, M, N, K):
+    """Operands that are column views of 4-padded storage (odd logical widths, as the engine's
+    padded buffers are) take the 16-B load path; the padding must never leak into the result."""
+    def padded(r, c, seed):
+        base = torch.full((r, (c + 3) // 4 * 4), float("nan"), device=DEV)   # poison the padding
+        base[:, :c] = mat(r, c, seed=seed)
+        return base[:, :c]
+    a = padded(*((K, M) if ta else (M, K)), seed=61)
+    b = padded(*((N, K) if tb else (K, N)), seed=62)
+    c = torch.zeros(M, N, device=DEV)
+    for tile in (32, 64):
+        hip.tile_override = tile
+        hip.gemm(a, b, c, ta=ta, tb=tb)
+        torch.cuda.synchronize()
+        A = bf(a).t() if ta else bf(a)
+        B = bf(b).t() if tb else bf(b)
+        assert torch.isfinite(c).all()
+        assert (c - A @ B).abs().max().item() <= 1e-4 * math.sqrt(K) * 10 + 1e-5
+    hip.tile_override = None
