@@ -159,6 +159,8 @@ __device__ __forceinline__ void slerp_weights(float saa, float sbb, float sab, f
 }
 
 constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
+constexpr int ACT_PF = 8;      // logits prefetched per lane (rows up to 512 wide)
+constexpr int ACT_PFS = 12;    // slerp real-row values prefetched per lane (rows up to 768 wide)
 constexpr size_t LDS_BYTES = 160 * 1024;
 
 struct ActSmem {
@@ -196,20 +198,31 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
                                                                   const uint64_t* ctr, uint32_t stream_id,
                                                                   SlerpFuse sl) {
   extern __shared__ float act_smem[];
-  const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
-  if (r >= rows) return;
+  const int rc = min(r, rows - 1);
   const int D = sp.dim, S = sp.n_span;
+  const float* x = logits + (size_t)rc * ldl;
+  // the row's logits (and the slerp's real row) are requested before the span tables are staged,
+  // so the three global round trips overlap (rows up to ACT_PF*64 wide stay in registers)
+  const bool pre = D <= ACT_PF * 64;
+  float xr[ACT_PF];
+#pragma unroll
+  for (int k = 0; k < ACT_PF; ++k) xr[k] = pre ? x[min(lane + 64 * k, D - 1)] : 0.f;
+  const bool pre_s = sl.real != nullptr && sl.cols <= ACT_PFS * 64;
+  const float* a_row = sl.real ? sl.real + (size_t)rc * sl.ld : nullptr;
+  float ar[ACT_PFS];
+#pragma unroll
+  for (int k = 0; k < ACT_PFS; ++k) ar[k] = pre_s ? a_row[min(lane + 64 * k, sl.cols - 1)] : 0.f;
+  const ActSmem t = act_stage_tables(sp, act_smem);
+  if (r >= rows) return;
   float* v = t.rows + (size_t)wv * (D + 2 * S);
   float* stat = v + D;
-  const float* x = logits + (size_t)r * ldl;
   float* y = out + (size_t)r * ldo;
   const uint64_t step = ctr ? *ctr : 0ull;
   RngArgs rng{seed, ctr, stream_id};
   const uint64_t base = (uint64_t)r << 20;
-  for (int j = lane; j < D; j += 64) {
-    const float xv = x[j];
+  auto act_elem = [&](int j, float xv) {
     if (t.kind[t.elem[j]] == 0) {
       const float th = tanhf(xv);
       y[j] = th;
@@ -217,6 +230,13 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
     } else {
       v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
     }
+  };
+  if (pre) {
+#pragma unroll
+    for (int k = 0; k < ACT_PF; ++k)
+      if (lane + 64 * k < D) act_elem(lane + 64 * k, xr[k]);
+  } else {
+    for (int j = lane; j < D; j += 64) act_elem(j, x[j]);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -243,13 +263,26 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   if (sl.real == nullptr) return;
   // fused slerp(real_r, fake_r) of the gradient penalty (one launch less per step): the fake row
   // is this row's activation (LDS, j < D) followed by its conditional columns (global)
-  const float* a = sl.real + (size_t)r * sl.ld;
+  const float* a = a_row;
   float saa = 0.f, sbb = 0.f, sab = 0.f;
-  for (int j = lane; j < sl.cols; j += 64) {
-    const float ra = a[j], fb = j < D ? v[j] : y[j];
-    saa += ra * ra;
-    sbb += fb * fb;
-    sab += ra * fb;
+  if (pre_s) {
+#pragma unroll
+    for (int k = 0; k < ACT_PFS; ++k) {
+      const int j = lane + 64 * k;
+      if (j < sl.cols) {
+        const float ra = ar[k], fb = j < D ? v[j] : y[j];
+        saa += ra * ra;
+        sbb += fb * fb;
+        sab += ra * fb;
+      }
+    }
+  } else {
+    for (int j = lane; j < sl.cols; j += 64) {
+      const float ra = a[j], fb = j < D ? v[j] : y[j];
+      saa += ra * ra;
+      sbb += fb * fb;
+      sab += ra * fb;
+    }
   }
   saa = wave_sum(saa);
   sbb = wave_sum(sbb);
@@ -259,7 +292,15 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   float wa, wb;
   slerp_weights(saa, sbb, sab, alpha, wa, wb);
   float* o = sl.out + (size_t)r * sl.ld;
-  for (int j = lane; j < sl.cols; j += 64) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
+  if (pre_s) {
+#pragma unroll
+    for (int k = 0; k < ACT_PFS; ++k) {
+      const int j = lane + 64 * k;
+      if (j < sl.cols) o[j] = wa * ar[k] + wb * (j < D ? v[j] : y[j]);
+    }
+  } else {
+    for (int j = lane; j < sl.cols; j += 64) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
+  }
 }
 
 static size_t act_smem_bytes(const SpanTables& sp, int waves) {
@@ -297,20 +338,38 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
                                                                     int ldg, int rows, float inv_tau, float* loss) {
   extern __shared__ float act_smem[];
-  const ActSmem t = act_stage_tables(sp, act_smem);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
-  if (r >= rows) return;
+  const int rc = min(r, rows - 1);
   const int D = sp.dim, S = sp.n_span;
+  const float* g = dact + (size_t)rc * ldd;
+  const float* y = act + (size_t)rc * lda;
+  const float* x = logits + (size_t)rc * ldl;
+  // the row's gradients, activations and logits (and its conditional column) are requested
+  // before the span tables are staged: one overlapped round trip instead of three
+  const bool pre = D <= ACT_PF * 64;
+  float gr[ACT_PF], yr[ACT_PF], xr[ACT_PF];
+#pragma unroll
+  for (int k = 0; k < ACT_PF; ++k) {
+    const int j = min(lane + 64 * k, D - 1);
+    gr[k] = pre ? g[j] : 0.f;
+    yr[k] = pre ? y[j] : 0.f;
+    xr[k] = pre ? x[j] : 0.f;
+  }
+  const int cr = col[rc];
+  const int orow = opt[rc];
+  const ActSmem t = act_stage_tables(sp, act_smem);
+  if (r >= rows) return;
   float* gy = t.rows + (size_t)wv * (D + 2 * S);
   float* stat = gy + D;
-  const float* g = dact + (size_t)r * ldd;
-  const float* y = act + (size_t)r * lda;
-  const float* x = logits + (size_t)r * ldl;
   float* d = dl + (size_t)r * ldg;
-  const int cr = col[r];
-  const int orow = opt[r];
-  for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
+  if (pre) {
+#pragma unroll
+    for (int k = 0; k < ACT_PF; ++k)
+      if (lane + 64 * k < D) gy[lane + 64 * k] = gr[k] * yr[k];
+  } else {
+    for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   int ce_span = -1;
@@ -345,17 +404,23 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
   __builtin_amdgcn_wave_barrier();
   const int ot = cst + min(orow, max(cw - 1, 0));
   const float invB = 1.f / (float)rows;
-  for (int j = lane; j < D; j += 64) {
+  auto grad_elem = [&](int j, float gj, float yj, float xj) {
     const int s = t.elem[j];
     float v;
     if (t.kind[s] == 0) {
-      const float yy = y[j];
-      v = g[j] * (1.f - yy * yy);
+      v = gj * (1.f - yj * yj);
     } else {
-      v = y[j] * (g[j] - stat[2 * s]) * inv_tau;
-      if (j >= cst && j < cst + cw) v += (__expf(x[j] - lse) - (j == ot ? 1.f : 0.f)) * invB;
+      v = yj * (gj - stat[2 * s]) * inv_tau;
+      if (j >= cst && j < cst + cw) v += (__expf(xj - lse) - (j == ot ? 1.f : 0.f)) * invB;
     }
     d[j] = v;
+  };
+  if (pre) {
+#pragma unroll
+    for (int k = 0; k < ACT_PF; ++k)
+      if (lane + 64 * k < D) grad_elem(lane + 64 * k, gr[k], yr[k], xr[k]);
+  } else {
+    for (int j = lane; j < D; j += 64) grad_elem(j, g[j], y[j], x[j]);
   }
 }
 
