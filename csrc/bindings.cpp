@@ -123,7 +123,8 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
             int64_t Dd, const Tensor& cdf, const Tensor& cond_off, const Tensor& cond_w, const optional<Tensor>& row_off,
             const optional<Tensor>& row_cnt, const optional<Tensor>& rows, const optional<Tensor>& data,
             const optional<Tensor>& col, const optional<Tensor>& opt, const optional<Tensor>& step_bump,
-            const optional<Tensor>& metrics, bool zero_metrics, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+            const optional<Tensor>& step_bump2, const optional<Tensor>& metrics, bool zero_metrics, int64_t seed,
+            const Tensor& rng_ctr, int64_t stream) {
   check_f32_2d(h, "h");
   fedtgan::SampleArgs a{};
   a.B = (int)h.size(0);
@@ -144,8 +145,9 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
   }
   if (xr.has_value() && xr->defined()) {
     check_f32_2d(*xr, "xr");
-    TORCH_CHECK(xr->size(0) == a.B && xr->size(1) == Dd + a.C, "sample: xr shape");
-    TORCH_CHECK(a.B <= 4096, "sample: batch > 4096 not supported by the in-LDS permutation");
+    // the real block may cover only the leading rows (a D-phase batch drawn together with a G-phase one)
+    TORCH_CHECK(xr->size(0) >= 1 && xr->size(0) <= a.B && xr->size(1) == Dd + a.C, "sample: xr shape");
+    a.n_real = (int)xr->size(0);
     TORCH_CHECK(row_off.has_value() && row_cnt.has_value() && rows.has_value() && data.has_value(), "sample: tables");
     TORCH_CHECK(data->size(1) == Dd && data->is_contiguous(), "sample: data");
     a.xr = fp(*xr);
@@ -161,6 +163,7 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
   a.col = optp<int>(col);
   a.opt = optp<int>(opt);
   a.step_bump = optp<float>(step_bump);
+  a.step_bump2 = optp<float>(step_bump2);
   a.metrics = optp<float>(metrics);
   a.zero_metrics = zero_metrics ? 1 : 0;
   a.seed = (uint64_t)seed;
@@ -196,13 +199,15 @@ void activate(const Tensor& logits, const Tensor& out, const Tensor& start, cons
     check_f32_2d(*slerp_real, "slerp real");
     check_f32_2d(*slerp_out, "slerp out");
     TORCH_CHECK(ld_of(*slerp_real) == ld_of(*slerp_out) && ld_of(*slerp_real) == ld_of(out), "activate: slerp strides");
-    TORCH_CHECK(slerp_real->size(0) == out.size(0) && slerp_out->size(0) == out.size(0) &&
+    TORCH_CHECK(slerp_real->size(0) >= 1 && slerp_real->size(0) <= out.size(0) &&
+                    slerp_out->size(0) == slerp_real->size(0) &&
                     slerp_real->size(1) == slerp_cols && slerp_out->size(1) == slerp_cols &&
                     slerp_cols >= logits.size(1) && slerp_cols <= ld_of(out), "activate: slerp shapes");
     sl.real = cfp(*slerp_real);
     sl.out = fp(*slerp_out);
     sl.ld = ld_of(out);
     sl.cols = (int)slerp_cols;
+    sl.rows = (int)slerp_real->size(0);
     sl.stream = (uint32_t)slerp_stream;
   }
   fedtgan::launch_activate(cfp(logits), ld_of(logits), fp(out), ld_of(out), (int)logits.size(0),
@@ -303,15 +308,19 @@ void colsum(at::TensorList srcs, at::TensorList outs) {
 
 void bn_relu_train(const Tensor& a, const Tensor& gamma, const Tensor& beta, const Tensor& out, const Tensor& nhat,
                    const Tensor& mean, const Tensor& invstd, const Tensor& rm, const Tensor& rv, double momentum,
-                   double eps) {
+                   double eps, int64_t groups) {
   check_f32_2d(a, "a");
   check_f32_2d(out, "out");
   check_f32_2d(nhat, "nhat");
   TORCH_CHECK(a.size(0) <= 1024, "bn_relu_train: batch > 1024 unsupported (rows kept in registers)");
+  TORCH_CHECK(groups == 1 || groups == 2, "bn_relu_train: 1 or 2 batches");
+  TORCH_CHECK(a.size(0) % groups == 0 && a.size(0) / groups >= 1, "bn_relu_train: rows must split evenly");
   TORCH_CHECK(out.sizes() == a.sizes() && nhat.sizes() == a.sizes() && gamma.numel() == a.size(1), "bn: shapes");
+  TORCH_CHECK(mean.is_contiguous() && invstd.is_contiguous() && mean.numel() == groups * a.size(1) &&
+                  invstd.numel() == groups * a.size(1), "bn_relu_train: mean/invstd must be contiguous [groups, cols]");
   fedtgan::launch_bn_relu_train(cfp(a), ld_of(a), cfp(gamma), cfp(beta), fp(out), ld_of(out), fp(nhat), ld_of(nhat),
-                                fp(mean), fp(invstd), fp(rm), fp(rv), (int)a.size(0), (int)a.size(1), (float)momentum,
-                                (float)eps, cur_stream());
+                                fp(mean), fp(invstd), fp(rm), fp(rv), (int)a.size(0), (int)a.size(1), (int)groups,
+                                (float)momentum, (float)eps, cur_stream());
 }
 
 void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Tensor& gamma, const Tensor& invstd,
@@ -481,7 +490,8 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
-      "Tensor(f!)? step_bump, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, int stream) -> ()");
+      "Tensor(f!)? step_bump, Tensor(h!)? step_bump2, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, "
+      "int stream) -> ()");
   m.def(
       "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, Tensor elem, "
       "float tau, int seed, Tensor rng_ctr, int stream, Tensor? slerp_real, Tensor(b!)? slerp_out, int slerp_cols, "
@@ -498,7 +508,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("colsum_ex(Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, Tensor?[] dot_e, Tensor?[] dot_out) -> ()");
   m.def(
       "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
-      "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps) -> ()");
+      "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
   m.def(
       "bn_relu_bwd(Tensor dr, Tensor r, Tensor nhat, Tensor gamma, Tensor invstd, Tensor(a!) da, Tensor(b!) dgamma, "
       "Tensor(c!) dbeta, Tensor(d!)? dbias) -> ()");

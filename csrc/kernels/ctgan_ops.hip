@@ -84,11 +84,14 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (blockIdx.x == 0 && tid == 0) {
     if (a.step_bump) a.step_bump[0] += 1.0f;
+    if (a.step_bump2) a.step_bump2[0] += 1.0f;
     if (a.zero_metrics && a.metrics) {
       a.metrics[0] = 0.f; a.metrics[1] = 0.f; a.metrics[2] = 0.f; a.metrics[3] = 0.f;
     }
   }
-  const bool with_real = a.xr != nullptr && a.n_col > 0;
+  // rows [0, n_real) get a real row (the D phase); the rest only noise + condition (the G phase
+  // of the same step when both batches are drawn by one launch)
+  const int n_real = (a.xr != nullptr && a.n_col > 0) ? a.n_real : 0;
   RngArgs rk{a.seed, a.rng_ctr, a.rng_stream + 1u};
   const uint4 pkey = rng4(rk, step, 0ull);
   RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
@@ -113,9 +116,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
       if (xf) xf[i] = v;
     }
     if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
-    if (!with_real) continue;
-    // real row drawn for the condition of fake row perm[b]
-    const int p = (int)feistel_perm((uint32_t)b, (uint32_t)a.B, pkey);
+    if (b >= n_real) continue;
+    // real row drawn for the condition of fake row perm[b] (a permutation of the real-row block)
+    const int p = (int)feistel_perm((uint32_t)b, (uint32_t)n_real, pkey);
     int pc = 0, po = 0;
     draw_cond_wave(a, step, p, lane, pc, po);
     const int64_t cnt = a.row_cnt[(size_t)pc * a.maxw + po];
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
 #pragma unroll
   for (int k = 0; k < ACT_PF; ++k) xr[k] = pre ? x[min(lane + 64 * k, D - 1)] : 0.f;
   const bool pre_s = sl.real != nullptr && sl.cols <= ACT_PFS * 64;
-  const float* a_row = sl.real ? sl.real + (size_t)rc * sl.ld : nullptr;
+  const float* a_row = sl.real ? sl.real + (size_t)min(rc, sl.rows - 1) * sl.ld : nullptr;
   float ar[ACT_PFS];
 #pragma unroll
   for (int k = 0; k < ACT_PFS; ++k) ar[k] = pre_s ? a_row[min(lane + 64 * k, sl.cols - 1)] : 0.f;
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
       v[j] = o;     // each lane re-reads only its own elements below
     }
   }
-  if (sl.real == nullptr) return;
+  if (sl.real == nullptr || r >= sl.rows) return;
   // fused slerp(real_r, fake_r) of the gradient penalty (one launch less per step): the fake row
   // is this row's activation (LDS, j < D) followed by its conditional columns (global)
   const float* a = a_row;
@@ -588,66 +591,85 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
 // Loads use clamped (always valid) addresses and are masked afterwards (no predicated loads).
 constexpr int BN_COLS = 16, BN_GROUPS = 32;
 
+// ``groups`` (1 or 2) independent batches of rows/groups consecutive rows each: the D-phase and
+// G-phase batches of a step go through the generator as ONE M = 2B GEMM chain, but BatchNorm keeps
+// per-batch statistics (`ctgan.py:40-44` runs twice per step) and the running statistics are
+// updated batch after batch, in row order -- exactly the reference's two forward passes.
+constexpr int BN_MAXG = 2;
+
 template <int MAXR>
 __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
-    float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, float momentum,
-    float eps) {
-  __shared__ float red[BN_GROUPS][BN_COLS + 1];
-  __shared__ float stat[2][BN_COLS];
+    float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
+    float momentum, float eps) {
+  __shared__ float red[BN_MAXG][BN_GROUPS][BN_COLS + 1];
+  __shared__ float stat[BN_MAXG][2][BN_COLS];
   const int lc = threadIdx.x % BN_COLS, grp = threadIdx.x / BN_COLS;
   const int c = blockIdx.x * BN_COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
+  const int rpg = rows / groups;
   float x[MAXR];
-  float s = 0.f;
+  float s[BN_MAXG] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
     const float v = a[(size_t)min(r, rows - 1) * lda + cc];
     x[i] = (r < rows) ? v : 0.f;
-    s += x[i];
+    if (r >= rpg) s[1] += x[i]; else s[0] += x[i];
   }
-  red[grp][lc] = s;
+#pragma unroll
+  for (int g = 0; g < BN_MAXG; ++g) red[g][grp][lc] = s[g];
   __syncthreads();
-  if (grp == 0) {
+  if (grp < groups) {   // one row-group of threads per batch
     float t = 0.f;
-    for (int i = 0; i < BN_GROUPS; ++i) t += red[i][lc];
-    stat[0][lc] = t / (float)rows;
+    for (int i = 0; i < BN_GROUPS; ++i) t += red[grp][i][lc];
+    stat[grp][0][lc] = t / (float)rpg;
   }
   __syncthreads();
-  const float mu = stat[0][lc];
-  float q = 0.f;
+  const float mu0 = stat[0][0][lc], mu1 = groups > 1 ? stat[1][0][lc] : 0.f;
+  float q[BN_MAXG] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
-    const float d = (r < rows) ? x[i] - mu : 0.f;
-    q += d * d;
+    const bool g1 = r >= rpg;
+    const float d = (r < rows) ? x[i] - (g1 ? mu1 : mu0) : 0.f;
+    if (g1) q[1] += d * d; else q[0] += d * d;
   }
   __syncthreads();
-  red[grp][lc] = q;
+#pragma unroll
+  for (int g = 0; g < BN_MAXG; ++g) red[g][grp][lc] = q[g];
   __syncthreads();
-  if (grp == 0) {
+  if (grp < groups) {
     float t = 0.f;
-    for (int i = 0; i < BN_GROUPS; ++i) t += red[i][lc];
-    const float var = t / (float)rows;
-    stat[1][lc] = rsqrtf(var + eps);
-    if (ok) {
-      mean[c] = mu;
-      invstd[c] = stat[1][lc];
-      rm[c] = (1.f - momentum) * rm[c] + momentum * mu;
-      rv[c] = (1.f - momentum) * rv[c] + momentum * var * (float)rows / (float)max(rows - 1, 1);
-    }
+    for (int i = 0; i < BN_GROUPS; ++i) t += red[grp][i][lc];
+    stat[grp][1][lc] = t / (float)rpg;    // biased batch variance
   }
   __syncthreads();
+  if (grp == 0 && ok) {
+    float m = rm[c], v = rv[c];
+    const float unb = (float)rpg / (float)max(rpg - 1, 1);
+    for (int g = 0; g < groups; ++g) {   // batch after batch, in row order
+      const float mu = stat[g][0][lc], var = stat[g][1][lc];
+      mean[(size_t)g * cols + c] = mu;
+      invstd[(size_t)g * cols + c] = rsqrtf(var + eps);
+      m = (1.f - momentum) * m + momentum * mu;
+      v = (1.f - momentum) * v + momentum * var * unb;
+    }
+    rm[c] = m;
+    rv[c] = v;
+  }
   if (!ok) return;
-  const float is = stat[1][lc], gm = gamma[c], bt = beta[c];
+  const float is0 = rsqrtf(stat[0][1][lc] + eps);
+  const float is1 = groups > 1 ? rsqrtf(stat[1][1][lc] + eps) : 0.f;
+  const float gm = gamma[c], bt = beta[c];
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * BN_GROUPS;
     if (r < rows) {
-      const float n = (x[i] - mu) * is;
+      const bool g1 = r >= rpg;
+      const float n = (x[i] - (g1 ? mu1 : mu0)) * (g1 ? is1 : is0);
       nhat[(size_t)r * ldn + c] = n;
       const float y = n * gm + bt;
       out[(size_t)r * ldo + c] = y > 0.f ? y : 0.f;
@@ -657,17 +679,17 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
 
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
-                          float momentum, float eps, hipStream_t stream) {
+                          int groups, float momentum, float eps, hipStream_t stream) {
   const dim3 grid((cols + BN_COLS - 1) / BN_COLS), block(BN_COLS * BN_GROUPS);
   if (rows <= 8 * BN_GROUPS)
     hipLaunchKernelGGL(bn_relu_train_kernel<8>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, momentum, eps);
+                       invstd, rm, rv, rows, cols, groups, momentum, eps);
   else if (rows <= 16 * BN_GROUPS)
     hipLaunchKernelGGL(bn_relu_train_kernel<16>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, momentum, eps);
+                       invstd, rm, rv, rows, cols, groups, momentum, eps);
   else
     hipLaunchKernelGGL(bn_relu_train_kernel<32>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, momentum, eps);
+                       invstd, rm, rv, rows, cols, groups, momentum, eps);
 }
 
 template <int MAXR>

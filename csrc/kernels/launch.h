@@ -62,7 +62,9 @@ struct SampleArgs {
   const float* data;        // encoded training matrix [n_rows, Dd]
   int* col;
   int* opt;
+  int n_real;               // rows [0, n_real) also draw a real row into xr (xr has n_real rows)
   float* step_bump;         // optimizer step counter bumped by this launch (nullable)
+  float* step_bump2;        // a second one (both phases of a step drawn by one launch; nullable)
   float* metrics;           // zeroed by this launch when zero_metrics
   int zero_metrics;
   uint64_t seed;
@@ -89,6 +91,7 @@ struct SlerpFuse {
   const float* real;   // [rows, ld] real rows
   float* out;          // [rows, ld] interpolates
   int ld, cols;        // cols = data_dim + n_opt (the fake row continues past the activation)
+  int rows;            // only activation rows r < rows are interpolated
   uint32_t stream;
 };
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
@@ -124,7 +127,7 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
-                          float momentum, float eps, hipStream_t stream);
+                          int groups, float momentum, float eps, hipStream_t stream);
 
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,

@@ -117,11 +117,11 @@ class MDGANRuntime(FedRuntime):
     def _client_step(self):
         eng, o, B = self.engine, self.engine.ops, self.engine.B
         # D step: local batch, remote generator, local D update
-        o.sample_train(eng.tables, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B], eng.Xd[B:2 * B], eng.Dd, eng.col,
+        o.sample_train(eng.tables, eng.H, eng.z_cols, eng.c_cols, eng.X_fake, eng.X_real, eng.Dd, eng.col,
                        eng.opt, step_counter=eng.stepD, metrics=eng.metrics, zero_metrics=True, stream_id=1)
         self.time_train_d.append(self._remote_logits())
-        o.activate(eng.logits, eng.Xd[0:B, :eng.Dd], eng.spans, eng.cfg.tau, stream_id=2)
-        o.slerp(eng.Xd[B:2 * B], eng.Xd[0:B], eng.Xd[2 * B:3 * B], stream_id=3)
+        o.activate(eng.logits, eng.X_fake[:, :eng.Dd], eng.spans, eng.cfg.tau, stream_id=2)
+        o.slerp(eng.X_real, eng.X_fake, eng.X_interp, stream_id=3)
         eng._d_update()
         # G step: feedback dL/dlogits for the server
         o.sample_train(eng.tables, eng.H, eng.z_cols, eng.c_cols, eng.Xg, None, eng.Dd, eng.col, eng.opt,

@@ -87,6 +87,7 @@ class EngineConfig:
     precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
     graph_unroll: int = 8       # GPU: training steps captured per hipGraph (fewer graph launches)
     streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
+    paired: bool = True         # draw + generate the D- and G-phase batches of a step in one pass
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -282,19 +283,35 @@ class CTGANEngine:
         dev, f32 = self.device, torch.float32
         B, nP = self.B, self.nP
         z = lambda *s: torch.zeros(*s, dtype=f32, device=dev)  # noqa: E731
-        self.H = _padded_rows(B, self.Hw, dev)
-        self.abuf = [z(B, g) for g in self.gdims]
-        self.nhat = [z(B, g) for g in self.gdims]
-        self.bn_mean = [z(g) for g in self.gdims]
-        self.bn_invstd = [z(g) for g in self.gdims]
+        # generator forward buffers hold two batches: rows [0, B) the D phase, [B, 2B) the G phase.
+        # The paired prepare runs both through ONE M = 2B GEMM chain (BN statistics per batch);
+        # the per-phase paths use the G-phase rows, which are also what the G backward reads.
+        self.H2 = _padded_rows(2 * B, self.Hw, dev)
+        self.abuf2 = [z(2 * B, g) for g in self.gdims]
+        self.nhat2 = [z(2 * B, g) for g in self.gdims]
+        self.bn_mean2 = [z(2, g) for g in self.gdims]
+        self.bn_invstd2 = [z(2, g) for g in self.gdims]
+        self.logits2 = _padded_rows(2 * B, self.Dd, dev)
+        self.H = self.H2[B:]
+        self.abuf = [t[B:] for t in self.abuf2]
+        self.nhat = [t[B:] for t in self.nhat2]
+        self.bn_mean = [t[1] for t in self.bn_mean2]
+        self.bn_invstd = [t[1] for t in self.bn_invstd2]
+        self.logits = self.logits2[B:]
         self.da = [z(B, g) for g in self.gdims]
-        self.logits = _padded_rows(B, self.Dd, dev)
         self.dlogits = _padded_rows(B, self.Dd, dev)
         self.dH = _padded_rows(B, self.Hw, dev)
-        self.Xd = z(3 * B, self.Din)
+        # discriminator inputs, one buffer: [interp | real | fake (D phase) | fake (G phase)].
+        # D's stacked batch is the first 3B rows; both phases' fake rows are contiguous, so one
+        # activation launch writes them; the G phase's rows are separate so its prepare can overlap
+        # the D update (lanes)
+        self.Xall = z(4 * B, self.Din)
+        self.X_interp = self.Xall[0:B]
+        self.X_real = self.Xall[B:2 * B]
+        self.X_fake = self.Xall[2 * B:3 * B]
+        self.Xd = self.Xall[0:3 * B]
         self.X = self.Xd.view(3 * nP, self.K1)
-        # the G phase's fake rows have their own buffer so its prepare can overlap the D update
-        self.Xg = z(B, self.Din)
+        self.Xg = self.Xall[3 * B:4 * B]
         self.XgP = self.Xg.view(nP, self.K1)
         self.dact = None
         self.dl = [z(3 * nP, h) for h in self.ddims]
@@ -303,11 +320,15 @@ class CTGANEngine:
         self.y = z(3 * nP)
         self.gbuf = z(nP, self.K1)
         inv = 1.0 / nP
-        self.coef3 = torch.cat([torch.full((nP,), inv), torch.full((nP,), -inv), torch.ones(nP)]).to(dev, f32)
-        self.wloss3 = torch.cat([torch.full((nP,), inv), torch.full((nP,), -inv), torch.zeros(nP)]).to(dev, f32)
+        # packed-row slices of the stacked D batch: interpolates, then real, then fake
+        self.rows_i, self.rows_fr = slice(0, nP), slice(nP, 3 * nP)
+        self.coef3 = torch.cat([torch.ones(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).to(dev, f32)
+        self.wloss3 = torch.cat([torch.zeros(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).to(dev, f32)
         self.coefg = torch.full((nP,), -inv, dtype=f32, device=dev)
-        self.col = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.opt = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.col2 = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+        self.opt2 = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+        self.col = self.col2[B:]
+        self.opt = self.opt2[B:]
         self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
 
     # ================================================================= data
@@ -378,18 +399,21 @@ class CTGANEngine:
             return _ext(x, kp), _ext(W, kp)
         return x, W
 
-    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None):
+    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None, paired=False):
         """Residual stack + output layer; with ``act_out`` the activation is fused onto the
-        output GEMM (tanh / Gumbel-softmax into act_out, Philox stream ``stream_id``)."""
+        output GEMM (tanh / Gumbel-softmax into act_out, Philox stream ``stream_id``).
+        paired: H / logits hold both batches of a step (2B rows, BN statistics per batch)."""
         o = self.ops
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
             x, W = self._kpad(H, a, self.p[f"G.{i}.W"])
+            abuf, nh = (self.abuf2[i], self.nhat2[i]) if paired else (self.abuf[i], self.nhat[i])
+            mean, istd = (self.bn_mean2[i], self.bn_invstd2[i]) if paired else (self.bn_mean[i], self.bn_invstd[i])
             o.linear_bn_relu(x, W, self.p[f"G.{i}.b"], self.p[f"G.{i}.gamma"],
                              self.p[f"G.{i}.beta"], H[:, b_:a],
-                             self.abuf[i] if nhat else None, self.nhat[i] if nhat else None,
-                             self.bn_mean[i], self.bn_invstd[i], self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
-                             training, self.cfg.bn_momentum, self.cfg.bn_eps)
+                             abuf if nhat else None, nh if nhat else None,
+                             mean, istd, self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
+                             training, self.cfg.bn_momentum, self.cfg.bn_eps, groups=2 if paired else 1)
         x, W = self._kpad(H, 0, self.p["G.out.W"])
         if act_out is None:
             o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
@@ -458,21 +482,36 @@ class CTGANEngine:
         self._d_update()
 
     def _d_prepare(self):
-        """Draw the batch and build the D input: [fake | real | slerp(real, fake)] rows."""
-        o, B = self.ops, self.B
-        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xd[0:B], self.Xd[B:2 * B], self.Dd,
+        """Draw the batch and build the D input: [slerp(real, fake) | real | fake] rows."""
+        o = self.ops
+        o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.X_fake, self.X_real, self.Dd,
                        self.col, self.opt, step_counter=self.stepD, metrics=self.metrics, zero_metrics=True,
                        stream_id=1)
         # activation of the fake rows + slerp(real, fake) for the gradient penalty in one launch
-        self._g_forward(self.H, self.logits, training=True, act_out=self.Xd[0:B, :self.Dd], stream_id=2,
-                        slerp=(self.Xd[B:2 * B], self.Xd[0:B], self.Xd[2 * B:3 * B], 3))
+        self._g_forward(self.H, self.logits, training=True, act_out=self.X_fake[:, :self.Dd], stream_id=2,
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3))
+
+    def _prepare_paired(self):
+        """Both phases' batches in one pass: one sampler launch draws the D-phase batch (with real
+        rows) and the G-phase batch, and the generator runs once on the 2B stacked rows.
+
+        Exact w.r.t. the reference's two separate forwards (`Client/.../distributed.py:185-265`):
+        the D step never changes G, BN uses per-batch statistics, and the running statistics are
+        updated D batch first, then G batch.  Halves the generator-side launches of a step and
+        doubles their workgroups (M = 1000 fills the chip better than M = 500)."""
+        o, B = self.ops, self.B
+        o.sample_train(self.tables, self.H2, self.z_cols, self.c_cols, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
+                       self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
+                       zero_metrics=True, stream_id=1)
+        self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True)
 
     def _d_update(self):
         """D forward on the stacked rows, WGAN + GP backward, D Adam step."""
         o, B, nP = self.ops, self.B, self.nP
         L = len(self.ddims)
         allr = slice(0, 3 * nP)
-        I = slice(2 * nP, 3 * nP)
+        I = self.rows_i
         self._d_forward(allr, stream_base=4, coef=self.coef3)
         self._a_chain(allr)
         # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
@@ -488,7 +527,7 @@ class CTGANEngine:
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I])
             inp = self.dl[i][I]
             prev = self.dl[i]
-        fr = slice(0, 2 * nP)
+        fr = self.rows_fr
         # bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN loss value, one launch.
         # (dl[L-1][I] holds R_{L-1} by now: coef = 1 there gives dpen/dv; wloss = 0 there.)
         src, out, w, dot = self._wgan_job(allr, self.wloss3, self.metrics[0:1])
@@ -594,7 +633,12 @@ class CTGANEngine:
     def _one_step(self):
         if hasattr(self.ops, "begin_step"):
             self.ops.begin_step(self)
-        if self.lanes is None:      # the reference order: D step, then G step
+        if self.lanes is None and self.cfg.paired:
+            # both batches drawn and generated up front (G is unchanged by the D update)
+            self._prepare_paired()
+            self._d_update()
+            self._g_update()
+        elif self.lanes is None:      # the reference order: D step, then G step
             self._d_step()
             self._g_step()
         else:

@@ -133,20 +133,24 @@ class HipOps:
                     float(bn_eps), self.f32, *(head or (None, None, None)), int(tile))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
-                       momentum=0.1, eps=1e-5):
+                       momentum=0.1, eps=1e-5, groups=1):
+        """groups = 2: the rows are two batches (BN statistics per batch, running stats updated
+        batch after batch); mean / invstd are then [2, cols]."""
         if training:
             # (fusing the split-K reduction into this BN launch was measured slower: the BN grid
             # has only cols/16 workgroups to pull the slabs -- profiles/README.md)
             self.gemm(x, W, abuf, tb=True, bias=b)
-            self.L.bn_relu_train(abuf, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps))
+            self.L.bn_relu_train(abuf, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps),
+                                 int(groups))
         else:
             self.gemm(x, W, out, tb=True, bias=b, epi=EPI_BN_EVAL_RELU, bn=(gamma, beta, rmean, rvar), bn_eps=eps)
 
     def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
-                    eps=1e-5):
+                    eps=1e-5, groups=1):
         if not training:
             raise NotImplementedError("eval-mode BN is fused into the GEMM epilogue on the HIP backend")
-        self.L.bn_relu_train(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps))
+        self.L.bn_relu_train(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps),
+                             int(groups))
 
     def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
         self.L.bn_relu_bwd(dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias)
@@ -154,20 +158,24 @@ class HipOps:
     # ------------------------------------------------------------------ samplers
     def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,
                      metrics=None, zero_metrics=False, stream_id=0):
+        """x_real may cover only the leading x_real.shape[0] rows of h / x_fake: those rows are the
+        D-phase batch, the rest a G-phase batch drawn by the same launch.  step_counter: a device
+        counter or a pair of them, bumped by the launch."""
         E = z_cols[1] - z_cols[0]
+        sc = step_counter if isinstance(step_counter, (tuple, list)) else (step_counter, None)
         if x_real is not None:
             self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, x_real, Dd, t["cdf_log"], t["cond_offset"],
                           t["cond_width"], t["row_offset"], t["row_count"], t["rows"], t["data"], col_out, opt_out,
-                          step_counter, metrics, bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
+                          sc[0], sc[1], metrics, bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
         else:
             self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, None, Dd, t["cdf_log"], t["cond_offset"],
-                          t["cond_width"], None, None, None, None, col_out, opt_out, step_counter, metrics,
+                          t["cond_width"], None, None, None, None, col_out, opt_out, sc[0], sc[1], metrics,
                           bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
 
     def sample_gen(self, t, h, c_cols, z_cols, col_out=None, opt_out=None, stream_id=0):
         E = z_cols[1] - z_cols[0]
         self.L.sample(h, z_cols[0], c_cols[0], E, None, None, 0, t["cdf_emp"], t["cond_offset"], t["cond_width"],
-                      None, None, None, None, col_out, opt_out, None, None, False, self.seed, self.ctr,
+                      None, None, None, None, col_out, opt_out, None, None, None, False, self.seed, self.ctr,
                       int(stream_id) * 16)
 
     # ------------------------------------------------------------------ activations

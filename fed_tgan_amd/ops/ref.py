@@ -62,7 +62,14 @@ class TorchOps:
         h[:, z_cols] <- N(0,1); h[:, c_cols] <- c1; x_fake[:, Dd:] <- c1; x_real <- [data[row], c1[perm]].
         t: dict of device tables (cdf_log, cond_offset, cond_width, row_offset, row_count, rows, data).
         (step_counter / metrics are bookkeeping of the HIP backend; eager Adam counts its own steps.)
+        When x_real covers only the leading rows, those rows are a D-phase batch and the rest a
+        G-phase batch (no real rows) drawn in the same call.
         """
+        if x_real is not None and x_real.shape[0] < h.shape[0]:
+            n = x_real.shape[0]
+            self.sample_train(t, h[:n], z_cols, c_cols, x_fake[:n], x_real, Dd, col_out[:n], opt_out[:n])
+            self.sample_train(t, h[n:], z_cols, c_cols, x_fake[n:], None, Dd, col_out[n:], opt_out[n:])
+            return
         dev = h.device
         B = h.shape[0]
         x_fake_c = x_fake[:, Dd:]
@@ -113,7 +120,17 @@ class TorchOps:
 
     # ------------------------------------------------------------------ batch norm + relu
     def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
-                    eps=1e-5):
+                    eps=1e-5, groups=1):
+        """groups > 1: the rows are that many consecutive batches, each normalised with its own
+        statistics; running statistics are updated batch after batch; mean / invstd [groups, cols]."""
+        if groups > 1:
+            n = a.shape[0] // groups
+            for g in range(groups):
+                r = slice(g * n, (g + 1) * n)
+                self.bn_relu_fwd(a[r], gamma, beta, out[r], None if nhat is None else nhat[r],
+                                 None if mean is None else mean[g], None if invstd is None else invstd[g],
+                                 rmean, rvar, training, momentum, eps)
+            return
         if training:
             mu = a.mean(0)
             var = a.var(0, unbiased=False)
@@ -132,10 +149,10 @@ class TorchOps:
         out.copy_(torch.relu(nh * gamma + beta))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
-                       momentum=0.1, eps=1e-5):
+                       momentum=0.1, eps=1e-5, groups=1):
         """out = relu(BN(x @ W^T + b)); training mode uses batch statistics and updates running ones."""
         a = torch.addmm(b, x, W.t())
-        self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps)
+        self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps, groups)
 
     def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
         dy = dr * (r > 0).to(dr.dtype)

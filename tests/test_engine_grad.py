@@ -78,14 +78,14 @@ def test_d_step_matches_autograd():
     eng._d_step()
     P = _d_params(eng, before)
     L = len(eng.ddims)
-    Xf = eng.Xd[0:B].reshape(nP, eng.K1).clone()
-    Xr = eng.Xd[B:2 * B].reshape(nP, eng.K1).clone()
+    Xf = eng.X_fake.reshape(nP, eng.K1).clone()
+    Xr = eng.X_real.reshape(nP, eng.K1).clone()
     Xi = eng.ops.rec["interp"].reshape(nP, eng.K1).clone().requires_grad_(True)
     Ws = [P[f"D.{i}.W"] for i in range(L)]
     bs = [P[f"D.{i}.b"] for i in range(L)]
-    mf = _masks(eng, slice(0, nP), P, Xf)
+    mf = _masks(eng, slice(2 * nP, 3 * nP), P, Xf)
     mr = _masks(eng, slice(nP, 2 * nP), P, Xr)
-    mi = _masks(eng, slice(2 * nP, 3 * nP), P, Xi.detach())
+    mi = _masks(eng, slice(0, nP), P, Xi.detach())
     yf = d_forward_masked(Xf, Ws, bs, mf, P["D.out.W"], P["D.out.b"])
     yr = d_forward_masked(Xr, Ws, bs, mr, P["D.out.W"], P["D.out.b"])
     yi = d_forward_masked(Xi, Ws, bs, mi, P["D.out.W"], P["D.out.b"])
@@ -180,14 +180,14 @@ def test_deeper_discriminator_gp():
     eng._d_step()
     P = _d_params(eng, before)
     L = len(eng.ddims)
-    Xf = eng.Xd[0:B].reshape(nP, eng.K1).clone()
-    Xr = eng.Xd[B:2 * B].reshape(nP, eng.K1).clone()
+    Xf = eng.X_fake.reshape(nP, eng.K1).clone()
+    Xr = eng.X_real.reshape(nP, eng.K1).clone()
     Xi = eng.ops.rec["interp"].reshape(nP, eng.K1).clone().requires_grad_(True)
     Ws = [P[f"D.{i}.W"] for i in range(L)]
     bs = [P[f"D.{i}.b"] for i in range(L)]
-    yf = d_forward_masked(Xf, Ws, bs, _masks(eng, slice(0, nP), P, Xf), P["D.out.W"], P["D.out.b"])
+    yf = d_forward_masked(Xf, Ws, bs, _masks(eng, slice(2 * nP, 3 * nP), P, Xf), P["D.out.W"], P["D.out.b"])
     yr = d_forward_masked(Xr, Ws, bs, _masks(eng, slice(nP, 2 * nP), P, Xr), P["D.out.W"], P["D.out.b"])
-    yi = d_forward_masked(Xi, Ws, bs, _masks(eng, slice(2 * nP, 3 * nP), P, Xi.detach()), P["D.out.W"],
+    yi = d_forward_masked(Xi, Ws, bs, _masks(eng, slice(0, nP), P, Xi.detach()), P["D.out.W"],
                           P["D.out.b"])
     g = torch.autograd.grad(yi.sum(), Xi, create_graph=True)[0]
     pen = ((g.norm(2, dim=1) - 1) ** 2).mean() * 10.0
@@ -217,3 +217,46 @@ def test_padded_storage_stays_zero():
             assert torch.count_nonzero(_ext(buf, _ceil4(buf.shape[1]))[:, buf.shape[1]:]) == 0
     x, W = eng._kpad(eng.H, 0, eng.p["G.out.W"])
     assert x.shape[1] % 4 == 0 and W.shape[1] == x.shape[1]
+
+
+def test_paired_prepare_equals_two_phase_forwards():
+    """The paired prepare (both phases' batches through one 2B-row generator pass) equals two
+    separate training-mode forwards: per-batch BN statistics, running stats updated D batch then
+    G batch, and the D input blocks / G-phase views it fills are the ones the updates read."""
+    eng, tr = _setup()
+    B = eng.B
+    ref = CTGANEngine(tr.layout, eng.cfg, "cpu", backend="torch")
+    ref.flat.copy_(eng.flat)
+    eng._prepare_paired()
+    a0 = eng.off[0]
+    for half in (slice(0, B), slice(B, 2 * B)):
+        ref.H[:, a0:].copy_(eng.H2[half, a0:])
+        ref._g_forward(ref.H, ref.logits, training=True)
+        assert torch.allclose(ref.logits, eng.logits2[half], rtol=1e-5, atol=1e-5)
+        for i in range(len(eng.gdims)):
+            assert torch.allclose(ref.nhat[i], eng.nhat2[i][half], rtol=1e-5, atol=1e-5)
+    # running statistics after both batches, in the reference's order (D batch first)
+    sA, sB = eng.group_range["S"]
+    assert torch.allclose(ref.flat[sA:sB], eng.flat[sA:sB], rtol=1e-6, atol=1e-6)
+    # G-phase views and the G-phase batch's BN statistics
+    for i in range(len(eng.gdims)):
+        assert eng.bn_invstd[i].data_ptr() == eng.bn_invstd2[i][1].data_ptr()
+        assert torch.allclose(ref.bn_invstd[i], eng.bn_invstd[i], rtol=1e-5)
+    assert eng.H.data_ptr() == eng.H2[B:].data_ptr()
+    # conditions: fake rows carry their batch's one-hot, real rows a permutation of the D batch's
+    c = eng.c_cols
+    assert torch.equal(eng.X_fake[:, eng.Dd:], eng.H2[:B, c[0]:c[1]])
+    assert torch.equal(eng.Xg[:, eng.Dd:], eng.H2[B:, c[0]:c[1]])
+    assert torch.equal(eng.X_real[:, eng.Dd:].sum(0), eng.X_fake[:, eng.Dd:].sum(0))
+    assert torch.equal(eng.col, eng.col2[B:])
+    assert torch.all(eng.X_interp.abs().sum(1) > 0)
+
+
+def test_paired_step_trains():
+    """A few paired steps run end to end and stay finite (both phases' metrics written)."""
+    eng, _ = _setup()
+    eng.ops = TorchOps()
+    for _ in range(3):
+        eng._one_step()
+    m = eng.metrics
+    assert bool(torch.isfinite(m).all()) and float(m[1]) > 0

@@ -47,3 +47,59 @@ def test_hip_step_matches_torch_step():
     eng_h._g_forward(eng_h.H, eng_h.logits, training=True)
     torch.cuda.synchronize()
     assert torch.allclose(eng_t.logits, eng_h.logits, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("batch", [100, 500])
+def test_hip_paired_forward_matches_torch(batch):
+    """The paired generator pass (2B rows, per-batch BN) on the HIP kernels equals the torch ops:
+    logits of both batches, per-batch normalised activations and statistics, running statistics."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    eng_t, tr = _engine("torch", batch=batch)
+    eng_h, _ = _engine("hip", batch=batch)
+    eng_h.flat.copy_(eng_t.flat)
+    x = torch.randn(2 * eng_t.B, eng_t.Hw, device="cuda:0")
+    x[batch:] = 0.5 * x[batch:] + 1.0       # the two batches have different statistics
+    eng_t.H2.copy_(x)
+    eng_h.H2.copy_(x)
+    eng_t._g_forward(eng_t.H2, eng_t.logits2, training=True, paired=True)
+    eng_h._g_forward(eng_h.H2, eng_h.logits2, training=True, paired=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(eng_t.logits2, eng_h.logits2, rtol=3e-2, atol=3e-2)
+    for i in range(len(eng_t.gdims)):
+        assert torch.allclose(eng_t.bn_mean2[i], eng_h.bn_mean2[i], rtol=1e-2, atol=1e-2)
+        assert torch.allclose(eng_t.bn_invstd2[i], eng_h.bn_invstd2[i], rtol=2e-2, atol=1e-3)
+        assert torch.allclose(eng_t.nhat2[i], eng_h.nhat2[i], rtol=3e-2, atol=3e-2)
+    sA, sB = eng_t.group_range["S"]
+    assert torch.allclose(eng_t.flat[sA:sB], eng_h.flat[sA:sB], rtol=1e-2, atol=1e-2)
+
+
+def test_hip_paired_prepare_fills_d_inputs():
+    """One paired sampler + generator launch sequence: conditions of both batches, real rows for
+    the D batch only, interpolates on the slerp arc, step counters of both optimizers bumped."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    eng, tr = _engine("hip", batch=500)
+    B, Dd = eng.B, eng.Dd
+    sd, sg = float(eng.stepD), float(eng.stepG)
+    eng._prepare_paired()
+    torch.cuda.synchronize()
+    assert float(eng.stepD) == sd + 1 and float(eng.stepG) == sg + 1
+    c = eng.c_cols
+    assert torch.equal(eng.X_fake[:, Dd:], eng.H2[:B, c[0]:c[1]])
+    assert torch.equal(eng.Xg[:, Dd:], eng.H2[B:, c[0]:c[1]])
+    assert torch.equal(eng.H2[:, c[0]:c[1]].sum(1), torch.ones(2 * B, device="cuda:0"))
+    assert torch.equal(eng.X_real[:, Dd:].sum(0), eng.X_fake[:, Dd:].sum(0))
+    # G-phase col/opt select the G batch's hot condition columns
+    offs = torch.as_tensor(tr.layout.cond_offset, device="cuda:0").long()
+    hot = offs[eng.col.long()] + eng.opt.long()
+    assert torch.equal(eng.H2[B:, c[0]:c[1]].argmax(1), hot)
+    # interpolates lie in span{real, fake} of their row (slerp weights), non-degenerate
+    r, f, i = (t.double() for t in (eng.X_real, eng.X_fake, eng.X_interp))
+    G = torch.stack([torch.stack([(r * r).sum(1), (r * f).sum(1)], 1),
+                     torch.stack([(r * f).sum(1), (f * f).sum(1)], 1)], 1)
+    rhs = torch.stack([(r * i).sum(1), (f * i).sum(1)], 1)
+    w = torch.linalg.solve(G + 1e-9 * torch.eye(2, dtype=G.dtype, device=G.device), rhs)
+    resid = (i - w[:, :1] * r - w[:, 1:] * f).norm(dim=1) / i.norm(dim=1).clamp_min(1e-12)
+    assert float(resid.max()) < 1e-3
+    assert bool(torch.isfinite(eng.Xall).all())

@@ -53,9 +53,9 @@ def test_hip_d_update_matches_autograd(precision):
     B, nP = eng.B, eng.nP
     eng._d_prepare()
     torch.cuda.synchronize()
-    Xf = eng.Xd[0:B].reshape(nP, eng.K1).clone()
-    Xr = eng.Xd[B:2 * B].reshape(nP, eng.K1).clone()
-    Xi0 = eng.Xd[2 * B:3 * B].reshape(nP, eng.K1).clone()
+    Xf = eng.X_fake.reshape(nP, eng.K1).clone()
+    Xr = eng.X_real.reshape(nP, eng.K1).clone()
+    Xi0 = eng.X_interp.reshape(nP, eng.K1).clone()
     P = {n: t.detach().clone() for n, t in eng.p.items() if n.startswith("D.")}
     eng._d_update()
     torch.cuda.synchronize()
@@ -64,9 +64,9 @@ def test_hip_d_update_matches_autograd(precision):
     Ws = [Q[f"D.{i}.W"] for i in range(L)]
     bs = [Q[f"D.{i}.b"] for i in range(L)]
     Xi = Xi0.clone().requires_grad_(True)
-    yf = d_forward_masked(Xf, Ws, bs, _masks(eng, slice(0, nP), P, Xf), Q["D.out.W"], Q["D.out.b"])
+    yf = d_forward_masked(Xf, Ws, bs, _masks(eng, slice(2 * nP, 3 * nP), P, Xf), Q["D.out.W"], Q["D.out.b"])
     yr = d_forward_masked(Xr, Ws, bs, _masks(eng, slice(nP, 2 * nP), P, Xr), Q["D.out.W"], Q["D.out.b"])
-    yi = d_forward_masked(Xi, Ws, bs, _masks(eng, slice(2 * nP, 3 * nP), P, Xi0), Q["D.out.W"], Q["D.out.b"])
+    yi = d_forward_masked(Xi, Ws, bs, _masks(eng, slice(0, nP), P, Xi0), Q["D.out.W"], Q["D.out.b"])
     g = torch.autograd.grad(yi.sum(), Xi, create_graph=True)[0]
     pen = ((g.norm(2, dim=1) - 1) ** 2).mean() * 10.0
     loss = yf.mean() - yr.mean()
@@ -137,7 +137,9 @@ def test_side_stream_overlap_is_race_free():
     out = []
     for streams in (False, True):
         torch.manual_seed(0)
-        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, streams=streams), DEV, backend="hip", seed=5)
+        # (both per-phase: the lanes path draws each phase's batch separately)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, streams=streams, paired=False), DEV, backend="hip",
+                          seed=5)
         eng.set_training_data(X)
         eng.train_steps(6, use_graph=True)
         torch.cuda.synchronize()

@@ -250,7 +250,7 @@ def test_sampler_statistics(hip):
     B, Dd, C = eng.B, eng.Dd, eng.C
     counts = np.zeros((tr.layout.n_col, eng.tables["cdf_log"].shape[1]))
     for it in range(40):
-        eng.ops.sample_train(eng.tables, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B], eng.Xd[B:2 * B], Dd, eng.col,
+        eng.ops.sample_train(eng.tables, eng.H, eng.z_cols, eng.c_cols, eng.X_fake, eng.X_real, Dd, eng.col,
                              eng.opt, stream_id=1)
         eng.ops.L.rng_bump(eng.ops.ctr)
         torch.cuda.synchronize()
@@ -258,12 +258,12 @@ def test_sampler_statistics(hip):
         np.add.at(counts, (col, opt), 1)
         c1 = eng.H[:, eng.c_cols[0]:eng.c_cols[1]]
         assert torch.equal(c1.sum(1), torch.ones(B, device=DEV))
-        assert torch.equal(eng.Xd[0:B, Dd:], c1)
+        assert torch.equal(eng.X_fake[:, Dd:], c1)
         # real rows carry the permuted condition and agree with it
-        c2 = eng.Xd[B:2 * B, Dd:]
+        c2 = eng.X_real[:, Dd:]
         assert torch.equal(c2.sum(0), c1.sum(0))
         hot = c2.argmax(1).cpu().numpy()
-        real = eng.Xd[B:2 * B, :Dd].cpu().numpy()
+        real = eng.X_real[:, :Dd].cpu().numpy()
         offs = tr.layout.cond_offset
         for b in range(0, B, 7):
             cc = np.searchsorted(offs, hot[b], side="right") - 1

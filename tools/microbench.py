@@ -62,6 +62,10 @@ def main():
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
     shapes = {
         "G0 fwd 500x256x(E+C) NT": (*eng._kpad(eng.H, eng.off[0], eng.p["G.0.W"]), eng.abuf[0], False, True),
+        "G0 fwd paired 1000x256x(E+C) NT": (*eng._kpad(eng.H2, eng.off[0], eng.p["G.0.W"]), eng.abuf2[0], False, True),
+        "G1 fwd paired 1000x256x(E+C+256) NT": (*eng._kpad(eng.H2, eng.off[1], eng.p["G.1.W"]), eng.abuf2[1], False,
+                                                 True),
+        "Gout fwd paired 1000xDdxHw NT": (*eng._kpad(eng.H2, 0, eng.p["G.out.W"]), eng.logits2, False, True),
         "G1 fwd 500x256x(E+C+256) NT": (*eng._kpad(eng.H, eng.off[1], eng.p["G.1.W"]), eng.abuf[1], False, True),
         "Gout fwd 500xDdxHw NT": (*eng._kpad(eng.H, 0, eng.p["G.out.W"]), eng.logits, False, True),
         "D0 fwd 150x256xK1 NT": (eng.X, eng.p["D.0.W"], eng.dl[0], False, True),
@@ -71,7 +75,7 @@ def main():
         "dV0 256xK1x150 TN": (eng.A[0], eng.X, eng.g["D.0.W"], True, False),
         "dWout DdxHwx500 TN": (eng.dlogits, *eng._kpad(eng.H, 0, eng.g["G.out.W"]), True, False),
         "dH 500x512xDd NN": (eng.dlogits, eng.p["G.out.W"][:, :eng.off[0]], eng.dH[:, :eng.off[0]], False, False),
-        "R0 50x256xK1 NT": (eng.X[2 * nP:], eng.p["D.0.W"], eng.dl[0][2 * nP:], False, True),
+        "R0 50x256xK1 NT": (eng.X[eng.rows_i], eng.p["D.0.W"], eng.dl[0][eng.rows_i], False, True),
         "dW1 256x(E+C+256)x500 TN": (eng.da[1], *eng._kpad(eng.H, eng.off[1], eng.g["G.1.W"]), True, False),
     }
     if args.split_sweep:
@@ -95,25 +99,36 @@ def main():
     for name, (a, b, c, ta, tb) in shapes.items():
         res[name] = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
     t = eng.tables
-    res["sample_train D"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B],
-                                                            eng.Xd[B:2 * B], eng.Dd, eng.col, eng.opt), dev)
-    res["sample_train G"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.Xd[0:B], None,
+    res["sample_train D"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.X_fake,
+                                                            eng.X_real, eng.Dd, eng.col, eng.opt), dev)
+    res["sample_train G"] = per_call(lambda: o.sample_train(t, eng.H, eng.z_cols, eng.c_cols, eng.Xg, None,
                                                             eng.Dd, eng.col, eng.opt), dev)
-    res["activate"] = per_call(lambda: o.activate(eng.logits, eng.Xd[0:B, :eng.Dd], eng.spans), dev)
-    res["act_bwd_ce"] = per_call(lambda: o.act_bwd_ce(eng.gbuf.view(B, eng.Din)[:, :eng.Dd], eng.Xd[0:B, :eng.Dd],
+    res["sample_train paired (D+G)"] = per_call(lambda: o.sample_train(t, eng.H2, eng.z_cols, eng.c_cols,
+                                                                        eng.Xall[2 * B:], eng.X_real, eng.Dd, eng.col2,
+                                                                        eng.opt2), dev)
+    res["activate"] = per_call(lambda: o.activate(eng.logits, eng.Xg[:, :eng.Dd], eng.spans), dev)
+    res["activate + slerp"] = per_call(lambda: o.activate(eng.logits, eng.X_fake[:, :eng.Dd], eng.spans,
+                                                          slerp=(eng.X_real, eng.X_fake, eng.X_interp, 3)), dev)
+    res["activate paired + slerp"] = per_call(lambda: o.activate(eng.logits2, eng.Xall[2 * B:, :eng.Dd], eng.spans,
+                                                                 slerp=(eng.X_real, eng.X_fake, eng.X_interp, 3)), dev)
+    res["act_bwd_ce"] = per_call(lambda: o.act_bwd_ce(eng.gbuf.view(B, eng.Din)[:, :eng.Dd], eng.Xg[:, :eng.Dd],
                                                       eng.logits, eng.spans, eng.cond_spans, eng.col, eng.opt,
                                                       eng.dlogits, eng.metrics[3:4]), dev)
     res["bn_relu_train"] = per_call(lambda: o.bn_relu_fwd(eng.abuf[0], eng.p["G.0.gamma"], eng.p["G.0.beta"],
                                                           eng.H[:, eng.off[1]:eng.off[0]], eng.nhat[0], eng.bn_mean[0],
                                                           eng.bn_invstd[0], eng.p["G.0.rm"], eng.p["G.0.rv"]), dev)
+    res["bn_relu_train paired"] = per_call(lambda: o.bn_relu_fwd(eng.abuf2[0], eng.p["G.0.gamma"], eng.p["G.0.beta"],
+                                                                 eng.H2[:, eng.off[1]:eng.off[0]], eng.nhat2[0],
+                                                                 eng.bn_mean2[0], eng.bn_invstd2[0], eng.p["G.0.rm"],
+                                                                 eng.p["G.0.rv"], groups=2), dev)
     res["adam D"] = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8, 0.0),
                              dev)
-    res["slerp"] = per_call(lambda: o.slerp(eng.Xd[B:2 * B], eng.Xd[0:B], eng.Xd[2 * B:3 * B]), dev)
-    res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[2 * nP:], 10.0, eng.metrics[1:2]), dev)
-    res["full step (graph, side lanes)"] = per_call(eng._one_step, dev, n=5, reps=20)
-    lanes, eng.lanes = eng.lanes, None
-    res["full step (graph, one stream)"] = per_call(eng._one_step, dev, n=5, reps=20)
-    eng.lanes = lanes
+    res["slerp"] = per_call(lambda: o.slerp(eng.X_real, eng.X_fake, eng.X_interp), dev)
+    res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[eng.rows_i], 10.0, eng.metrics[1:2]), dev)
+    eng.cfg.paired = False
+    res["full step (graph, per-phase prepare)"] = per_call(eng._one_step, dev, n=5, reps=20)
+    eng.cfg.paired = True
+    res["full step (graph, paired prepare)"] = per_call(eng._one_step, dev, n=5, reps=20)
     for k, v in res.items():
         print(f"{v:9.2f} us  {k}")
 
