@@ -479,6 +479,17 @@ void kmeans_step(const Tensor& x, const Tensor& n_rows, const Tensor& centers, c
 
 std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
+// kernel variant knobs for measured sweeps (tools/microbench.py); returns the previous value
+int64_t set_tuning(const std::string& key, int64_t value) {
+  if (key == "bn_cols") {
+    TORCH_CHECK(value == 4 || value == 8 || value == 16, "bn_cols must be 4, 8 or 16");
+    const int64_t prev = fedtgan::g_bn_cols;
+    fedtgan::g_bn_cols = (int)value;
+    return prev;
+  }
+  TORCH_CHECK(false, "unknown tuning key ", key);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(fedtgan, m) {
@@ -531,6 +542,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
       "int threads) -> ()");
   m.def("py_float(float x) -> str", &py_float);
+  m.def("set_tuning(str key, int value) -> int", &set_tuning);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {

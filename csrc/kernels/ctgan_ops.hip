@@ -586,10 +586,13 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
 }
 
 // ============================================================================ batch norm + relu
-// One workgroup owns BN_COLS columns; its BN_GROUPS row-groups keep up to MAXR rows per thread in
-// registers, so statistics, normalisation and the backward need a single pass over global memory.
+// One 512-thread workgroup owns COLS columns; its 512/COLS row-groups keep up to MAXR rows per
+// thread in registers, so statistics, normalisation and the backward need a single pass over
+// global memory.  Column reductions are wave64 butterflies (shfl_xor over the row-groups of a
+// wave) followed by one 8-entry LDS combine across the waves -- no serial LDS scans.
 // Loads use clamped (always valid) addresses and are masked afterwards (no predicated loads).
-constexpr int BN_COLS = 16, BN_GROUPS = 32;
+constexpr int BN_THREADS = 512, BN_WAVES = BN_THREADS / 64;
+int g_bn_cols = 8;    // columns per workgroup (tuning knob, see set_tuning)
 
 // ``groups`` (1 or 2) independent batches of rows/groups consecutive rows each: the D-phase and
 // G-phase batches of a step go through the generator as ONE M = 2B GEMM chain, but BatchNorm keeps
@@ -597,16 +600,38 @@ constexpr int BN_COLS = 16, BN_GROUPS = 32;
 // updated batch after batch, in row order -- exactly the reference's two forward passes.
 constexpr int BN_MAXG = 2;
 
-template <int MAXR>
-__global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
+// sum over every row-group of the workgroup for this thread's column; NV values at once.
+// sh: [NV][BN_WAVES][COLS] LDS; ends with a barrier so sh can be reused right away.
+template <int COLS, int NV>
+__device__ __forceinline__ void bn_colsum(float (&v)[NV], float* sh) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lc = threadIdx.x % COLS;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+#pragma unroll
+    for (int o = COLS; o < 64; o <<= 1) v[k] += __shfl_xor(v[k], o, 64);
+    if (lane < COLS) sh[(k * BN_WAVES + wv) * COLS + lc] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < BN_WAVES; ++w) t += sh[(k * BN_WAVES + w) * COLS + lc];
+    v[k] = t;
+  }
+  __syncthreads();
+}
+
+template <int COLS, int MAXR>
+__global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps) {
-  __shared__ float red[BN_MAXG][BN_GROUPS][BN_COLS + 1];
-  __shared__ float stat[BN_MAXG][2][BN_COLS];
-  const int lc = threadIdx.x % BN_COLS, grp = threadIdx.x / BN_COLS;
-  const int c = blockIdx.x * BN_COLS + lc;
+  constexpr int GROUPS = BN_THREADS / COLS;
+  __shared__ float sh[BN_MAXG * BN_WAVES * COLS];
+  const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
+  const int c = blockIdx.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   const int rpg = rows / groups;
@@ -614,59 +639,45 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
   float s[BN_MAXG] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * BN_GROUPS;
+    const int r = grp + i * GROUPS;
     const float v = a[(size_t)min(r, rows - 1) * lda + cc];
     x[i] = (r < rows) ? v : 0.f;
     if (r >= rpg) s[1] += x[i]; else s[0] += x[i];
   }
-#pragma unroll
-  for (int g = 0; g < BN_MAXG; ++g) red[g][grp][lc] = s[g];
-  __syncthreads();
-  if (grp < groups) {   // one row-group of threads per batch
-    float t = 0.f;
-    for (int i = 0; i < BN_GROUPS; ++i) t += red[grp][i][lc];
-    stat[grp][0][lc] = t / (float)rpg;
-  }
-  __syncthreads();
-  const float mu0 = stat[0][0][lc], mu1 = groups > 1 ? stat[1][0][lc] : 0.f;
+  bn_colsum<COLS, BN_MAXG>(s, sh);
+  const float mu0 = s[0] / (float)rpg, mu1 = s[1] / (float)rpg;
   float q[BN_MAXG] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * BN_GROUPS;
+    const int r = grp + i * GROUPS;
     const bool g1 = r >= rpg;
     const float d = (r < rows) ? x[i] - (g1 ? mu1 : mu0) : 0.f;
     if (g1) q[1] += d * d; else q[0] += d * d;
   }
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < BN_MAXG; ++g) red[g][grp][lc] = q[g];
-  __syncthreads();
-  if (grp < groups) {
-    float t = 0.f;
-    for (int i = 0; i < BN_GROUPS; ++i) t += red[grp][i][lc];
-    stat[grp][1][lc] = t / (float)rpg;    // biased batch variance
-  }
-  __syncthreads();
+  bn_colsum<COLS, BN_MAXG>(q, sh);
+  const float var0 = q[0] / (float)rpg, var1 = q[1] / (float)rpg;   // biased batch variances
+  const float is0 = rsqrtf(var0 + eps), is1 = rsqrtf(var1 + eps);
   if (grp == 0 && ok) {
-    float m = rm[c], v = rv[c];
     const float unb = (float)rpg / (float)max(rpg - 1, 1);
-    for (int g = 0; g < groups; ++g) {   // batch after batch, in row order
-      const float mu = stat[g][0][lc], var = stat[g][1][lc];
-      mean[(size_t)g * cols + c] = mu;
-      invstd[(size_t)g * cols + c] = rsqrtf(var + eps);
-      m = (1.f - momentum) * m + momentum * mu;
-      v = (1.f - momentum) * v + momentum * var * unb;
+    float m = rm[c], v = rv[c];
+    mean[c] = mu0;
+    invstd[c] = is0;
+    m = (1.f - momentum) * m + momentum * mu0;          // batch after batch, in row order
+    v = (1.f - momentum) * v + momentum * var0 * unb;
+    if (groups > 1) {
+      mean[(size_t)cols + c] = mu1;
+      invstd[(size_t)cols + c] = is1;
+      m = (1.f - momentum) * m + momentum * mu1;
+      v = (1.f - momentum) * v + momentum * var1 * unb;
     }
     rm[c] = m;
     rv[c] = v;
   }
   if (!ok) return;
-  const float is0 = rsqrtf(stat[0][1][lc] + eps);
-  const float is1 = groups > 1 ? rsqrtf(stat[1][1][lc] + eps) : 0.f;
   const float gm = gamma[c], bt = beta[c];
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * BN_GROUPS;
+    const int r = grp + i * GROUPS;
     if (r < rows) {
       const bool g1 = r >= rpg;
       const float n = (x[i] - (g1 ? mu1 : mu0)) * (g1 ? is1 : is0);
@@ -677,37 +688,53 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_train_kernel(
   }
 }
 
+template <int COLS>
+static void bn_train_cols(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
+                          float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
+                          int groups, float momentum, float eps, hipStream_t stream) {
+  constexpr int GROUPS = BN_THREADS / COLS;
+  const dim3 grid((cols + COLS - 1) / COLS), block(BN_THREADS);
+#define BN_TRAIN_LAUNCH(R)                                                                                          \
+  hipLaunchKernelGGL((bn_relu_train_kernel<COLS, R>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, \
+                     ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps)
+  if (rows <= 4 * GROUPS) BN_TRAIN_LAUNCH(4);
+  else if (rows <= 8 * GROUPS) BN_TRAIN_LAUNCH(8);
+  else if (rows <= 16 * GROUPS) BN_TRAIN_LAUNCH(16);
+  else if (rows <= 32 * GROUPS) BN_TRAIN_LAUNCH(32);
+  else BN_TRAIN_LAUNCH(64);
+#undef BN_TRAIN_LAUNCH
+}
+
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream) {
-  const dim3 grid((cols + BN_COLS - 1) / BN_COLS), block(BN_COLS * BN_GROUPS);
-  if (rows <= 8 * BN_GROUPS)
-    hipLaunchKernelGGL(bn_relu_train_kernel<8>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, groups, momentum, eps);
-  else if (rows <= 16 * BN_GROUPS)
-    hipLaunchKernelGGL(bn_relu_train_kernel<16>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, groups, momentum, eps);
+  if (g_bn_cols == 4)
+    bn_train_cols<4>(a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps,
+                     stream);
+  else if (g_bn_cols == 16)
+    bn_train_cols<16>(a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum,
+                      eps, stream);
   else
-    hipLaunchKernelGGL(bn_relu_train_kernel<32>, grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean,
-                       invstd, rm, rv, rows, cols, groups, momentum, eps);
+    bn_train_cols<8>(a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps,
+                     stream);
 }
 
-template <int MAXR>
-__global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
+template <int COLS, int MAXR>
+__global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols) {
-  __shared__ float red[2][BN_GROUPS][BN_COLS + 1];
-  __shared__ float stat[2][BN_COLS];
-  const int lc = threadIdx.x % BN_COLS, grp = threadIdx.x / BN_COLS;
-  const int c = blockIdx.x * BN_COLS + lc;
+  constexpr int GROUPS = BN_THREADS / COLS;
+  __shared__ float sh[2 * BN_WAVES * COLS];
+  const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
+  const int c = blockIdx.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   float dy[MAXR], nh[MAXR];
-  float s1 = 0.f, s2 = 0.f;
+  float st[2] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * BN_GROUPS;
+    const int r = grp + i * GROUPS;
     const size_t rr = (size_t)min(r, rows - 1);
     const float rv = r_[rr * ldr + cc];
     const float dv = dr[rr * lddr + cc];
@@ -717,58 +744,56 @@ __global__ __launch_bounds__(BN_COLS* BN_GROUPS) void bn_relu_bwd_kernel(
     const float n = in ? nv : 0.f;
     dy[i] = d;
     nh[i] = n;
-    s1 += d;
-    s2 += d * n;
+    st[0] += d;
+    st[1] += d * n;
   }
-  red[0][grp][lc] = s1;
-  red[1][grp][lc] = s2;
-  __syncthreads();
-  if (grp == 0) {
-    float t1 = 0.f, t2 = 0.f;
-    for (int i = 0; i < BN_GROUPS; ++i) { t1 += red[0][i][lc]; t2 += red[1][i][lc]; }
-    stat[0][lc] = t1;
-    stat[1][lc] = t2;
-    if (ok) { dbeta[c] = t1; dgamma[c] = t2; }
-  }
-  __syncthreads();
-  const float sdy = stat[0][lc], sdyn = stat[1][lc];
+  bn_colsum<COLS, 2>(st, sh);
+  const float sdy = st[0], sdyn = st[1];
+  if (grp == 0 && ok) { dbeta[c] = sdy; dgamma[c] = sdyn; }
   const float k = gamma[cc] * invstd[cc];
   const float invn = 1.f / (float)rows;
-  float sda = 0.f;
+  float sda[1] = {0.f};
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * BN_GROUPS;
+    const int r = grp + i * GROUPS;
     if (r < rows && ok) {
       const float v = k * (dy[i] - sdy * invn - nh[i] * sdyn * invn);
       da[(size_t)r * ldda + c] = v;
-      sda += v;
+      sda[0] += v;
     }
   }
   if (dbias) {
-    __syncthreads();
-    red[0][grp][lc] = sda;
-    __syncthreads();
-    if (grp == 0 && ok) {
-      float t = 0.f;
-      for (int i = 0; i < BN_GROUPS; ++i) t += red[0][i][lc];
-      dbias[c] = t;
-    }
+    bn_colsum<COLS, 1>(sda, sh);
+    if (grp == 0 && ok) dbias[c] = sda[0];
   }
+}
+
+template <int COLS>
+static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
+                        const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
+                        float* dbias, int rows, int cols, hipStream_t stream) {
+  constexpr int GROUPS = BN_THREADS / COLS;
+  const dim3 grid((cols + COLS - 1) / COLS), block(BN_THREADS);
+#define BN_BWD_LAUNCH(R)                                                                                          \
+  hipLaunchKernelGGL((bn_relu_bwd_kernel<COLS, R>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, \
+                     invstd, da, ldda, dgamma, dbeta, dbias, rows, cols)
+  if (rows <= 4 * GROUPS) BN_BWD_LAUNCH(4);
+  else if (rows <= 8 * GROUPS) BN_BWD_LAUNCH(8);
+  else if (rows <= 16 * GROUPS) BN_BWD_LAUNCH(16);
+  else if (rows <= 32 * GROUPS) BN_BWD_LAUNCH(32);
+  else BN_BWD_LAUNCH(64);
+#undef BN_BWD_LAUNCH
 }
 
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream) {
-  const dim3 grid((cols + BN_COLS - 1) / BN_COLS), block(BN_COLS * BN_GROUPS);
-  if (rows <= 8 * BN_GROUPS)
-    hipLaunchKernelGGL(bn_relu_bwd_kernel<8>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
-                       ldda, dgamma, dbeta, dbias, rows, cols);
-  else if (rows <= 16 * BN_GROUPS)
-    hipLaunchKernelGGL(bn_relu_bwd_kernel<16>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
-                       ldda, dgamma, dbeta, dbias, rows, cols);
+  if (g_bn_cols == 4)
+    bn_bwd_cols<4>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
+  else if (g_bn_cols == 16)
+    bn_bwd_cols<16>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
   else
-    hipLaunchKernelGGL(bn_relu_bwd_kernel<32>, grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da,
-                       ldda, dgamma, dbeta, dbias, rows, cols);
+    bn_bwd_cols<8>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
 }
 
 // ============================================================================ Adam

@@ -125,6 +125,7 @@ struct ColsumJob {
 };
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
+extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream);

@@ -121,6 +121,17 @@ def main():
                                                                  eng.H2[:, eng.off[1]:eng.off[0]], eng.nhat2[0],
                                                                  eng.bn_mean2[0], eng.bn_invstd2[0], eng.p["G.0.rm"],
                                                                  eng.p["G.0.rv"], groups=2), dev)
+    for bc in (4, 8, 16):
+        prev = torch.ops.fedtgan.set_tuning("bn_cols", bc)
+        res[f"bn_relu_train paired cols={bc}"] = per_call(
+            lambda: o.bn_relu_fwd(eng.abuf2[0], eng.p["G.0.gamma"], eng.p["G.0.beta"], eng.H2[:, eng.off[1]:eng.off[0]],
+                                  eng.nhat2[0], eng.bn_mean2[0], eng.bn_invstd2[0], eng.p["G.0.rm"], eng.p["G.0.rv"],
+                                  groups=2), dev)
+        res[f"bn_relu_bwd cols={bc}"] = per_call(
+            lambda: o.bn_relu_bwd(eng.dH[:, eng.off[1]:eng.off[0]], eng.H[:, eng.off[1]:eng.off[0]], eng.nhat[0],
+                                  eng.p["G.0.gamma"], eng.bn_invstd[0], eng.da[0], eng.g["G.0.gamma"],
+                                  eng.g["G.0.beta"], eng.g["G.0.b"]), dev)
+        torch.ops.fedtgan.set_tuning("bn_cols", prev)
     res["adam D"] = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8, 0.0),
                              dev)
     res["slerp"] = per_call(lambda: o.slerp(eng.X_real, eng.X_fake, eng.X_interp), dev)
