@@ -226,9 +226,12 @@ void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, con
   const int64_t rows = logits.size(0);
   TORCH_CHECK(dact.size(0) == rows && act.size(0) == rows && dlogits.size(0) == rows && col.numel() >= rows,
               "act_bwd_ce: rows");
+  // loss with one entry per row: per-row terms (summed later), else accumulated into loss[0]
+  const bool per_row = rows > 1 && loss.numel() == rows;
+  TORCH_CHECK(per_row || loss.numel() >= 1, "act_bwd_ce: loss");
   fedtgan::launch_act_bwd_ce(cfp(dact), ld_of(dact), cfp(act), ld_of(act), cfp(logits), ld_of(logits),
                              spans_of(start, width, kind, cidx, elem), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
-                             ld_of(dlogits), (int)rows, (float)tau, fp(loss), cur_stream());
+                             ld_of(dlogits), (int)rows, (float)tau, fp(loss), per_row ? 1 : 0, cur_stream());
 }
 
 void slerp(const Tensor& real, const Tensor& fake, const Tensor& out, int64_t seed, const Tensor& rng_ctr,
@@ -246,8 +249,9 @@ void gp_scale(const Tensor& g, const Tensor& out, double lam, const Tensor& loss
   check_f32_2d(g, "g");
   check_f32_2d(out, "out");
   TORCH_CHECK(g.sizes() == out.sizes(), "gp_scale: shapes");
+  const bool per_row = g.size(0) > 1 && loss.numel() == g.size(0);   // per-pack terms, summed later
   fedtgan::launch_gp_scale(cfp(g), ld_of(g), fp(out), ld_of(out), (int)g.size(0), (int)g.size(1), (float)lam,
-                           fp(loss), cur_stream());
+                           fp(loss), per_row ? 1 : 0, cur_stream());
 }
 
 void d_head(const Tensor& d, const Tensor& ms, const Tensor& v, const Tensor& e, const Tensor& coef,

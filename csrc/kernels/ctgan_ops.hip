@@ -25,32 +25,40 @@ namespace fedtgan {
 // ============================================================================ sampling
 // One wave per batch row.  The option of the sampled conditional column is found with a
 // lane-parallel inverse-CDF search (each lane tests one CDF entry, a ballot picks the first
-// hit) -- one memory round trip instead of a serial scan over the span.
+// hit) -- one memory round trip instead of a serial scan over the span.  A D-phase row needs two
+// such draws (its own condition and the one of the permuted fake row its real row serves); their
+// first CDF chunks are requested together, and the noise is generated while they are in flight.
 constexpr int SAMPLE_THREADS = 256;
-constexpr int SAMPLE_WAVES = SAMPLE_THREADS / 64;
-constexpr int SAMPLE_ROWS_PER_WAVE = 2;
-constexpr int SAMPLE_ROWS = SAMPLE_WAVES * SAMPLE_ROWS_PER_WAVE;   // rows per workgroup
-constexpr int MAX_PERM = 4096;
+constexpr int SAMPLE_ROWS = SAMPLE_THREADS / 64;   // rows per workgroup (one per wave)
 
-__device__ __forceinline__ void draw_cond_wave(const SampleArgs& a, uint64_t step, int b, int lane, int& col,
-                                               int& opt) {
+struct CondDraw {
+  int col, w;
+  float u;
+  const float* cdf;
+};
+
+__device__ __forceinline__ CondDraw cond_draw_begin(const SampleArgs& a, uint64_t step, int b) {
   RngArgs rng{a.seed, a.rng_ctr, a.rng_stream};
   const uint4 r = rng4(rng, step, (uint64_t)b);
-  col = min((int)(u01(r.x) * a.n_col), a.n_col - 1);
-  const float u = u01(r.y);
-  const float* cdf = a.cdf + (size_t)col * a.maxw;
-  const int w = a.cond_w[col];
-  int found = w - 1;
-  for (int base = 0; base < w; base += 64) {
+  CondDraw d;
+  d.col = min((int)(u01(r.x) * a.n_col), a.n_col - 1);
+  d.u = u01(r.y);
+  d.cdf = a.cdf + (size_t)d.col * a.maxw;
+  d.w = a.cond_w[d.col];
+  return d;
+}
+
+// first chunk already loaded (cv0 = cdf[lane]); rare wider spans continue chunk by chunk
+__device__ __forceinline__ int cond_draw_finish(const SampleArgs& a, const CondDraw& d, float cv0, int lane) {
+  unsigned long long hit = __ballot(lane < d.w && cv0 > d.u);
+  if (hit) return min(__ffsll((long long)hit) - 1, d.w - 1);
+  for (int base = 64; base < d.w; base += 64) {
     const int i = base + lane;
-    const float cv = cdf[min(i, a.maxw - 1)];
-    const unsigned long long hit = __ballot(i < w && cv > u);
-    if (hit) {
-      found = base + __ffsll((long long)hit) - 1;
-      break;
-    }
+    const float cv = d.cdf[min(i, a.maxw - 1)];
+    hit = __ballot(i < d.w && cv > d.u);
+    if (hit) return min(base + __ffsll((long long)hit) - 1, d.w - 1);
   }
-  opt = min(found, w - 1);
+  return d.w - 1;
 }
 
 // Keyed pseudo-random permutation of [0, n): a 4-round Feistel network on the smallest even
@@ -89,49 +97,65 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
       a.metrics[0] = 0.f; a.metrics[1] = 0.f; a.metrics[2] = 0.f; a.metrics[3] = 0.f;
     }
   }
+  const int b = blockIdx.x * SAMPLE_ROWS + wv;
+  if (b >= a.B) return;
   // rows [0, n_real) get a real row (the D phase); the rest only noise + condition (the G phase
   // of the same step when both batches are drawn by one launch)
   const int n_real = (a.xr != nullptr && a.n_col > 0) ? a.n_real : 0;
-  RngArgs rk{a.seed, a.rng_ctr, a.rng_stream + 1u};
-  const uint4 pkey = rng4(rk, step, 0ull);
-  RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
-  RngArgs rp{a.seed, a.rng_ctr, a.rng_stream + 3u};
-  for (int q = 0; q < SAMPLE_ROWS_PER_WAVE; ++q) {
-    const int b = blockIdx.x * SAMPLE_ROWS + wv * SAMPLE_ROWS_PER_WAVE + q;
-    if (b >= a.B) break;
-    int col = 0, opt = 0;
-    if (a.n_col > 0) draw_cond_wave(a, step, b, lane, col, opt);
-    const int hot = a.n_col > 0 ? a.cond_off[col] + opt : -1;
-    float* hrow = a.h + (size_t)b * a.ldh;
-    for (int i = lane; i < (a.E + 1) / 2; i += 64) {
-      const uint4 r = rng4(rz, step, (uint64_t)b * a.E + i);
-      const float2 z = box_muller(r.x, r.y);
-      hrow[a.zc + 2 * i] = z.x;
-      if (2 * i + 1 < a.E) hrow[a.zc + 2 * i + 1] = z.y;
+  const bool real = b < n_real;
+  // (1) both condition draws: RNG + column tables, then the first CDF chunk of each
+  CondDraw own{}, per{};
+  float cv_own = 0.f, cv_per = 0.f;
+  int p = 0;
+  if (a.n_col > 0) {
+    own = cond_draw_begin(a, step, b);
+    if (real) {
+      RngArgs rk{a.seed, a.rng_ctr, a.rng_stream + 1u};
+      p = (int)feistel_perm((uint32_t)b, (uint32_t)n_real, rng4(rk, step, 0ull));
+      per = cond_draw_begin(a, step, p);     // the condition of fake row perm[b]
     }
-    float* xf = a.xf ? a.xf + (size_t)b * a.ldx + a.Dd : nullptr;
-    for (int i = lane; i < a.C; i += 64) {
-      const float v = (i == hot) ? 1.f : 0.f;
-      hrow[a.cc + i] = v;
-      if (xf) xf[i] = v;
-    }
-    if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
-    if (b >= n_real) continue;
-    // real row drawn for the condition of fake row perm[b] (a permutation of the real-row block)
-    const int p = (int)feistel_perm((uint32_t)b, (uint32_t)n_real, pkey);
-    int pc = 0, po = 0;
-    draw_cond_wave(a, step, p, lane, pc, po);
-    const int64_t cnt = a.row_cnt[(size_t)pc * a.maxw + po];
-    const uint4 r4 = rng4(rp, step, (uint64_t)b);
-    int64_t pick = (int64_t)(u01d(r4.x, r4.y) * (double)(cnt > 0 ? cnt : 1));
-    if (pick >= cnt) pick = cnt > 0 ? cnt - 1 : 0;
-    const int64_t row = a.rows[a.row_off[(size_t)pc * a.maxw + po] + pick];
-    const float* src = a.data + (size_t)row * a.Dd;
-    float* dst = a.xr + (size_t)b * a.ldx;
-    for (int i = lane; i < a.Dd; i += 64) dst[i] = src[i];
-    const int phot = a.cond_off[pc] + po;
-    for (int i = lane; i < a.C; i += 64) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
+    cv_own = own.cdf[min(lane, a.maxw - 1)];
+    if (real) cv_per = per.cdf[min(lane, a.maxw - 1)];
   }
+  // (2) the noise while the CDF chunks are in flight
+  float* hrow = a.h + (size_t)b * a.ldh;
+  RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
+  for (int i = lane; i < (a.E + 1) / 2; i += 64) {
+    const uint4 r = rng4(rz, step, (uint64_t)b * a.E + i);
+    const float2 z = box_muller(r.x, r.y);
+    hrow[a.zc + 2 * i] = z.x;
+    if (2 * i + 1 < a.E) hrow[a.zc + 2 * i + 1] = z.y;
+  }
+  // (3) options, one-hot conditions
+  int col = 0, opt = 0;
+  if (a.n_col > 0) {
+    col = own.col;
+    opt = cond_draw_finish(a, own, cv_own, lane);
+  }
+  const int hot = a.n_col > 0 ? a.cond_off[col] + opt : -1;
+  float* xf = a.xf ? a.xf + (size_t)b * a.ldx + a.Dd : nullptr;
+  for (int i = lane; i < a.C; i += 64) {
+    const float v = (i == hot) ? 1.f : 0.f;
+    hrow[a.cc + i] = v;
+    if (xf) xf[i] = v;
+  }
+  if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
+  if (!real) return;
+  // (4) real row for the permuted condition: count -> CSR entry -> row copy
+  const int pc = per.col, po = cond_draw_finish(a, per, cv_per, lane);
+  const size_t cell = (size_t)pc * a.maxw + po;
+  const int64_t cnt = a.row_cnt[cell];
+  const int64_t off = a.row_off[cell];
+  RngArgs rp{a.seed, a.rng_ctr, a.rng_stream + 3u};
+  const uint4 r4 = rng4(rp, step, (uint64_t)b);
+  int64_t pick = (int64_t)(u01d(r4.x, r4.y) * (double)(cnt > 0 ? cnt : 1));
+  if (pick >= cnt) pick = cnt > 0 ? cnt - 1 : 0;
+  const int64_t row = a.rows[off + pick];
+  const float* src = a.data + (size_t)row * a.Dd;
+  float* dst = a.xr + (size_t)b * a.ldx;
+  const int phot = a.cond_off[pc] + po;
+  for (int i = lane; i < a.C; i += 64) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
+  for (int i = lane; i < a.Dd; i += 64) dst[i] = src[i];
 }
 
 void launch_sample(const SampleArgs& a, hipStream_t stream) {
@@ -165,26 +189,28 @@ constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image 
 constexpr int ACT_PF = 8;      // logits prefetched per lane (rows up to 512 wide)
 constexpr int ACT_PFS = 12;    // slerp real-row values prefetched per lane (rows up to 768 wide)
 constexpr size_t LDS_BYTES = 160 * 1024;
+constexpr int EI_SOFTMAX = 1 << 30;   // einfo bit: the element belongs to a softmax span
 
 struct ActSmem {
-  int* elem;    // [D]  element -> span
+  int* einfo;   // [D]  element -> span index | EI_SOFTMAX
   int* kind;    // [S]
   int* start;   // [S]
   int* width;   // [S]
   int* cidx;    // [S]
-  float* rows;  // [waves][D + 2S]
+  float* rows;  // [waves][D + 2S]: row image, then per-span statistics
 };
 
 __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float* smem) {
   const int D = sp.dim, S = sp.n_span;
   ActSmem t;
-  t.elem = reinterpret_cast<int*>(smem);
-  t.kind = t.elem + D;
+  t.einfo = reinterpret_cast<int*>(smem);
+  t.kind = t.einfo + D;
   t.start = t.kind + S;
   t.width = t.start + S;
   t.cidx = t.width + S;
   t.rows = reinterpret_cast<float*>(t.cidx + S);
-  for (int i = threadIdx.x; i < D; i += blockDim.x) t.elem[i] = sp.elem_span[i];
+  // (the host encodes the softmax bit into elem_span: no dependent table lookup here)
+  for (int i = threadIdx.x; i < D; i += blockDim.x) t.einfo[i] = sp.elem_span[i];
   for (int i = threadIdx.x; i < S; i += blockDim.x) {
     t.kind[i] = sp.kind[i];
     t.start[i] = sp.start[i];
@@ -195,6 +221,25 @@ __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float*
   return t;
 }
 
+// order-preserving float <-> uint map (for ds_max_u32 on floats); 0 is below every float
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Segmented softmax without serial per-span loops: every lane folds its own elements into the
+// span's LDS statistics with ds_max_u32 / ds_add_f32 (per-wave statistics block), so the cost
+// no longer scales with the widest span.  Gumbel noise: one Philox call feeds 4 elements of a
+// lane (index (row, k/4, lane)).
 __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* __restrict__ logits, int ldl,
                                                                   float* __restrict__ out, int ldo, int rows,
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
@@ -214,51 +259,62 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   for (int k = 0; k < ACT_PF; ++k) xr[k] = pre ? x[min(lane + 64 * k, D - 1)] : 0.f;
   const bool pre_s = sl.real != nullptr && sl.cols <= ACT_PFS * 64;
   const float* a_row = sl.real ? sl.real + (size_t)min(rc, sl.rows - 1) * sl.ld : nullptr;
-  float ar[ACT_PFS];
+  float ar[ACT_PFS], fc[ACT_PFS];
+  const float* f_row = out + (size_t)rc * ldo;   // the fake row's condition columns (j >= D) are in place
 #pragma unroll
-  for (int k = 0; k < ACT_PFS; ++k) ar[k] = pre_s ? a_row[min(lane + 64 * k, sl.cols - 1)] : 0.f;
+  for (int k = 0; k < ACT_PFS; ++k) {
+    const int j = min(lane + 64 * k, sl.cols - 1);
+    ar[k] = pre_s ? a_row[j] : 0.f;
+    fc[k] = (pre_s && sl.cols > D) ? f_row[max(j, D)] : 0.f;   // (j <= cols - 1 already)
+  }
   const ActSmem t = act_stage_tables(sp, act_smem);
   if (r >= rows) return;
   float* v = t.rows + (size_t)wv * (D + 2 * S);
-  float* stat = v + D;
+  uint32_t* smax = reinterpret_cast<uint32_t*>(v + D);
+  float* ssum = v + D + S;
   float* y = out + (size_t)r * ldo;
   const uint64_t step = ctr ? *ctr : 0ull;
   RngArgs rng{seed, ctr, stream_id};
   const uint64_t base = (uint64_t)r << 20;
-  auto act_elem = [&](int j, float xv) {
-    if (t.kind[t.elem[j]] == 0) {
+  for (int s2 = lane; s2 < S; s2 += 64) { smax[s2] = 0u; ssum[s2] = 0.f; }
+  wave_lds_sync();
+  uint4 u4 = make_uint4(0u, 0u, 0u, 0u);
+  auto act_elem = [&](int j, int k, float xv) {
+    if ((k & 3) == 0) u4 = rng4(rng, step, base + (uint64_t)(k >> 2) * 64u + (uint64_t)lane);
+    const uint32_t u = (k & 3) == 0 ? u4.x : (k & 3) == 1 ? u4.y : (k & 3) == 2 ? u4.z : u4.w;
+    const int info = t.einfo[j];
+    if (!(info & EI_SOFTMAX)) {
       const float th = tanhf(xv);
       y[j] = th;
       v[j] = th;    // (read back by the fused slerp; tanh elements have no softmax input)
     } else {
-      v[j] = (xv + gumbel(rng4(rng, step, base + j).x)) * inv_tau;
+      const float g = (xv + gumbel(u)) * inv_tau;
+      v[j] = g;
+      atomicMax(&smax[info & (EI_SOFTMAX - 1)], f2ord(g));
     }
   };
   if (pre) {
 #pragma unroll
     for (int k = 0; k < ACT_PF; ++k)
-      if (lane + 64 * k < D) act_elem(lane + 64 * k, xr[k]);
+      if (lane + 64 * k < D) act_elem(lane + 64 * k, k, xr[k]);
   } else {
-    for (int j = lane; j < D; j += 64) act_elem(j, x[j]);
+    for (int j = lane, k = 0; j < D; j += 64, ++k) act_elem(j, k, x[j]);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  for (int s = lane; s < S; s += 64) {
-    if (t.kind[s] == 0) continue;
-    const int st = t.start[s], w = t.width[s];
-    float m = -INFINITY;
-    for (int i = 0; i < w; ++i) m = fmaxf(m, v[st + i]);
-    float sum = 0.f;
-    for (int i = 0; i < w; ++i) sum += __expf(v[st + i] - m);
-    stat[2 * s] = m;
-    stat[2 * s + 1] = 1.f / sum;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   for (int j = lane; j < D; j += 64) {
-    const int s = t.elem[j];
-    if (t.kind[s] != 0) {
-      const float o = __expf(v[j] - stat[2 * s]) * stat[2 * s + 1];
+    const int info = t.einfo[j];
+    if (info & EI_SOFTMAX) {
+      const int s2 = info & (EI_SOFTMAX - 1);
+      const float e = __expf(v[j] - ord2f(smax[s2]));
+      v[j] = e;
+      atomicAdd(&ssum[s2], e);
+    }
+  }
+  wave_lds_sync();
+  for (int j = lane; j < D; j += 64) {
+    const int info = t.einfo[j];
+    if (info & EI_SOFTMAX) {
+      const float o = v[j] / ssum[info & (EI_SOFTMAX - 1)];
       y[j] = o;
       v[j] = o;     // each lane re-reads only its own elements below
     }
@@ -273,7 +329,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
     for (int k = 0; k < ACT_PFS; ++k) {
       const int j = lane + 64 * k;
       if (j < sl.cols) {
-        const float ra = ar[k], fb = j < D ? v[j] : y[j];
+        const float ra = ar[k], fb = j < D ? v[j] : fc[k];
         saa += ra * ra;
         sbb += fb * fb;
         sab += ra * fb;
@@ -299,7 +355,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
 #pragma unroll
     for (int k = 0; k < ACT_PFS; ++k) {
       const int j = lane + 64 * k;
-      if (j < sl.cols) o[j] = wa * ar[k] + wb * (j < D ? v[j] : y[j]);
+      if (j < sl.cols) o[j] = wa * ar[k] + wb * (j < D ? v[j] : fc[k]);
     }
   } else {
     for (int j = lane; j < sl.cols; j += 64) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
@@ -333,13 +389,15 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
   hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl);
 }
 
-// backward of the activation + fused conditional cross-entropy, one wave per row
+// backward of the activation + fused conditional cross-entropy, one wave per row; the per-span
+// sums of g*y are LDS ds_add_f32 folds (no serial per-span loops)
 __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float* __restrict__ dact, int ldd,
                                                                     const float* __restrict__ act, int lda,
                                                                     const float* __restrict__ logits, int ldl,
                                                                     SpanTables sp, const int* __restrict__ col,
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
-                                                                    int ldg, int rows, float inv_tau, float* loss) {
+                                                                    int ldg, int rows, float inv_tau, float* loss,
+                                                                    int loss_per_row) {
   extern __shared__ float act_smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
@@ -363,28 +421,29 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
   const int orow = opt[rc];
   const ActSmem t = act_stage_tables(sp, act_smem);
   if (r >= rows) return;
-  float* gy = t.rows + (size_t)wv * (D + 2 * S);
-  float* stat = gy + D;
+  float* xs = t.rows + (size_t)wv * (D + 2 * S);         // [D] the row's logits (for the CE's LSE)
+  float* stat = xs + D;                                  // [S] per-span sum of g*y
   float* d = dl + (size_t)r * ldg;
+  for (int s2 = lane; s2 < S; s2 += 64) stat[s2] = 0.f;
+  // the conditioned span of this row (exactly one lane finds it)
+  int ce_span = -1;
+  for (int s2 = lane; s2 < S; s2 += 64)
+    if (t.kind[s2] != 0 && t.cidx[s2] == cr) ce_span = s2;
+  wave_lds_sync();
+  auto fold = [&](int j, float gj, float yj, float xj) {
+    const int info = t.einfo[j];
+    xs[j] = xj;
+    if (info & EI_SOFTMAX) atomicAdd(&stat[info & (EI_SOFTMAX - 1)], gj * yj);
+  };
   if (pre) {
 #pragma unroll
     for (int k = 0; k < ACT_PF; ++k)
-      if (lane + 64 * k < D) gy[lane + 64 * k] = gr[k] * yr[k];
+      if (lane + 64 * k < D) fold(lane + 64 * k, gr[k], yr[k], xr[k]);
   } else {
-    for (int j = lane; j < D; j += 64) gy[j] = g[j] * y[j];
+    for (int j = lane; j < D; j += 64) fold(j, g[j], y[j], x[j]);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  int ce_span = -1;
-  for (int s = lane; s < S; s += 64) {
-    if (t.kind[s] == 0) continue;
-    const int st = t.start[s], w = t.width[s];
-    float dot = 0.f;
-    for (int i = 0; i < w; ++i) dot += gy[st + i];
-    stat[2 * s] = dot;
-    if (t.cidx[s] == cr) ce_span = s;
-  }
-  // the conditioned span of this row (exactly one lane found it): wave-parallel log-sum-exp
+  wave_lds_sync();
+  // wave-parallel log-sum-exp over the conditioned span
   const unsigned long long who = __ballot(ce_span >= 0);
   int cst = 0, cw = 0;
   float lse = 0.f;
@@ -394,26 +453,32 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
     cst = t.start[cs];
     cw = t.width[cs];
     float m = -INFINITY;
-    for (int i = lane; i < cw; i += 64) m = fmaxf(m, x[cst + i]);
+    for (int i = lane; i < cw; i += 64) m = fmaxf(m, xs[cst + i]);
     m = wave_max(m);
     float sm = 0.f;
-    for (int i = lane; i < cw; i += 64) sm += __expf(x[cst + i] - m);
+    for (int i = lane; i < cw; i += 64) sm += __expf(xs[cst + i] - m);
     sm = wave_sum(sm);
     lse = m + __logf(sm);
     const int o = min(orow, cw - 1);
-    if (lane == 0) atomicAdd(loss, (lse - x[cst + o]) / (float)rows);
+    if (lane == 0) {
+      const float term = (lse - xs[cst + o]) / (float)rows;
+      // per-row terms are summed by a later column-sum launch: hundreds of same-address device
+      // atomics serialise at the memory-side atomic unit
+      if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+    }
+  } else if (lane == 0 && loss_per_row) {
+    loss[r] = 0.f;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_sync();
   const int ot = cst + min(orow, max(cw - 1, 0));
   const float invB = 1.f / (float)rows;
   auto grad_elem = [&](int j, float gj, float yj, float xj) {
-    const int s = t.elem[j];
+    const int info = t.einfo[j];
     float v;
-    if (t.kind[s] == 0) {
+    if (!(info & EI_SOFTMAX)) {
       v = gj * (1.f - yj * yj);
     } else {
-      v = yj * (gj - stat[2 * s]) * inv_tau;
+      v = yj * (gj - stat[info & (EI_SOFTMAX - 1)]) * inv_tau;
       if (j >= cst && j < cst + cw) v += (__expf(xj - lse) - (j == ot ? 1.f : 0.f)) * invB;
     }
     d[j] = v;
@@ -429,13 +494,13 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
 
 void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, const float* logits, int ldl, SpanTables sp,
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
-                       hipStream_t stream) {
+                       int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(act_bwd_ce_kernel, lds);
   hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
-                     1.f / tau, loss);
+                     1.f / tau, loss, loss_per_row);
 }
 
 size_t activation_smem_bytes(const SpanTables& sp) { return act_smem_bytes(sp, act_waves(sp)); }
@@ -474,7 +539,8 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
 
 // one workgroup per packed row
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
-                                                       int ldo, int rows, int cols, float lam, float* loss) {
+                                                       int ldo, int rows, int cols, float lam, float* loss,
+                                                       int loss_per_row) {
   __shared__ float sh[8];
   const int r = blockIdx.x;
   const float* x = g + (size_t)r * ldg;
@@ -491,13 +557,17 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
   const float coef = lam * 2.f * (n - 1.f) / (fmaxf(n, 1e-30f) * (float)rows);
   float* o = out + (size_t)r * ldo;
   for (int i = threadIdx.x; i < cols; i += blockDim.x) o[i] = coef * x[i];
-  if (threadIdx.x == 0) atomicAdd(loss, lam * (n - 1.f) * (n - 1.f) / (float)rows);
+  if (threadIdx.x == 0) {
+    const float term = lam * (n - 1.f) * (n - 1.f) / (float)rows;
+    if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+  }
 }
 
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
-                     hipStream_t stream) {
+                     int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(gp_scale_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss);
+  hipLaunchKernelGGL(gp_scale_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                     loss_per_row);
 }
 
 // one wave per row: y = d.v + e ; a = coef * v * ms ; loss += wloss * y

@@ -99,13 +99,13 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
 
 void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, const float* logits, int ldl, SpanTables sp,
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
-                       hipStream_t stream);
+                       int loss_per_row, hipStream_t stream);
 
 void launch_slerp(const float* real, const float* fake, float* out, int rows, int cols, int ld, uint64_t seed,
                   const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
 
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
-                     hipStream_t stream);
+                     int loss_per_row, hipStream_t stream);
 
 void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const float* v, const float* e,
                    const float* coef, const float* wloss, float* y, float* a, int lda, int rows, int cols, float* loss,

@@ -330,6 +330,10 @@ class CTGANEngine:
         self.col = self.col2[B:]
         self.opt = self.opt2[B:]
         self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
+        # per-pack penalty / per-row cond-CE terms, summed into metrics by the column-sum launch that
+        # follows (no same-address atomics in the producing kernels)
+        self.pen_rows = z(nP)
+        self.ce_rows = z(B)
 
     # ================================================================= data
     def set_training_data(self, encoded, rows: RowIndex | None = None, cond: CondTables | None = None):
@@ -440,7 +444,8 @@ class CTGANEngine:
     def _g_loss_metric(self):
         """The G-phase WGAN value alone (split roles: the client has no generator backward)."""
         src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
-        self.ops.colsum_many([src], [out], weights=[w], dots=[dot])
+        self.ops.colsum_many([src, self.ce_rows.view(-1, 1)], [out, self.metrics[3:4]], weights=[w, None],
+                             dots=[dot, None])
 
     def _wgan_job(self, rows: slice, wloss, loss_out):
         """colsum job computing loss_out += sum_r wloss[r] (D(x_r) - ...) = sum_r wloss[r](d_r . v + e)."""
@@ -516,7 +521,7 @@ class CTGANEngine:
         self._a_chain(allr)
         # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
         o.gemm(self.A[0][I], self.p["D.0.W"], self.gbuf)
-        o.gp_scale(self.gbuf, self.X[I], self.cfg.gp_lambda, self.metrics[1:2])
+        o.gp_scale(self.gbuf, self.X[I], self.cfg.gp_lambda, self.pen_rows)
         # R-chain on the main lane; each layer's weight-gradient GEMM (one GEMM over the stacked
         # rows) starts on a side lane as soon as its right operand is complete
         inp = self.X[I]
@@ -531,9 +536,9 @@ class CTGANEngine:
         # bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN loss value, one launch.
         # (dl[L-1][I] holds R_{L-1} by now: coef = 1 there gives dpen/dv; wloss = 0 there.)
         src, out, w, dot = self._wgan_job(allr, self.wloss3, self.metrics[0:1])
-        o.colsum_many([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src],
-                      [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out],
-                      weights=[None] * L + [self.coef3, w], dots=[None] * (L + 1) + [dot])
+        o.colsum_many([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src, self.pen_rows.view(-1, 1)],
+                      [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out, self.metrics[1:2]],
+                      weights=[None] * L + [self.coef3, w, None], dots=[None] * (L + 1) + [dot, None])
         self._join(1, 2)
         # d(loss)/d(e_out) = sum of the +-1/n_packs seeds = 0 (stays zero from allocation)
         b1, b2 = self.cfg.betas
@@ -565,7 +570,7 @@ class CTGANEngine:
         o.gemm(self.A[0][fk], self.p["D.0.W"], self.gbuf)            # d(-mean D)/dX, packed
         dx = self.gbuf.view(B, self.Din)
         o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
-                     self.opt, self.dlogits, self.metrics[3:4], self.cfg.tau)
+                     self.opt, self.dlogits, self.ce_rows, self.cfg.tau)
 
     def _g_backward(self):
         """self.dlogits -> G parameter gradients (self.gradG), through the saved forward buffers."""
@@ -575,9 +580,10 @@ class CTGANEngine:
         with self._lane(1):
             x, dW = self._kpad(self.H, 0, self.g["G.out.W"])
             o.gemm(self.dlogits, x, dW, ta=True)
-            # G.out bias grad + the G-phase WGAN value (-mean D(fake)) in one launch
+            # G.out bias grad + the G-phase WGAN value (-mean D(fake)) + the cond CE sum in one launch
             src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
-            o.colsum_many([self.dlogits, src], [self.g["G.out.b"], out], weights=[None, w], dots=[None, dot])
+            o.colsum_many([self.dlogits, src, self.ce_rows.view(-1, 1)], [self.g["G.out.b"], out, self.metrics[3:4]],
+                          weights=[None, w, None], dots=[None, dot, None])
         top = self.off[0]
         if Lg:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])

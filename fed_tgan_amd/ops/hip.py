@@ -103,9 +103,9 @@ class HipOps:
                     ci += 1
                 else:
                     cidx.append(-1)
-            elem = []
+            elem = []      # data column -> span index, | 1 << 30 for softmax spans (kernel-side einfo)
             for i, (s, w, k) in enumerate(spans):
-                elem.extend([i] * w)
+                elem.extend([i | ((1 << 30) if k != 0 else 0)] * w)
             mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
             t = (mk([s for s, _, _ in spans]), mk([w for _, w, _ in spans]), mk([k for _, _, k in spans]), mk(cidx),
                  mk(elem))

@@ -185,7 +185,8 @@ class TorchOps:
                 out[:, s:s + w].copy_(torch.softmax((x + g) / tau, dim=1))
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):
-        """dlogits = d(act)/d(logits)^T dact + d(cond_loss)/d(logits); loss_out[0] <- cond_loss."""
+        """dlogits = d(act)/d(logits)^T dact + d(cond_loss)/d(logits); loss_out[0] <- cond_loss, or, when
+        loss_out has one entry per row, the per-row terms (their sum is cond_loss)."""
         for s, w, k in spans:
             g = dact[:, s:s + w]
             y = act[:, s:s + w]
@@ -194,7 +195,8 @@ class TorchOps:
             else:
                 dlogits[:, s:s + w].copy_(y * (g - (g * y).sum(1, keepdim=True)) / tau)
         B = logits.shape[0]
-        loss = torch.zeros((), device=logits.device, dtype=logits.dtype)
+        per_row = B > 1 and loss_out.numel() == B
+        loss = torch.zeros(B if per_row else (), device=logits.device, dtype=logits.dtype)
         colL = col.long()
         optL = opt.long()
         for c, (s, w) in enumerate(cond_spans):
@@ -202,11 +204,15 @@ class TorchOps:
             x = logits[:, s:s + w]
             tgt = torch.clamp(optL, max=w - 1).view(-1, 1)
             lse = torch.logsumexp(x, dim=1)
-            loss = loss + (sel * (lse - x.gather(1, tgt).view(-1))).sum()
+            term = sel * (lse - x.gather(1, tgt).view(-1))
+            loss = loss + (term if per_row else term.sum())
             sm = torch.softmax(x, dim=1)
             sm = sm - torch.zeros_like(sm).scatter_(1, tgt, 1.0)
             dlogits[:, s:s + w] += sm * (sel / B).view(-1, 1)
-        loss_out[0] = loss / B
+        if per_row:
+            loss_out.copy_(loss / B)
+        else:
+            loss_out[0] = loss / B
 
     # ------------------------------------------------------------------ gradient penalty pieces
     def slerp(self, real, fake, out, stream_id=0):
@@ -224,7 +230,10 @@ class TorchOps:
     def gp_scale(self, g, out, lam, loss_out):
         n = g.norm(dim=1, keepdim=True)
         P = g.shape[0]
-        loss_out[0] = lam * ((n - 1) ** 2).mean()
+        if P > 1 and loss_out.numel() == P:       # per-pack terms (summed by a later column sum)
+            loss_out.copy_(lam * ((n.view(-1) - 1) ** 2) / P)
+        else:
+            loss_out[0] = lam * ((n - 1) ** 2).mean()
         out.copy_(g * (lam * 2.0 * (n - 1) / (n.clamp_min(1e-30) * P)))
 
     # ------------------------------------------------------------------ discriminator head

@@ -113,7 +113,7 @@ def main():
                                                                  slerp=(eng.X_real, eng.X_fake, eng.X_interp, 3)), dev)
     res["act_bwd_ce"] = per_call(lambda: o.act_bwd_ce(eng.gbuf.view(B, eng.Din)[:, :eng.Dd], eng.Xg[:, :eng.Dd],
                                                       eng.logits, eng.spans, eng.cond_spans, eng.col, eng.opt,
-                                                      eng.dlogits, eng.metrics[3:4]), dev)
+                                                      eng.dlogits, eng.ce_rows), dev)
     res["bn_relu_train"] = per_call(lambda: o.bn_relu_fwd(eng.abuf[0], eng.p["G.0.gamma"], eng.p["G.0.beta"],
                                                           eng.H[:, eng.off[1]:eng.off[0]], eng.nhat[0], eng.bn_mean[0],
                                                           eng.bn_invstd[0], eng.p["G.0.rm"], eng.p["G.0.rv"]), dev)
@@ -135,7 +135,7 @@ def main():
     res["adam D"] = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8, 0.0),
                              dev)
     res["slerp"] = per_call(lambda: o.slerp(eng.X_real, eng.X_fake, eng.X_interp), dev)
-    res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[eng.rows_i], 10.0, eng.metrics[1:2]), dev)
+    res["gp_scale"] = per_call(lambda: o.gp_scale(eng.gbuf, eng.X[eng.rows_i], 10.0, eng.pen_rows), dev)
     eng.cfg.paired = False
     res["full step (graph, per-phase prepare)"] = per_call(eng._one_step, dev, n=5, reps=20)
     eng.cfg.paired = True
