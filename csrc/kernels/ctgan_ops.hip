@@ -537,7 +537,44 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
                      ctr, stream_id);
 }
 
-// one workgroup per packed row
+// one workgroup per packed row.  The vector variant keeps the whole row in registers (up to
+// GP_V4 float4 per thread, loaded in one burst), so the row is read once: norm, then scale.
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+constexpr int GP_V4 = 8;    // rows up to 8 * 256 * 4 = 8192 wide stay in registers
+
+__device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, float* loss, int loss_per_row,
+                                          float* sh, float& coef) {
+  s = block_sum(s, sh);
+  const float n = sqrtf(s);
+  coef = lam * 2.f * (n - 1.f) / (fmaxf(n, 1e-30f) * (float)rows);
+  if (threadIdx.x == 0) {
+    const float term = lam * (n - 1.f) * (n - 1.f) / (float)rows;
+    if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+  }
+}
+
+__global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
+                                                          int ldo, int rows, int cols, float lam, float* loss,
+                                                          int loss_per_row) {
+  __shared__ float sh[8];
+  const int r = blockIdx.x;
+  const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
+  const int n4 = cols / 4;
+  f32x4 v[GP_V4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i) v[i] = x[min((int)threadIdx.x + 256 * i, n4 - 1)];
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i)
+    if ((int)threadIdx.x + 256 * i < n4) s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+  float coef;
+  gp_finish(r, s, rows, lam, loss, loss_per_row, sh, coef);
+  f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)r * ldo);
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i)
+    if ((int)threadIdx.x + 256 * i < n4) o[threadIdx.x + 256 * i] = v[i] * coef;
+}
+
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                        int ldo, int rows, int cols, float lam, float* loss,
                                                        int loss_per_row) {
@@ -552,22 +589,23 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
     s1 += w * w;
   }
   if (i < cols) s0 += x[i] * x[i];
-  const float s = block_sum(s0 + s1, sh);
-  const float n = sqrtf(s);
-  const float coef = lam * 2.f * (n - 1.f) / (fmaxf(n, 1e-30f) * (float)rows);
+  float coef;
+  gp_finish(r, s0 + s1, rows, lam, loss, loss_per_row, sh, coef);
   float* o = out + (size_t)r * ldo;
   for (int i = threadIdx.x; i < cols; i += blockDim.x) o[i] = coef * x[i];
-  if (threadIdx.x == 0) {
-    const float term = lam * (n - 1.f) * (n - 1.f) / (float)rows;
-    if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
-  }
 }
 
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
                      int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(gp_scale_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
-                     loss_per_row);
+  const bool v4 = cols % 4 == 0 && ldg % 4 == 0 && ldo % 4 == 0 && cols <= GP_V4 * 256 * 4 &&
+                  reinterpret_cast<uintptr_t>(g) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (v4)
+    hipLaunchKernelGGL(gp_scale_v4_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                       loss_per_row);
+  else
+    hipLaunchKernelGGL(gp_scale_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                       loss_per_row);
 }
 
 // one wave per row: y = d.v + e ; a = coef * v * ms ; loss += wloss * y

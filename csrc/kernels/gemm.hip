@@ -320,23 +320,25 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
       }
 }
 
+// Every slab load of an output element is issued before the first is consumed (SMAX >= splits
+// clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
+constexpr int GEMM_MAX_SPLITS = 64;
+
+template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
   const int splits = g.splitk;
   const size_t total = (size_t)g.M * g.N;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(idx / g.N), n = (int)(idx % g.N);
-    // independent partial sums so the slab loads are in flight together
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int z = 0;
-    for (; z + 4 <= splits; z += 4) {
-      s0 += g.ws[(size_t)z * total + idx];
-      s1 += g.ws[(size_t)(z + 1) * total + idx];
-      s2 += g.ws[(size_t)(z + 2) * total + idx];
-      s3 += g.ws[(size_t)(z + 3) * total + idx];
-    }
-    for (; z < splits; ++z) s0 += g.ws[(size_t)z * total + idx];
-    float v = g.alpha * ((s0 + s1) + (s2 + s3));
+    float part[SMAX];
+#pragma unroll
+    for (int z = 0; z < SMAX; ++z) part[z] = g.ws[(size_t)min(z, splits - 1) * total + idx];
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int z = 0; z < SMAX; ++z)
+      if (z < splits) acc[z & 3] += part[z];
+    float v = g.alpha * ((acc[0] + acc[1]) + (acc[2] + acc[3]));
     float* cp = g.c + (size_t)m * g.ldc + n;
     if (g.beta != 0.f) v += g.beta * (*cp);
     if (g.bias) v += g.bias[n];
@@ -352,6 +354,7 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   const int T = g.tile == 32 ? 32 : 64;   // square output tile
   const int tm = (g.M + T - 1) / T, tn = (g.N + T - 1) / T;
   if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
+  g.splitk = std::min(g.splitk, GEMM_MAX_SPLITS);   // the epilogue holds every slab value in registers
   int kchunk = (std::max(g.K, 1) + g.splitk - 1) / g.splitk;
   kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
   g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
@@ -386,7 +389,10 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   if (grid.z > 1) {
     const size_t total = (size_t)g.M * g.N;
     int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
-    hipLaunchKernelGGL(gemm_splitk_epilogue, dim3(blocks), dim3(256), 0, stream, g);
+    if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, dim3(blocks), dim3(256), 0, stream, g);
+    else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, dim3(blocks), dim3(256), 0, stream, g);
+    else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, dim3(blocks), dim3(256), 0, stream, g);
+    else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, dim3(blocks), dim3(256), 0, stream, g);
   }
 }
 

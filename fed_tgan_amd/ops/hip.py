@@ -50,8 +50,13 @@ def _splitk(M: int, N: int, K: int, kc: int = 128) -> int:
     return _plan(M, N, K, kc)[1]
 
 
+GEMM_MAX_SPLITS = 64   # gemm.hip: the split-K epilogue keeps every slab value in registers
+
+
 def _effective_splits(K: int, sk: int, kc: int) -> int:
-    """The split count launch_gemm actually runs: K slices are rounded up to whole bursts."""
+    """The split count launch_gemm actually runs: at most GEMM_MAX_SPLITS, K slices rounded up to
+    whole bursts."""
+    sk = min(sk, GEMM_MAX_SPLITS)
     if sk <= 1:
         return 1
     kchunk = -(-max(K, 1) // sk)

@@ -417,3 +417,34 @@ def test_gemm_padded_views_use_vector_loads(hip, ta, tb, M, N, K):
         assert torch.isfinite(c).all()
         assert (c - A @ B).abs().max().item() <= 1e-4 * math.sqrt(K) * 10 + 1e-5
     hip.tile_override = None
+
+
+@pytest.mark.parametrize("cols", [6260, 6259, 40])
+def test_gp_scale_per_row_terms(hip, cols):
+    """Vector (16-B, register-resident) and scalar variants; per-pack loss terms sum to the penalty."""
+    g = mat(50, cols, seed=30) * 0.02
+    o1, o2 = torch.zeros_like(g), torch.zeros_like(g)
+    rows1 = torch.zeros(50, device=DEV)
+    l2 = torch.zeros(1, device=DEV)
+    hip.gp_scale(g, o1, 10.0, rows1)
+    REF.gp_scale(g, o2, 10.0, l2)
+    torch.cuda.synchronize()
+    assert torch.allclose(o1, o2, atol=1e-6, rtol=1e-4)
+    assert torch.allclose(rows1.sum(), l2[0], rtol=1e-4)
+
+
+@pytest.mark.parametrize("splits", [2, 5, 8, 13, 16, 25, 40, 64, 100])
+def test_gemm_split_counts(hip, splits):
+    """Every split-K epilogue variant (register-held slabs: <= 8 / 16 / 32 / 64 splits; requests
+    above 64 are capped) reduces all slabs and applies the epilogue."""
+    a, b = mat(50, 9000, seed=40) * 0.1, mat(256, 9000, seed=41) * 0.1
+    bias = mat(256, seed=42)
+    c = torch.zeros(50, 256, device=DEV)
+    hip.split_override = splits
+    try:
+        hip.gemm(a, b, c, tb=True, bias=bias, epi=3)    # EPI_RELU
+    finally:
+        hip.split_override = None
+    torch.cuda.synchronize()
+    ref = torch.relu(a.double() @ b.double().t() + bias.double()).float()
+    assert ((c - ref).norm() / ref.norm()).item() < 1e-2
