@@ -84,7 +84,8 @@ class ThreadComm(Comm):
     def heartbeat(self, timeout_s: float):
         self.g.wait()
 
-    def gather_rows(self, t, counts, ranks, dst: int = 0):
+    def gather_rows(self, t, counts, ranks, dst: int = 0, to_host: bool = True):
+        # (threads share host memory: the rows always come back as host tensors)
         parts = self.all_gather_object(t.cpu())
         if self.rank != dst:
             return None

@@ -84,6 +84,7 @@ class EngineConfig:
     bn_momentum: float = 0.1
     bn_eps: float = 1e-5
     gen_chunk: int = 8192
+    gen_graph: bool = True      # GPU: replay the generation pass (per sample count) as one hipGraph
     precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
     graph_unroll: int = 8       # GPU: training steps captured per hipGraph (fewer graph launches)
     streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
@@ -144,6 +145,7 @@ class CTGANEngine:
         self.tables: Dict[str, torch.Tensor] = {}
         self.gen_tables = None
         self._gen_bufs = None
+        self._gen_graphs: Dict[int, tuple] = {}   # n -> (hipGraph, H, logits, out) of generate_decoded
         self.graphs: Dict[int, object] = {}    # steps per graph -> captured hipGraph
         self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
@@ -392,6 +394,7 @@ class CTGANEngine:
         self.gen_tables = {"cols": cols, "mu": torch.as_tensor(mu, dtype=torch.float64, device=dev),
                            "sd": torch.as_tensor(sd, dtype=torch.float64, device=dev)}
         self._gen_bufs = None
+        self._gen_graphs = {}
 
     # ================================================================= forward pieces
     def _kpad(self, H, a: int, W: torch.Tensor):
@@ -733,18 +736,51 @@ class CTGANEngine:
         return out
 
     @torch.no_grad()
-    def generate_decoded(self, n: int) -> torch.Tensor:
-        """Fused sample -> G(eval) -> Gumbel-argmax/tanh decode: [n, n_cols] float64 on device."""
+    def generate_decoded(self, n: int, use_graph: bool | None = None) -> torch.Tensor:
+        """Fused sample -> G(eval) -> Gumbel-argmax/tanh decode: [n, n_cols] float64 on device.
+
+        On a GPU the whole pass for a given n (every chunk's sampler, eval-BN GEMMs and decode
+        launches) is captured once into a hipGraph and replayed each round; the result is a fresh
+        tensor (a device copy of the graph's static output)."""
         if self.gen_tables is None:
             raise RuntimeError("set_generation_tables() first")
+        if use_graph is None:
+            use_graph = self.device.type == "cuda" and self.cfg.gen_graph and self.ops.name == "hip"
+        if use_graph:
+            ent = self._gen_graphs.get(n) or self._capture_gen(n)
+            ent[0].replay()
+            return ent[3].clone()
         out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
+        self._gen_pass(n, out, self._gen_buffers)
+        return out
+
+    def _gen_pass(self, n: int, out: torch.Tensor, bufs):
         for a in range(0, n, self.cfg.gen_chunk):
             b = min(n, a + self.cfg.gen_chunk)
-            H, logits = self._gen_buffers(b - a)
+            H, logits = bufs(b - a)
             self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, stream_id=21)
             self._g_forward(H, logits, training=False, nhat=False)
             self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23)
-        return out
+
+    def _capture_gen(self, n: int):
+        """Capture generate_decoded(n) with its own static buffers (graphs hold no tensor refs)."""
+        from ..utils.devsync import CAPTURE_LOCK
+        m = min(n, self.cfg.gen_chunk)
+        H, lg = _padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device)
+        out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
+        bufs = lambda k: (H[:k], lg[:k])  # noqa: E731
+        with CAPTURE_LOCK:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):      # warm-up (decode tables, lazy init); advances the RNG once
+                self._gen_pass(n, out, bufs)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
+                self._gen_pass(n, out, bufs)
+        self._gen_graphs[n] = (g, H, lg, out)
+        return self._gen_graphs[n]
 
     def _gen_buffers(self, n: int):
         if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n:

@@ -141,14 +141,16 @@ class Comm:
         return out
 
     # ------------------------------------------------------------------ data plane
-    def gather_rows(self, t: torch.Tensor, counts: Sequence[int], ranks: Sequence[int], dst: int = 0):
+    def gather_rows(self, t: torch.Tensor, counts: Sequence[int], ranks: Sequence[int], dst: int = 0,
+                    to_host: bool = True):
         """Row-concatenate the [counts[i], C] tensors of ``ranks`` (in order) on ``dst``.
 
         With an RCCL data plane the device tensors move GPU to GPU over xGMI (padded to the
-        largest share, one ``gather``) and ``dst`` copies the result to the host once; the
-        gloo path gathers host tensors.  Returns the host tensor on ``dst``, None elsewhere."""
+        largest share, one ``gather``) and ``dst`` copies the result to the host once (or, with
+        ``to_host=False``, keeps it on the device for an asynchronous copy); the gloo path gathers
+        host tensors.  Returns the tensor on ``dst``, None elsewhere."""
         if self.world_size == 1:
-            return t.cpu()
+            return t.cpu() if to_host else t
         nccl = self.data_backend == "nccl"
         width = t.shape[1]
         m = max(counts)
@@ -161,7 +163,8 @@ class Comm:
             return None
         order = dist.get_process_group_ranks(group) if group is not dist.group.WORLD else list(range(self.world_size))
         parts = {r: g for r, g in zip(order, gl)}
-        return torch.cat([parts[r][:n] for r, n in zip(ranks, counts)]).cpu()
+        out = torch.cat([parts[r][:n] for r, n in zip(ranks, counts)])
+        return out.cpu() if to_host else out
 
     def weighted_all_reduce(self, flat: torch.Tensor, weight: float) -> torch.Tensor:
         """flat <- sum_i w_i * flat_i over the data group (in place).

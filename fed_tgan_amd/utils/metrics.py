@@ -2,7 +2,7 @@
 
 The reference keeps ad-hoc wall timers per round (`Server/dtds/distributed.py:790-829`) and
 only writes the accumulated round time.  ``PhaseTimer`` records train / aggregate /
-sample+dump phases (device-synchronised when a GPU is used) and ``MetricsLog`` appends one
+sample+dump phases (synchronised with the compute stream when a GPU is used) and ``MetricsLog`` appends one
 JSON object per round (losses, weights, phase times) for observability.
 """
 from __future__ import annotations
@@ -13,7 +13,7 @@ import time
 from typing import Dict
 
 import torch
-from .devsync import device_sync
+from .devsync import stream_sync
 
 
 class PhaseTimer:
@@ -25,13 +25,13 @@ class PhaseTimer:
     @contextlib.contextmanager
     def phase(self, name: str, device=None):
         if self.sync and device is not None and getattr(device, "type", "") == "cuda":
-            device_sync(device)
+            stream_sync(device)
         t = time.perf_counter()
         try:
             yield
         finally:
             if self.sync and device is not None and getattr(device, "type", "") == "cuda":
-                device_sync(device)
+                stream_sync(device)
             dt = time.perf_counter() - t
             self.totals[name] = self.totals.get(name, 0.0) + dt
             self._last[name] = dt

@@ -42,11 +42,52 @@ def step_only(eng, dev):
         print(f"full step: side lanes {a:8.2f} us   one stream {b:8.2f} us")
 
 
+def gen_only(eng, tr, X, dev):
+    """generate_decoded(40000): eager vs hipGraph, chunk 8192 vs one chunk (wall time per call)."""
+    from fed_tgan_amd.models.samplers import CondTables
+    eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+    for chunk in (8192, 40000):
+        eng.cfg.gen_chunk = chunk
+        eng._gen_bufs, eng._gen_graphs = None, {}
+        for graph in (False, True):
+            eng.generate_decoded(40000, use_graph=graph)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for _ in range(10):
+                v = eng.generate_decoded(40000, use_graph=graph)
+            torch.cuda.synchronize(dev)
+            us = (time.perf_counter() - t) / 10 * 1e6
+            t = time.perf_counter()
+            for _ in range(10):
+                h = v.cpu()
+            d2h = (time.perf_counter() - t) / 10 * 1e6
+            print(f"generate_decoded(40000) chunk={chunk:6d} graph={graph!s:5}: {us:9.1f} us   "
+                  f"(D2H pageable copy {d2h:8.1f} us)", flush=True)
+
+
+def unroll_sweep(eng, dev):
+    """Wall time of one 80-step local epoch for several steps-per-graph settings."""
+    for U in (1, 2, 4, 8, 16, 40, 80):
+        eng.cfg.graph_unroll = U
+        eng.graphs = {}
+        eng.train_steps(80)
+        torch.cuda.synchronize(dev)
+        best = 1e9
+        for _ in range(5):
+            t = time.perf_counter()
+            eng.train_steps(80)
+            torch.cuda.synchronize(dev)
+            best = min(best, time.perf_counter() - t)
+        print(f"graph_unroll={U:3d}: epoch of 80 steps {best * 1e3:8.3f} ms  ({best / 80 * 1e6:7.1f} us/step)", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
     ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
+    ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
+    ap.add_argument("--unroll", action="store_true", help="epoch time vs training steps captured per graph")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -59,6 +100,10 @@ def main():
     res = {}
     if args.step_only:
         return step_only(eng, dev)
+    if args.gen:
+        return gen_only(eng, tr, X, dev)
+    if args.unroll:
+        return unroll_sweep(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
     shapes = {
         "G0 fwd 500x256x(E+C) NT": (*eng._kpad(eng.H, eng.off[0], eng.p["G.0.W"]), eng.abuf[0], False, True),
