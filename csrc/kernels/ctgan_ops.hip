@@ -298,7 +298,16 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
     for (int k = 0; k < ACT_PF; ++k)
       if (lane + 64 * k < D) act_elem(lane + 64 * k, k, xr[k]);
   } else {
-    for (int j = lane, k = 0; j < D; j += 64, ++k) act_elem(j, k, x[j]);
+    // wide rows: chunks of ACT_PF * 64 columns, each chunk's loads issued together (a plain
+    // strided loop waits one memory round trip per 64 columns)
+    for (int c0 = 0; c0 < D; c0 += ACT_PF * 64) {
+      float xc[ACT_PF];
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k) xc[k] = x[min(c0 + lane + 64 * k, D - 1)];
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k)
+        if (c0 + lane + 64 * k < D) act_elem(c0 + lane + 64 * k, (c0 >> 6) + k, xc[k]);
+    }
   }
   wave_lds_sync();
   for (int j = lane; j < D; j += 64) {
@@ -440,7 +449,19 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
     for (int k = 0; k < ACT_PF; ++k)
       if (lane + 64 * k < D) fold(lane + 64 * k, gr[k], yr[k], xr[k]);
   } else {
-    for (int j = lane; j < D; j += 64) fold(j, g[j], y[j], x[j]);
+    for (int c0 = 0; c0 < D; c0 += ACT_PF * 64) {   // chunked: one round trip per 512 columns
+      float gc[ACT_PF], yc[ACT_PF], xc[ACT_PF];
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k) {
+        const int j = min(c0 + lane + 64 * k, D - 1);
+        gc[k] = g[j];
+        yc[k] = y[j];
+        xc[k] = x[j];
+      }
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k)
+        if (c0 + lane + 64 * k < D) fold(c0 + lane + 64 * k, gc[k], yc[k], xc[k]);
+    }
   }
   wave_lds_sync();
   // wave-parallel log-sum-exp over the conditioned span
@@ -488,7 +509,20 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
     for (int k = 0; k < ACT_PF; ++k)
       if (lane + 64 * k < D) grad_elem(lane + 64 * k, gr[k], yr[k], xr[k]);
   } else {
-    for (int j = lane; j < D; j += 64) grad_elem(j, g[j], y[j], x[j]);
+    for (int c0 = 0; c0 < D; c0 += ACT_PF * 64) {
+      float gc[ACT_PF], yc[ACT_PF];
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k) {
+        const int j = min(c0 + lane + 64 * k, D - 1);
+        gc[k] = g[j];
+        yc[k] = y[j];
+      }
+#pragma unroll
+      for (int k = 0; k < ACT_PF; ++k) {
+        const int j = c0 + lane + 64 * k;
+        if (j < D) grad_elem(j, gc[k], yc[k], xs[j]);    // logits from the LDS copy
+      }
+    }
   }
 }
 
@@ -595,12 +629,48 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
   for (int i = threadIdx.x; i < cols; i += blockDim.x) o[i] = coef * x[i];
 }
 
+// rows wider than the register-resident variant: two passes over the row in chunks of
+// GP_V4 float4 per thread, each chunk's loads issued together
+__global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __restrict__ g, int ldg,
+                                                               float* __restrict__ out, int ldo, int rows, int cols,
+                                                               float lam, float* loss, int loss_per_row) {
+  __shared__ float sh[8];
+  const int r = blockIdx.x;
+  const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
+  const int n4 = cols / 4;
+  float s = 0.f;
+  for (int c0 = 0; c0 < n4; c0 += GP_V4 * 256) {
+    f32x4 v[GP_V4];
+#pragma unroll
+    for (int i = 0; i < GP_V4; ++i) v[i] = x[min(c0 + (int)threadIdx.x + 256 * i, n4 - 1)];
+#pragma unroll
+    for (int i = 0; i < GP_V4; ++i)
+      if (c0 + (int)threadIdx.x + 256 * i < n4)
+        s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+  }
+  float coef;
+  gp_finish(r, s, rows, lam, loss, loss_per_row, sh, coef);
+  f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)r * ldo);
+  for (int c0 = 0; c0 < n4; c0 += GP_V4 * 256) {
+    f32x4 v[GP_V4];
+#pragma unroll
+    for (int i = 0; i < GP_V4; ++i) v[i] = x[min(c0 + (int)threadIdx.x + 256 * i, n4 - 1)];
+#pragma unroll
+    for (int i = 0; i < GP_V4; ++i)
+      if (c0 + (int)threadIdx.x + 256 * i < n4) o[c0 + threadIdx.x + 256 * i] = v[i] * coef;
+  }
+}
+
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
                      int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
-  const bool v4 = cols % 4 == 0 && ldg % 4 == 0 && ldo % 4 == 0 && cols <= GP_V4 * 256 * 4 &&
-                  reinterpret_cast<uintptr_t>(g) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
-  if (v4)
+  const bool al = cols % 4 == 0 && ldg % 4 == 0 && ldo % 4 == 0 && reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  const bool v4 = al && cols <= GP_V4 * 256 * 4;
+  if (al && !v4)
+    hipLaunchKernelGGL(gp_scale_v4_wide_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam,
+                       loss, loss_per_row);
+  else if (v4)
     hipLaunchKernelGGL(gp_scale_v4_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row);
   else
@@ -947,7 +1017,9 @@ __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, c
 void launch_adam(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
                  float b2, float eps, float wd, uint64_t* rng_ctr_bump, hipStream_t stream) {
   const int64_t n4 = n / 4;
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 1024);
+  // one float4 per thread where possible: a grid-stride loop over few workgroups keeps too few
+  // loads in flight for HBM (19.5M-parameter wide-table D: 259 us at 1024 workgroups)
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 65535);
   hipLaunchKernelGGL(adam_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
                      reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
                      step, n4, lr, b1, b2, eps, wd, rng_ctr_bump);
