@@ -102,7 +102,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.rng_ctr = ctr_ptr(rng_ctr);
   g.rng_stream = (uint32_t)stream;
   g.f32 = f32 ? 1 : 0;
-  TORCH_CHECK(tile == 32 || tile == 64, "gemm: tile must be 32 or 64");
+  TORCH_CHECK(tile == 32 || tile == 64 || tile == 128, "gemm: tile must be 32, 64 or 128");
   g.vec = (vec_ok(a) && vec_ok(b)) ? 1 : 0;
   g.tile = (int)tile;
   if (head_a.has_value() && head_a->defined()) {

@@ -203,13 +203,17 @@ struct Cfg {
   // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
   // with 135 KB of LDS raised the per-workgroup rate of long-K GEMMs by 1.36x but cost more on
   // the short-K ones -- padding waste and one workgroup per CU -- so the step got slower.)
-  static constexpr int KC = F32 ? 64 : 128;
+  // (128x128 tiles halve the burst: two operands x 128 rows x 128 fp32 in flight would not fit
+  // the 256 architectural VGPRs next to the fragments and spill)
+  static constexpr int KC = (F32 ? 64 : 128) / (TM >= 128 ? 2 : 1);
   static constexpr int LD = F32 ? KC + 1 : KC + 8;            // LDS row stride (elements)
   static constexpr int ESZ = F32 ? 4 : 2;
   static constexpr int STAGE = (TM + TN) * LD * ESZ;          // bytes per stage (A image + B image)
 };
 
-// TM x TN output tile (64x64, or 32x32 for short-K GEMMs that would otherwise need split-K):
+// TM x TN output tile (64x64; 32x32 for short-K GEMMs that would otherwise need split-K; 128x128
+// for large-M x N GEMMs -- generation at M = 40k, wide tables -- where the operand re-reads of
+// small tiles make the GEMM L2-bandwidth-bound):
 // 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
 template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
@@ -298,6 +302,38 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   }
 
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  if constexpr (TM >= 128) {
+    // 64 accumulators per lane: a fully unrolled epilogue (Philox, loads, stores per element) is
+    // past the unroller's budget and the accumulator array would land in scratch, so the tile goes
+    // through LDS (the stage buffers are free now) and is written out row-contiguously
+    static_assert((size_t)TM * (TN + 1) * 4 <= 2 * C::STAGE, "epilogue tile must fit the stage buffers");
+    __syncthreads();
+    float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * (TN + 1) + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    for (int e = threadIdx.x; e < TM * TN; e += NT) {
+      const int ml = e / TN, nl = e - ml * TN;
+      const int m = m0 + ml, n = n0 + nl;
+      if (m >= g.M || n >= g.N) continue;
+      const float v0 = cs[ml * (TN + 1) + nl];
+      if (gridDim.z > 1) {
+        g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = v0;
+        continue;
+      }
+      float v = g.alpha * v0;
+      float* cp = g.c + (size_t)m * g.ldc + n;
+      if (g.beta != 0.f) v += g.beta * (*cp);
+      if (g.bias) v += g.bias[n];
+      *cp = apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -351,7 +387,7 @@ int gemm_kc(int f32) { return f32 ? Cfg<true, 64, 64>::KC : Cfg<false, 64, 64>::
 void launch_gemm(GemmArgs g, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0) return;
   const int KC = gemm_kc(g.f32);
-  const int T = g.tile == 32 ? 32 : 64;   // square output tile
+  const int T = g.tile == 32 ? 32 : (g.tile == 128 ? 128 : 64);   // square output tile
   const int tm = (g.M + T - 1) / T, tn = (g.N + T - 1) / T;
   if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
   g.splitk = std::min(g.splitk, GEMM_MAX_SPLITS);   // the epilogue holds every slab value in registers
@@ -369,6 +405,8 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
 #define FEDTGAN_GEMM_TILES(F, V)       \
   if (T == 32) {                       \
     FEDTGAN_GEMM_LAYOUTS(F, V, 32)     \
+  } else if (T == 128) {               \
+    FEDTGAN_GEMM_LAYOUTS(F, V, 128)    \
   } else {                             \
     FEDTGAN_GEMM_LAYOUTS(F, V, 64)     \
   }

@@ -28,15 +28,20 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
 
     Measured on MI355X (profiles/gemm_split_sweep_r1.txt): a split costs an epilogue launch
     (~4.6 us) and 64x64 tiles leave most CUs idle on these skinny shapes, so
+      * >= 256 128x128 tiles (generation at M = 40k, wide tables): 128x128, no split -- small
+        tiles re-read the fp32 operands from L2 so often that the GEMM becomes L2-bound;
       * >= 256 64x64 tiles: 64x64, no split (the grid already covers the chip);
       * short K (<= 8 bursts): 32x32 tiles, no split (4x the workgroups, no epilogue) --
         e.g. 500x256x432: 5.5 us vs 7.7 us for 64x64 split 4;
       * long K: 32x32 tiles split ~512 workgroups deep (one CU pulls only ~60-100 GB/s), at
         most 2 bursts per split, fp32 slabs capped at ~6 MB.
     """
+    t128 = -(-M // 128) * -(-N // 128)
     t64 = -(-M // 64) * -(-N // 64)
     t32 = -(-M // 32) * -(-N // 32)
     bursts = -(-K // kc)
+    if t128 >= 256 and K >= 256:
+        return 128, 1
     if t64 >= 256:
         return 64, 1
     if bursts <= 8:

@@ -37,7 +37,7 @@ def hip32():
     return HipOps(DEV, seed=1234, precision="fp32")
 
 
-@pytest.mark.parametrize("tile", [64, 32])
+@pytest.mark.parametrize("tile", [128, 64, 32])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(150, 256, 6240), (50, 6240, 256), (500, 323, 941), (7, 5, 3), (256, 430, 500),
                                    (500, 256, 432)])
