@@ -480,7 +480,9 @@ class FedRuntime:
         e = self.engine
         state = {"epoch": epoch, "flat": e.flat.cpu(), "mG": e.mG.cpu(), "vG": e.vG.cpu(), "mD": e.mD.cpu(),
                  "vD": e.vD.cpu(), "stepG": e.stepG.cpu(), "stepD": e.stepD.cpu(), "bn_batches": e.bn_batches,
-                 "round_times": list(self.round_times)}
+                 "round_times": list(self.round_times), "cpu_rng": torch.get_rng_state()}
+        if hasattr(e.ops, "ctr"):          # HIP backend: the device Philox step counter
+            state["rng_ctr"] = e.ops.ctr.cpu()
         torch.save(state, self._ckpt_path())
 
     def load_checkpoint(self):
@@ -492,6 +494,10 @@ class FedRuntime:
         for k in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
             getattr(e, k).copy_(st[k])
         e.bn_batches = int(st["bn_batches"])
+        if "cpu_rng" in st:
+            torch.set_rng_state(st["cpu_rng"])
+        if "rng_ctr" in st and hasattr(e.ops, "ctr"):
+            e.ops.ctr.copy_(st["rng_ctr"])
         self.start_epoch = int(st["epoch"])
         self.round_times = list(st["round_times"])
         self._epoch_done = self.start_epoch
