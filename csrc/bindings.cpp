@@ -491,6 +491,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_bn_cols = (int)value;
     return prev;
   }
+  if (key == "gemm_xcd_remap") {
+    const int64_t prev = fedtgan::g_gemm_xcd_remap;
+    TORCH_CHECK(value >= 0 && value <= 2, "gemm_xcd_remap: 0 off, 1 long-K tiles, 2 always");
+    fedtgan::g_gemm_xcd_remap = (int)value;
+    return prev;
+  }
   TORCH_CHECK(false, "unknown tuning key ", key);
 }
 

@@ -222,8 +222,23 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   constexpr int MI = TM / 32, NJ = TN / 32, WM = TM / 2, WN = TN / 2;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::STAGE];
 
-  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
-  const int kb = blockIdx.z * g.kchunk;
+  // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with
+  // its own L2), so consecutive workgroup ids -- the N tiles sharing one A row block -- would land
+  // on 8 different L2s.  Remap so each XCD gets a contiguous run of logical tiles.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (g.xcd_remap) {
+    const int total = gridDim.x * gridDim.y * gridDim.z;
+    const int lin = bx + gridDim.x * (by + gridDim.y * bz);
+    const int per = total / 8;
+    if (lin < 8 * per) {
+      const int logical = (lin % 8) * per + lin / 8;
+      bx = logical % gridDim.x;
+      by = (logical / gridDim.x) % gridDim.y;
+      bz = logical / (gridDim.x * gridDim.y);
+    }
+  }
+  const int n0 = bx * TN, m0 = by * TM;
+  const int kb = bz * g.kchunk;
   const int ke = min(g.K, kb + g.kchunk);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
@@ -323,7 +338,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
       if (m >= g.M || n >= g.N) continue;
       const float v0 = cs[ml * (TN + 1) + nl];
       if (gridDim.z > 1) {
-        g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = v0;
+        g.ws[((size_t)bz * g.M + m) * g.N + n] = v0;
         continue;
       }
       float v = g.alpha * v0;
@@ -345,7 +360,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
         if (m >= g.M || n >= g.N) continue;
         const float v0 = acc[i][j][r];
         if (gridDim.z > 1) {
-          g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = v0;
+          g.ws[((size_t)bz * g.M + m) * g.N + n] = v0;
           continue;
         }
         float v = g.alpha * v0;
@@ -359,6 +374,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
 constexpr int GEMM_MAX_SPLITS = 64;
+int g_gemm_xcd_remap = 1;   // 0 off, 1 long-K tiles only, 2 always
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
@@ -395,6 +411,10 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
   g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
   g.kchunk = kchunk;
+  // measured (profiles/README.md): the XCD-contiguous order pays off on long-K tiles (G-out paired
+  // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones
+  g.xcd_remap = g_gemm_xcd_remap == 2 ||
+                (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768)));
   dim3 grid(tn, tm, g.splitk), block(NT);
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \

@@ -42,6 +42,7 @@ struct GemmArgs {
   int vec;     // 1: both operands may be read with 16-B loads (see gemm.hip Chunk::load)
   int tile;    // output tile edge: 64 (default) or 32 (4x the workgroups, for short-K GEMMs)
   int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
+  int xcd_remap;   // 1: XCD-contiguous tile order (set by launch_gemm)
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -125,6 +126,7 @@ struct ColsumJob {
 };
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
+extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,

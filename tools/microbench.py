@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
     ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
     ap.add_argument("--unroll", action="store_true", help="epoch time vs training steps captured per graph")
+    ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -140,6 +141,19 @@ def main():
                 print(f"{name:28s} t{tile} " + "  ".join(row), flush=True)
             o.split_override = None
             o.tile_override = None
+        return
+    if args.xcd_sweep:
+        for name, (a, b, c, ta, tb) in shapes.items():
+            row = []
+            for rm in (0, 2):
+                prev = torch.ops.fedtgan.set_tuning("gemm_xcd_remap", rm)
+                row.append(per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev))
+                torch.ops.fedtgan.set_tuning("gemm_xcd_remap", prev)
+            print(f"{name:36s} dispatch order {row[0]:7.2f} us   XCD-contiguous {row[1]:7.2f} us", flush=True)
+        for rm in (0, 1, 2, 0, 1, 2):
+            prev = torch.ops.fedtgan.set_tuning("gemm_xcd_remap", rm)
+            print(f"full step xcd_remap={rm}: {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
+            torch.ops.fedtgan.set_tuning("gemm_xcd_remap", prev)
         return
     for name, (a, b, c, ta, tb) in shapes.items():
         res[name] = per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
