@@ -491,6 +491,18 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_bn_cols = (int)value;
     return prev;
   }
+  if (key == "adam_store") {
+    TORCH_CHECK(value == 0 || value == 2 || value == 16, "adam_store: 0 plain, 2 nt, 16 sc1");
+    const int64_t prev = fedtgan::g_adam_store;
+    fedtgan::g_adam_store = (int)value;
+    return prev;
+  }
+  if (key == "adam_max_blocks") {
+    TORCH_CHECK(value >= 1 && value <= 65535, "adam_max_blocks: 1..65535");
+    const int64_t prev = fedtgan::g_adam_max_blocks;
+    fedtgan::g_adam_max_blocks = (int)value;
+    return prev;
+  }
   if (key == "gemm_xcd_remap") {
     const int64_t prev = fedtgan::g_gemm_xcd_remap;
     TORCH_CHECK(value >= 0 && value <= 2, "gemm_xcd_remap: 0 off, 1 long-K tiles, 2 always");

@@ -385,8 +385,9 @@ static int act_waves(const SpanTables& sp) {
 
 template <typename K>
 static void allow_big_lds(K kernel, size_t bytes) {
-  if (bytes > 64 * 1024) hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (bytes > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
 }
 
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
@@ -975,6 +976,24 @@ void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, cons
 }
 
 // ============================================================================ Adam
+// Store policy of the updated p, m, v (tuning knob "adam_store"): 0 plain stores (dirty in L2, written
+// back at the kernel boundary: ~B / 6 TB/s, MI355X_MICROARCH.md "boundary"), otherwise a buffer store
+// with these cache bits (2 = nt, 16 = sc1 write-through) so the write-back overlaps the kernel.
+int g_adam_store = 16;
+int g_adam_max_blocks = 65535;
+
+template <int AUX>
+__device__ __forceinline__ void adam_store4(float4* base, __amdgpu_buffer_rsrc_t rs, int64_t i, float4 x) {
+  if constexpr (AUX == 0) {
+    base[i] = x;
+  } else {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 u = *reinterpret_cast<const u32x4*>(&x);
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, (int)(i * 16), 0, AUX);
+  }
+}
+
+template <int AUX>
 __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v,
                                                    const float* __restrict__ step, int64_t n4, float lr, float b1,
@@ -983,6 +1002,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
   const float bc1 = 1.f - powf(b1, t);
   const float bc2s = sqrtf(1.f - powf(b2, t));
   const float sz = lr / bc1;
+  const int bytes = (int)(n4 * 16);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(p, 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(m, 0, bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(v, 0, bytes, 0x00020000);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
     float* pf = reinterpret_cast<float*>(&pp);
@@ -996,7 +1019,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
       vf[q] = b2 * vf[q] + (1.f - b2) * gq * gq;
       pf[q] -= sz * mf[q] / (sqrtf(vf[q]) / bc2s + eps);
     }
-    p[i] = pp; m[i] = mm; v[i] = vv;
+    adam_store4<AUX>(p, rp, i, pp);
+    adam_store4<AUX>(m, rm, i, mm);
+    adam_store4<AUX>(v, rv, i, vv);
   }
   if (rng_bump && blockIdx.x == 0 && threadIdx.x == 0) rng_bump[0] += 1ull;
 }
@@ -1019,10 +1044,15 @@ void launch_adam(float* p, const float* g, float* m, float* v, const float* step
   const int64_t n4 = n / 4;
   // one float4 per thread where possible: a grid-stride loop over few workgroups keeps too few
   // loads in flight for HBM (19.5M-parameter wide-table D: 259 us at 1024 workgroups)
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 65535);
-  hipLaunchKernelGGL(adam_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, stream, reinterpret_cast<float4*>(p),
-                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),
-                     step, n4, lr, b1, b2, eps, wd, rng_ctr_bump);
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
+#define FEDTGAN_ADAM(AUX)                                                                                       \
+  hipLaunchKernelGGL(adam_kernel<AUX>, dim3(std::max(blocks, 1)), dim3(256), 0, stream, reinterpret_cast<float4*>(p), \
+                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),   \
+                     step, n4, lr, b1, b2, eps, wd, rng_ctr_bump)
+  if (g_adam_store == 2) FEDTGAN_ADAM(2);
+  else if (g_adam_store == 16) FEDTGAN_ADAM(16);
+  else FEDTGAN_ADAM(0);
+#undef FEDTGAN_ADAM
   if (n4 * 4 < n)
     hipLaunchKernelGGL(adam_tail_kernel, dim3(1), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2, eps,
                        wd);

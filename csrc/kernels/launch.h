@@ -127,6 +127,8 @@ struct ColsumJob {
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
+extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
+extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,

@@ -9,6 +9,7 @@ thread-local capture mode so every client captures and replays its own step grap
 """
 from __future__ import annotations
 
+import contextlib
 import threading
 import traceback
 from typing import Any, List, Optional
@@ -132,14 +133,20 @@ def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[tor
 
     def worker(rank: int):
         try:
+            stream_ctx = contextlib.nullcontext()
             if device.type == "cuda":
                 torch.cuda.set_device(device)
-            comm = ThreadComm(group, rank, device)
-            rt = FedRuntime(cfg, comm, device, federator=0)
-            rt.thread_local_capture = True
-            runtimes[rank] = rt
-            rt.initialize()
-            rt.fit()
+                # one HIP stream per emulated client: the clients' small step kernels (a few dozen
+                # workgroups each) run concurrently on the 256 CUs instead of queueing on one stream
+                if getattr(cfg, "client_streams", True):
+                    stream_ctx = torch.cuda.stream(torch.cuda.Stream(device))
+            with stream_ctx:
+                comm = ThreadComm(group, rank, device)
+                rt = FedRuntime(cfg, comm, device, federator=0)
+                rt.thread_local_capture = True
+                runtimes[rank] = rt
+                rt.initialize()
+                rt.fit()
         except BaseException as e:  # pragma: no cover - surfaced below
             errors.append(e)
             traceback.print_exc()

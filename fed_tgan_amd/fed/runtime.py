@@ -77,6 +77,7 @@ class FedConfig:
     # formatter threads of a CSV write (0: min(cores, 16)).  Measured: 4 background threads fall
     # behind a 21 ms round (the last flush then waits for a backlog): 20.9 -> 23.4 ms/epoch
     csv_threads: int = 0
+    client_streams: bool = True             # in-process emulation: one HIP stream per client thread
     seed: int = 0
     engine: EngineConfig = dataclasses.field(default_factory=EngineConfig)
     ckpt_every: int = 0

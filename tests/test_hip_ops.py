@@ -500,3 +500,24 @@ def test_wide_activation_and_backward(hip):
     torch.cuda.synchronize()
     assert torch.allclose(d1, d2, atol=1e-5, rtol=1e-4)
     assert torch.allclose(rows1.sum(), l2[0], rtol=1e-4)
+
+
+@pytest.mark.parametrize("aux", [0, 2, 16])
+def test_adam_store_policies_match_torch(hip, aux):
+    """Plain, non-temporal and write-through (sc1) buffer stores give the same Adam update."""
+    n = 4 * 70001 + 3
+    p = mat(n, seed=60)
+    g = mat(n, seed=61)
+    tp = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([tp], lr=2e-4, betas=(0.5, 0.9))
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    step = torch.ones(1, device=DEV)
+    prev = torch.ops.fedtgan.set_tuning("adam_store", aux)
+    try:
+        hip.adam(p, g, m, v, step, 2e-4, 0.5, 0.9, 1e-8, 0.0)
+    finally:
+        torch.ops.fedtgan.set_tuning("adam_store", prev)
+    tp.grad = g.clone()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(p, tp.detach(), atol=1e-6, rtol=1e-5)

@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
     ap.add_argument("--unroll", action="store_true", help="epoch time vs training steps captured per graph")
     ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
+    ap.add_argument("--adam-sweep", action="store_true", help="Adam store policy: plain / nt / sc1")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -141,6 +142,21 @@ def main():
                 print(f"{name:28s} t{tile} " + "  ".join(row), flush=True)
             o.split_override = None
             o.tile_override = None
+        return
+    if args.adam_sweep:
+        for aux in (0, 2, 16, 0, 2, 16):
+            prev = torch.ops.fedtgan.set_tuning("adam_store", aux)
+            t_adam = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8,
+                                             0.0), dev)
+            t_step = per_call(eng._one_step, dev, n=5, reps=20)
+            torch.ops.fedtgan.set_tuning("adam_store", prev)
+            print(f"adam_store={aux:2d}: adam D {t_adam:7.2f} us   full step {t_step:8.2f} us", flush=True)
+        for nb in (512, 1024, 2048, 65535):
+            prev = torch.ops.fedtgan.set_tuning("adam_max_blocks", nb)
+            t_adam = per_call(lambda: o.adam(eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 2e-4, 0.5, 0.9, 1e-8,
+                                             0.0), dev)
+            torch.ops.fedtgan.set_tuning("adam_max_blocks", prev)
+            print(f"adam_max_blocks={nb:5d}: adam D {t_adam:7.2f} us", flush=True)
         return
     if args.xcd_sweep:
         for name, (a, b, c, ta, tb) in shapes.items():

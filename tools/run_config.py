@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--json", default=None, help="append the JSON lines to this file")
+    ap.add_argument("--one-stream", action="store_true", help="emulated clients share one HIP stream")
     args = ap.parse_args()
 
     from fed_tgan_amd.data.schema import get_spec
@@ -53,7 +54,8 @@ def main():
     cfg = FedConfig(spec=spec, epochs=args.epochs, synthetic_rows=args.rows, shard_mode=args.shard,
                     dirichlet_alpha=args.alpha, out_dir=out, n_sample=args.n_sample, backend=args.backend,
                     gmm_backend="torch", aggregation=args.aggregation, seed=args.seed,
-                    engine=EngineConfig(precision=args.precision), verbose=True)
+                    engine=EngineConfig(precision=args.precision), verbose=True,
+                    client_streams=not args.one_stream)
     t0 = time.time()
     if args.clients == 1:
         rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=dev), dev)
