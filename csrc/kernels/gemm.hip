@@ -42,6 +42,17 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int NT = 256;
 
+// output / split-K slab store: plain, or write-through (sc1) so the kernel boundary finds no dirty
+// L2 lines to write back (MI355X_MICROARCH.md "boundary": + bytes / 6 TB/s)
+__device__ __forceinline__ void st_out(float* base, size_t idx, float v, int wt) {
+  if (wt) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)(idx * 4), 0, 16);
+  } else {
+    base[idx] = v;
+  }
+}
+
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
   const int epi = g.epi;
   if (epi == EPI_LRELU_DROPOUT) {
@@ -338,14 +349,14 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
       if (m >= g.M || n >= g.N) continue;
       const float v0 = cs[ml * (TN + 1) + nl];
       if (gridDim.z > 1) {
-        g.ws[((size_t)bz * g.M + m) * g.N + n] = v0;
+        st_out(g.ws, ((size_t)bz * g.M + m) * g.N + n, v0, g.wt);
         continue;
       }
       float v = g.alpha * v0;
       float* cp = g.c + (size_t)m * g.ldc + n;
       if (g.beta != 0.f) v += g.beta * (*cp);
       if (g.bias) v += g.bias[n];
-      *cp = apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n);
+      st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
     }
     return;
   }
@@ -360,21 +371,22 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
         if (m >= g.M || n >= g.N) continue;
         const float v0 = acc[i][j][r];
         if (gridDim.z > 1) {
-          g.ws[((size_t)bz * g.M + m) * g.N + n] = v0;
+          st_out(g.ws, ((size_t)bz * g.M + m) * g.N + n, v0, g.wt);
           continue;
         }
         float v = g.alpha * v0;
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
         if (g.bias) v += g.bias[n];
-        *cp = apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n);
+        st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
 }
 
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
 constexpr int GEMM_MAX_SPLITS = 64;
-int g_gemm_xcd_remap = 1;   // 0 off, 1 long-K tiles only, 2 always
+int g_gemm_xcd_remap = 1;
+int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores   // 0 off, 1 long-K tiles only, 2 always
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
@@ -394,7 +406,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
     float* cp = g.c + (size_t)m * g.ldc + n;
     if (g.beta != 0.f) v += g.beta * (*cp);
     if (g.bias) v += g.bias[n];
-    *cp = apply_epi(g, v, m, n, step, idx);
+    st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, idx), g.wt);
   }
 }
 
@@ -411,6 +423,9 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
   g.splitk = (std::max(g.K, 1) + kchunk - 1) / kchunk;
   g.kchunk = kchunk;
+  // (buffer stores take 32-bit byte offsets)
+  g.wt = g_gemm_store_wt && (int64_t)g.M * g.ldc * 4 < (int64_t)INT32_MAX &&
+         (int64_t)g.splitk * g.M * g.N * 4 < (int64_t)INT32_MAX;
   // measured (profiles/README.md): the XCD-contiguous order pays off on long-K tiles (G-out paired
   // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones
   g.xcd_remap = g_gemm_xcd_remap == 2 ||

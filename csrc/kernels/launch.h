@@ -43,6 +43,7 @@ struct GemmArgs {
   int tile;    // output tile edge: 64 (default) or 32 (4x the workgroups, for short-K GEMMs)
   int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
   int xcd_remap;   // 1: XCD-contiguous tile order (set by launch_gemm)
+  int wt;          // 1: write-through (sc1) output stores (set by launch_gemm)
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -129,6 +130,7 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
+extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,

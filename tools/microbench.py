@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--unroll", action="store_true", help="epoch time vs training steps captured per graph")
     ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
     ap.add_argument("--adam-sweep", action="store_true", help="Adam store policy: plain / nt / sc1")
+    ap.add_argument("--store-sweep", action="store_true", help="GEMM output stores: plain / write-through")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -142,6 +143,16 @@ def main():
                 print(f"{name:28s} t{tile} " + "  ".join(row), flush=True)
             o.split_override = None
             o.tile_override = None
+        return
+    if args.store_sweep:
+        for wt in (0, 1, 0, 1):
+            prev = torch.ops.fedtgan.set_tuning("gemm_store_wt", wt)
+            row = [per_call(lambda a=a, b=b, c=c, ta=ta, tb=tb: o.gemm(a, b, c, ta=ta, tb=tb), dev)
+                   for (a, b, c, ta, tb) in shapes.values()]
+            t_step = per_call(eng._one_step, dev, n=5, reps=20)
+            torch.ops.fedtgan.set_tuning("gemm_store_wt", prev)
+            print(f"gemm_store_wt={wt}: GEMMs " + " ".join(f"{x:5.2f}" for x in row) + f"   full step {t_step:8.2f} us",
+                  flush=True)
         return
     if args.adam_sweep:
         for aux in (0, 2, 16, 0, 2, 16):
