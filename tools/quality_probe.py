@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--rows", type=int, default=40000)
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--top", type=int, default=6)
+    ap.add_argument("--gmm", default="torch", help="torch | sklearn (VGM fit backend)")
     args = ap.parse_args()
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.data.synthetic import generate
@@ -59,7 +60,7 @@ def main():
     for seed in args.seeds:
         out = tempfile.mkdtemp(prefix="fedtgan_q_")
         cfg = FedConfig(spec=spec, epochs=args.epochs, synthetic_rows=args.rows, out_dir=out, n_sample=40000,
-                        gmm_backend="torch", seed=seed, engine=EngineConfig(precision=args.precision), verbose=False,
+                        gmm_backend=args.gmm, seed=seed, engine=EngineConfig(precision=args.precision), verbose=False,
                         async_csv=False)
         rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=dev), dev)
         rt.initialize()
@@ -70,7 +71,7 @@ def main():
             jsd, wd = stat_sim(real, fake, spec.categorical_list)
             cols = per_column(real, fake, set(spec.categorical_list))
             worst = sorted(cols.items(), key=lambda kv: -kv[1][1])[:args.top]
-            print(json.dumps({"seed": seed, "epoch": ep, "avg_jsd": round(jsd, 4), "avg_wd": round(wd, 4),
+            print(json.dumps({"gmm": args.gmm, "seed": seed, "epoch": ep, "avg_jsd": round(jsd, 4), "avg_wd": round(wd, 4),
                               "worst": [(k, v[0], round(v[1], 4)) for k, v in worst]}), flush=True)
 
 
