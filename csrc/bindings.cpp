@@ -173,14 +173,18 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
 }
 
 fedtgan::SpanTables spans_of(const Tensor& start, const Tensor& width, const Tensor& kind, const Tensor& cidx,
-                             const Tensor& elem) {
+                             const Tensor& packed, int64_t dim) {
   TORCH_CHECK(start.scalar_type() == at::kInt && width.scalar_type() == at::kInt && kind.scalar_type() == at::kInt &&
-                  cidx.scalar_type() == at::kInt && elem.scalar_type() == at::kInt,
+                  cidx.scalar_type() == at::kInt && packed.scalar_type() == at::kInt,
               "span tables must be int32");
   TORCH_CHECK(start.numel() == width.numel() && start.numel() == kind.numel() && start.numel() == cidx.numel(),
               "span tables: sizes");
+  const int S = (int)start.numel();
+  TORCH_CHECK(packed.is_contiguous() && packed.numel() == fedtgan::span_packed_len((int)dim, S) &&
+                  reinterpret_cast<uintptr_t>(packed.data_ptr()) % 16 == 0,
+              "span tables: packed table must hold [elem | kind | start | width | cidx] padded to 4 ints");
   fedtgan::SpanTables sp{start.data_ptr<int>(), width.data_ptr<int>(), kind.data_ptr<int>(), cidx.data_ptr<int>(),
-                         elem.data_ptr<int>(), (int)start.numel(), (int)elem.numel()};
+                         packed.data_ptr<int>(), S, (int)dim};
   TORCH_CHECK(fedtgan::activation_smem_bytes(sp) <= 160 * 1024, "activation: row image exceeds the 160 KiB LDS");
   return sp;
 }
@@ -192,7 +196,6 @@ void activate(const Tensor& logits, const Tensor& out, const Tensor& start, cons
   check_f32_2d(logits, "logits");
   check_f32_2d(out, "out");
   TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) >= logits.size(1), "activate: shapes");
-  TORCH_CHECK(elem.numel() == logits.size(1), "activate: elem_span must cover every data column");
   fedtgan::SlerpFuse sl{};
   if (slerp_real.has_value() && slerp_real->defined()) {
     TORCH_CHECK(slerp_out.has_value() && slerp_out->defined(), "activate: slerp needs an output");
@@ -211,14 +214,13 @@ void activate(const Tensor& logits, const Tensor& out, const Tensor& start, cons
     sl.stream = (uint32_t)slerp_stream;
   }
   fedtgan::launch_activate(cfp(logits), ld_of(logits), fp(out), ld_of(out), (int)logits.size(0),
-                           spans_of(start, width, kind, cidx, elem), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
+                           spans_of(start, width, kind, cidx, elem, logits.size(1)), (float)tau, (uint64_t)seed, ctr_ptr(rng_ctr),
                            (uint32_t)stream, sl, cur_stream());
 }
 
 void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, const Tensor& start, const Tensor& width,
                 const Tensor& kind, const Tensor& cidx, const Tensor& elem, const Tensor& col, const Tensor& opt,
                 const Tensor& dlogits, const Tensor& loss, double tau) {
-  TORCH_CHECK(elem.numel() == logits.size(1), "act_bwd_ce: elem_span must cover every data column");
   check_f32_2d(dact, "dact");
   check_f32_2d(act, "act");
   check_f32_2d(logits, "logits");
@@ -230,7 +232,7 @@ void act_bwd_ce(const Tensor& dact, const Tensor& act, const Tensor& logits, con
   const bool per_row = rows > 1 && loss.numel() == rows;
   TORCH_CHECK(per_row || loss.numel() >= 1, "act_bwd_ce: loss");
   fedtgan::launch_act_bwd_ce(cfp(dact), ld_of(dact), cfp(act), ld_of(act), cfp(logits), ld_of(logits),
-                             spans_of(start, width, kind, cidx, elem), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
+                             spans_of(start, width, kind, cidx, elem, logits.size(1)), col.data_ptr<int>(), opt.data_ptr<int>(), fp(dlogits),
                              ld_of(dlogits), (int)rows, (float)tau, fp(loss), per_row ? 1 : 0, cur_stream());
 }
 

@@ -208,14 +208,19 @@ __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float*
   t.start = t.kind + S;
   t.width = t.start + S;
   t.cidx = t.width + S;
-  t.rows = reinterpret_cast<float*>(t.cidx + S);
-  // (the host encodes the softmax bit into elem_span: no dependent table lookup here)
-  for (int i = threadIdx.x; i < D; i += blockDim.x) t.einfo[i] = sp.elem_span[i];
-  for (int i = threadIdx.x; i < S; i += blockDim.x) {
-    t.kind[i] = sp.kind[i];
-    t.start[i] = sp.start[i];
-    t.width[i] = sp.width[i];
-    t.cidx[i] = sp.cond_idx[i];
+  const int n4 = ((D + 4 * S + 3) & ~3) / 4;   // span_packed_len (launch.h) / 4
+  t.rows = smem + 4 * n4;
+  // one contiguous 16-B copy, ACT_STAGE loads in flight per thread before the first LDS store
+  constexpr int ACT_STAGE = 8;
+  const int4* src = reinterpret_cast<const int4*>(sp.packed);
+  int4* dst = reinterpret_cast<int4*>(smem);
+  for (int i0 = threadIdx.x; i0 < n4; i0 += ACT_STAGE * blockDim.x) {
+    int4 v[ACT_STAGE];
+#pragma unroll
+    for (int u = 0; u < ACT_STAGE; ++u) v[u] = src[min(i0 + u * (int)blockDim.x, n4 - 1)];
+#pragma unroll
+    for (int u = 0; u < ACT_STAGE; ++u)
+      if (i0 + u * (int)blockDim.x < n4) dst[i0 + u * blockDim.x] = v[u];
   }
   __syncthreads();
   return t;
@@ -372,7 +377,8 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
 }
 
 static size_t act_smem_bytes(const SpanTables& sp, int waves) {
-  return (size_t)(sp.dim + 4 * sp.n_span) * sizeof(int) + (size_t)waves * (sp.dim + 2 * sp.n_span) * sizeof(float);
+  return (size_t)span_packed_len(sp.dim, sp.n_span) * sizeof(int) +
+         (size_t)waves * (sp.dim + 2 * sp.n_span) * sizeof(float);
 }
 
 // wide tables (hundreds of columns, thousands of spans) get fewer rows per workgroup so the

@@ -81,10 +81,14 @@ struct SpanTables {
   const int* width;
   const int* kind;      // 0 tanh, 1 softmax
   const int* cond_idx;  // softmax span -> conditional column index (or -1)
-  const int* elem_span; // data column -> span index
+  // host-packed copy of every table the activation kernels stage in LDS, in LDS order:
+  // [elem_span | SOFTMAX bit (D) | kind (S) | start (S) | width (S) | cond_idx (S)], zero-padded to a
+  // multiple of 4 ints (one 16-B-load copy per workgroup instead of per-table loops)
+  const int* packed;
   int n_span;
   int dim;              // data_dim (sum of widths)
 };
+inline int span_packed_len(int dim, int n_span) { return (dim + 4 * n_span + 3) & ~3; }
 
 size_t activation_smem_bytes(const SpanTables& sp);   // dynamic LDS of the activation kernels
 

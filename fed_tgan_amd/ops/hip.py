@@ -116,9 +116,12 @@ class HipOps:
             elem = []      # data column -> span index, | 1 << 30 for softmax spans (kernel-side einfo)
             for i, (s, w, k) in enumerate(spans):
                 elem.extend([i | ((1 << 30) if k != 0 else 0)] * w)
+            st, wd, kd = [s for s, _, _ in spans], [w for _, w, _ in spans], [k for _, _, k in spans]
+            # the LDS image the activation kernels stage: [elem | kind | start | width | cidx], padded to 4
+            packed = elem + kd + st + wd + cidx
+            packed += [0] * (-len(packed) % 4)
             mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
-            t = (mk([s for s, _, _ in spans]), mk([w for _, w, _ in spans]), mk([k for _, _, k in spans]), mk(cidx),
-                 mk(elem))
+            t = (mk(st), mk(wd), mk(kd), mk(cidx), mk(packed))
             self._spans[key] = t
         return t
 
