@@ -69,3 +69,19 @@ def test_pending_host_copy_matches_sync_copy():
     torch.cuda.synchronize()
     assert ph.shape == (40000, 42) and np.array_equal(got, ref)
     assert float(junk[0, 0]) == 7.0
+
+
+def test_gpu_two_process_federation_gloo_data_plane(tmp_path):
+    """Two client processes driving HIP engines on the one GPU of the box (RCCL needs a GPU per rank,
+    so the data plane is gloo here): weighted all-reduce of device buffers, sharded generation
+    gathered to rank 0, uneven shares."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    cmd = [sys.executable, "-m", "dtds.distributed", "-world_size", "2", "-colocated", "-data_backend", "gloo",
+           "-backend", "hip", "-epochs", "2", "-synthetic_rows", "4000", "-n_sample", "3001", "-out_dir", str(tmp_path),
+           "-quiet"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check_outputs(tmp_path, 2, 3001)
