@@ -172,8 +172,12 @@ class FedRuntime:
     def _local_frame(self) -> pd.DataFrame:
         cfg, c = self.cfg, self.comm
         k, idx = c.n_clients, c.client_index
-        if cfg.datapath and os.path.exists(cfg.datapath.format(client=idx, rank=self.rank)):
-            return pd.read_csv(cfg.datapath.format(client=idx, rank=self.rank))
+        if cfg.datapath:
+            path = cfg.datapath.format(client=idx, rank=self.rank)
+            if os.path.exists(path):
+                return pd.read_csv(path)
+            print(f"[data] rank {self.rank}: {path} not found; using the synthetic {cfg.spec.name}-schema "
+                  f"generator ({cfg.synthetic_rows} rows, shard mode {cfg.shard_mode})", flush=True)
         if cfg.shard_mode == "independent":
             df = generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx)
         else:

@@ -160,3 +160,19 @@ def test_heartbeat_names_a_dead_rank(tmp_path):
     assert procs[0].returncode != 0
     assert "monitoredBarrier" in err0 and "1" in err0, err0[-2000:]
     assert time.time() - t0 < 240
+
+
+def test_real_csv_datapath_per_client(tmp_path):
+    """-datapath with '{client}' reads each client's own CSV (the reference's real-data path), with
+    blanks in a categorical column; the clients' row counts drive steps and weights."""
+    from fed_tgan_amd.data.synthetic import generate
+    spec = intrusion_spec()
+    for i, n in enumerate((1200, 700)):
+        df = generate(spec, n, seed=40 + i)
+        df.loc[df.index[:5], "protocol_type"] = np.nan          # blanks -> "empty" category
+        df.to_csv(tmp_path / f"intr_client{i}.csv", index=False)
+    cfg = _cfg(tmp_path, datapath=str(tmp_path / "intr_client{client}.csv"), synthetic_rows=999999)
+    rt = run_local_emulation(cfg, 2, backend="torch", device=torch.device("cpu"))
+    assert rt.rows == [1200, 700] and rt.steps == [12, 7]
+    out = pd.read_csv(tmp_path / "Intrusion_result" / "Intrusion_synthesis_epoch_1.csv")
+    assert out.shape == (600, 42)
