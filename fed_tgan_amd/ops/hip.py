@@ -50,11 +50,6 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
     return 32, int(max(1, min(-(-512 // t32), -(-bursts // 2), cap_ws)))
 
 
-def _splitk(M: int, N: int, K: int, kc: int = 128) -> int:
-    """Split factor of the plan (kept for callers that only need the split)."""
-    return _plan(M, N, K, kc)[1]
-
-
 GEMM_MAX_SPLITS = 64   # gemm.hip: the split-K epilogue keeps every slab value in registers
 
 
