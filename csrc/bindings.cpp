@@ -56,7 +56,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
           const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
-          const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile) {
+          const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -116,7 +116,27 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.head_coef = cfp(*head_coef);
     g.head_v = cfp(*head_v);
   }
-  fedtgan::launch_gemm(g, cur_stream());
+  // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
+  // must be independent -- neither reads what the other writes); group 0: launch now
+  thread_local fedtgan::GemmArgs held{};
+  thread_local bool has_held = false;
+  thread_local hipStream_t held_stream = nullptr;
+  const hipStream_t hs = cur_stream();
+  if (group == 1) {
+    TORCH_CHECK(!has_held, "gemm: a GEMM is already held for pairing");
+    held = g;
+    has_held = true;
+    held_stream = hs;
+    return;
+  }
+  if (group == 2) {
+    TORCH_CHECK(has_held && held_stream == hs, "gemm: group 2 needs a held GEMM on the same stream");
+    has_held = false;
+    fedtgan::launch_gemm_pair(held, g, hs);
+    return;
+  }
+  TORCH_CHECK(!has_held, "gemm: a held GEMM was never paired");
+  fedtgan::launch_gemm(g, hs);
 }
 
 void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<Tensor>& xf, const optional<Tensor>& xr,
@@ -510,6 +530,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gemm_store_wt = value ? 1 : 0;
     return prev;
   }
+  if (key == "gemm_pairs") {
+    const int64_t prev = fedtgan::g_gemm_pairs;
+    fedtgan::g_gemm_pairs = value ? 1 : 0;
+    return prev;
+  }
   if (key == "gemm_xcd_remap") {
     const int64_t prev = fedtgan::g_gemm_xcd_remap;
     TORCH_CHECK(value >= 0 && value <= 2, "gemm_xcd_remap: 0 off, 1 long-K tiles, 2 always");
@@ -526,7 +551,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
-      "Tensor? head_v, Tensor(e!)? head_a, int tile) -> ()");
+      "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

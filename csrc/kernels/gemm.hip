@@ -226,26 +226,27 @@ struct Cfg {
 // for large-M x N GEMMs -- generation at M = 40k, wide tables -- where the operand re-reads of
 // small tiles make the GEMM L2-bandwidth-bound):
 // 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
+// The body of one output tile; (bx, by, bz) index the tile within a (gx, gy, gz) tile grid.  Called by
+// gemm_kernel (one GEMM per launch) and gemm_pair_kernel (two independent GEMMs in one launch).
 template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
-__global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int gx, int gy, int gz,
+                                          unsigned char* __restrict__ smem) {
   using C = Cfg<F32, TM, TN>;
   constexpr int KC = C::KC;
   constexpr int MI = TM / 32, NJ = TN / 32, WM = TM / 2, WN = TN / 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * C::STAGE];
 
   // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with
   // its own L2), so consecutive workgroup ids -- the N tiles sharing one A row block -- would land
   // on 8 different L2s.  Remap so each XCD gets a contiguous run of logical tiles.
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (g.xcd_remap) {
-    const int total = gridDim.x * gridDim.y * gridDim.z;
-    const int lin = bx + gridDim.x * (by + gridDim.y * bz);
+    const int total = gx * gy * gz;
+    const int lin = bx + gx * (by + gy * bz);
     const int per = total / 8;
     if (lin < 8 * per) {
       const int logical = (lin % 8) * per + lin / 8;
-      bx = logical % gridDim.x;
-      by = (logical / gridDim.x) % gridDim.y;
-      bz = logical / (gridDim.x * gridDim.y);
+      bx = logical % gx;
+      by = (logical / gx) % gy;
+      bz = logical / (gx * gy);
     }
   }
   const int n0 = bx * TN, m0 = by * TM;
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
       const int m = m0 + ml, n = n0 + nl;
       if (m >= g.M || n >= g.N) continue;
       const float v0 = cs[ml * (TN + 1) + nl];
-      if (gridDim.z > 1) {
+      if (gz > 1) {
         st_out(g.ws, ((size_t)bz * g.M + m) * g.N + n, v0, g.wt);
         continue;
       }
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
         const int n = n0 + wn * WN + j * 16 + (lane & 15);
         if (m >= g.M || n >= g.N) continue;
         const float v0 = acc[i][j][r];
-        if (gridDim.z > 1) {
+        if (gz > 1) {
           st_out(g.ws, ((size_t)bz * g.M + m) * g.N + n, v0, g.wt);
           continue;
         }
@@ -384,9 +385,46 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
 
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
+__global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<F32, TM, TN>::STAGE];
+  gemm_tile<TA, TB, F32, VEC, TM, TN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z, smem);
+}
+
+// Two independent GEMMs in ONE launch (horizontal fusion): the first n1 workgroups run GEMM 1's
+// tiles, the rest GEMM 2's.  The step has several such pairs (e.g. a weight gradient and the next
+// backward product of the same layer); as two launches they pay a kernel boundary and run their
+// few dozen workgroups each back to back on an otherwise idle chip.
+struct Grid3 {
+  int x, y, z;
+};
+
+template <class P1, class P2>
+__global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2, Grid3 grid1, Grid3 grid2) {
+  constexpr int S1 = 2 * Cfg<false, P1::TM, P1::TM>::STAGE, S2 = 2 * Cfg<false, P2::TM, P2::TM>::STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[S1 > S2 ? S1 : S2];
+  const int n1 = grid1.x * grid1.y * grid1.z;
+  int b = blockIdx.x;
+  if (b < n1) {
+    gemm_tile<P1::TA, P1::TB, false, P1::VEC, P1::TM, P1::TM>(g1, b % grid1.x, (b / grid1.x) % grid1.y,
+                                                               b / (grid1.x * grid1.y), grid1.x, grid1.y, grid1.z, smem);
+  } else {
+    b -= n1;
+    gemm_tile<P2::TA, P2::TB, false, P2::VEC, P2::TM, P2::TM>(g2, b % grid2.x, (b / grid2.x) % grid2.y,
+                                                               b / (grid2.x * grid2.y), grid2.x, grid2.y, grid2.z, smem);
+  }
+}
+
+template <bool TA_, bool TB_, bool VEC_, int TM_>
+struct GemmShape {
+  static constexpr bool TA = TA_, TB = TB_, VEC = VEC_;
+  static constexpr int TM = TM_;
+};
+
 constexpr int GEMM_MAX_SPLITS = 64;
 int g_gemm_xcd_remap = 1;
-int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores   // 0 off, 1 long-K tiles only, 2 always
+int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
+int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)   // 0 off, 1 long-K tiles only, 2 always
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
@@ -412,10 +450,11 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
 
 int gemm_kc(int f32) { return f32 ? Cfg<true, 64, 64>::KC : Cfg<false, 64, 64>::KC; }
 
-void launch_gemm(GemmArgs g, hipStream_t stream) {
-  if (g.M <= 0 || g.N <= 0) return;
+// tile grid, split count, K chunk and per-launch flags of one GEMM
+static dim3 gemm_prepare(GemmArgs& g) {
   const int KC = gemm_kc(g.f32);
   const int T = g.tile == 32 ? 32 : (g.tile == 128 ? 128 : 64);   // square output tile
+  g.tile = T;
   const int tm = (g.M + T - 1) / T, tn = (g.N + T - 1) / T;
   if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
   g.splitk = std::min(g.splitk, GEMM_MAX_SPLITS);   // the epilogue holds every slab value in registers
@@ -430,7 +469,12 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
   // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones
   g.xcd_remap = g_gemm_xcd_remap == 2 ||
                 (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768)));
-  dim3 grid(tn, tm, g.splitk), block(NT);
+  return dim3(tn, tm, g.splitk);
+}
+
+static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
+  const dim3 block(NT);
+  const int T = g.tile;
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
   if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, 0, stream, g);       \
@@ -459,14 +503,64 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
 #undef FEDTGAN_GEMM_TILES
 #undef FEDTGAN_GEMM_LAYOUTS
 #undef FEDTGAN_GEMM_DISPATCH
-  if (grid.z > 1) {
-    const size_t total = (size_t)g.M * g.N;
-    int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
-    if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, dim3(blocks), dim3(256), 0, stream, g);
-    else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, dim3(blocks), dim3(256), 0, stream, g);
-    else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, dim3(blocks), dim3(256), 0, stream, g);
-    else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, dim3(blocks), dim3(256), 0, stream, g);
+}
+
+static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
+  if (g.splitk <= 1) return;
+  const size_t total = (size_t)g.M * g.N;
+  int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
+  if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, dim3(blocks), dim3(256), 0, stream, g);
+  else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, dim3(blocks), dim3(256), 0, stream, g);
+  else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, dim3(blocks), dim3(256), 0, stream, g);
+  else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, dim3(blocks), dim3(256), 0, stream, g);
+}
+
+void launch_gemm(GemmArgs g, hipStream_t stream) {
+  if (g.M <= 0 || g.N <= 0) return;
+  const dim3 grid = gemm_prepare(g);
+  gemm_dispatch(g, grid, stream);
+  gemm_epilogue_launch(g, stream);
+}
+
+// The instantiated pairs: a weight gradient (op(A) = A^T, 64- or 32-tile) beside the next backward
+// product (NT or NN, 32-tile), bf16 -- every pair the training step issues.  Anything else runs as
+// two launches.
+template <bool V1, bool V2>
+static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3 b, hipStream_t stream) {
+  const dim3 grid(a.x * a.y * a.z + b.x * b.y * b.z), block(NT);
+#define FEDTGAN_PAIR(T1, TA2, TB2)                                                                              \
+  hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>>), grid, block, \
+                     0, stream, g1, g2, a, b)
+  if (!(g1.ta && !g1.tb) || g2.ta || g2.tile != 32) return false;
+  if (g1.tile == 64) {
+    if (g2.tb) FEDTGAN_PAIR(64, false, true); else FEDTGAN_PAIR(64, false, false);
+  } else if (g1.tile == 32) {
+    if (g2.tb) FEDTGAN_PAIR(32, false, true); else FEDTGAN_PAIR(32, false, false);
+  } else {
+    return false;
   }
+#undef FEDTGAN_PAIR
+  return true;
+}
+
+void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
+  if (g1.M <= 0 || g1.N <= 0) return launch_gemm(g2, stream);
+  if (g2.M <= 0 || g2.N <= 0) return launch_gemm(g1, stream);
+  const dim3 d1 = gemm_prepare(g1), d2 = gemm_prepare(g2);
+  const Grid3 a{(int)d1.x, (int)d1.y, (int)d1.z}, b{(int)d2.x, (int)d2.y, (int)d2.z};
+  bool fused = false;
+  if (!g1.f32 && !g2.f32 && g_gemm_pairs) {
+    if (g1.vec && g2.vec) fused = gemm_pair_vec<true, true>(g1, a, g2, b, stream);
+    else if (g1.vec) fused = gemm_pair_vec<true, false>(g1, a, g2, b, stream);
+    else if (g2.vec) fused = gemm_pair_vec<false, true>(g1, a, g2, b, stream);
+    else fused = gemm_pair_vec<false, false>(g1, a, g2, b, stream);
+  }
+  if (!fused) {
+    gemm_dispatch(g1, d1, stream);
+    gemm_dispatch(g2, d2, stream);
+  }
+  gemm_epilogue_launch(g1, stream);
+  gemm_epilogue_launch(g2, stream);
 }
 
 }  // namespace fedtgan

@@ -47,6 +47,9 @@ struct GemmArgs {
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
+// two independent GEMMs in one launch where the pair is instantiated, else two launches
+void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream);
+extern int g_gemm_pairs;
 
 struct SampleArgs {
   int B, E, C, Dd, n_col, maxw, n_rows;

@@ -529,10 +529,12 @@ class CTGANEngine:
         # rows) starts on a side lane as soon as its right operand is complete
         inp = self.X[I]
         prev = self.X
+        pair = self.lanes is None     # weight gradient + R product of a layer: one launch
         for i in range(L):
             with self._lane(1 + i % 2):
-                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True)
-            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I])
+                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=1 if pair else 0)
+            o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
+                   group=2 if pair else 0)
             inp = self.dl[i][I]
             prev = self.dl[i]
         fr = self.rows_fr
@@ -580,15 +582,18 @@ class CTGANEngine:
         o = self.ops
         # generator backward: the dH chain on the main lane, weight gradients on side lanes
         Lg = len(self.gdims)
+        pair = self.lanes is None and Lg > 0   # weight gradient + dX product of a layer: one launch
+        top = self.off[0]
         with self._lane(1):
             x, dW = self._kpad(self.H, 0, self.g["G.out.W"])
-            o.gemm(self.dlogits, x, dW, ta=True)
+            o.gemm(self.dlogits, x, dW, ta=True, group=1 if pair else 0)
+            if pair:
+                o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top], group=2)
             # G.out bias grad + the G-phase WGAN value (-mean D(fake)) + the cond CE sum in one launch
             src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
             o.colsum_many([self.dlogits, src, self.ce_rows.view(-1, 1)], [self.g["G.out.b"], out, self.metrics[3:4]],
                           weights=[None, w, None], dots=[None, dot, None])
-        top = self.off[0]
-        if Lg:
+        if Lg and not pair:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
         for i in range(Lg - 1, -1, -1):
             a, b_ = self.off[i], self.off[i + 1]
@@ -596,10 +601,12 @@ class CTGANEngine:
                           self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"],
                           self.g[f"G.{i}.b"])
             if i > 0:
+                pair = self.lanes is None
                 with self._lane(2 + i % 2):
                     x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
-                    o.gemm(self.da[i], x, dW, ta=True)
-                o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0)
+                    o.gemm(self.da[i], x, dW, ta=True, group=1 if pair else 0)
+                o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0,
+                       group=2 if pair else 0)
             else:
                 x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
                 o.gemm(self.da[i], x, dW, ta=True)

@@ -122,9 +122,11 @@ class HipOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None):
+             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0):
         """C = epi(alpha op(A) op(B) + beta C + bias).  head = (coef [M], v [N], A_out [M, N]):
-        with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed)."""
+        with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
+        group 1 holds this GEMM, group 2 launches it together with the held one in ONE kernel (the
+        two must be independent); 0 launches now."""
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
@@ -138,7 +140,7 @@ class HipOps:
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
-                    float(bn_eps), self.f32, *(head or (None, None, None)), int(tile))
+                    float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1):

@@ -29,7 +29,7 @@ class TorchOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, head=None):
+             slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0):
         """c = epi(alpha * op(a) @ op(b) + beta * c + bias)."""
         A = a.t() if ta else a
         B = b.t() if tb else b

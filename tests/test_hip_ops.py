@@ -521,3 +521,38 @@ def test_adam_store_policies_match_torch(hip, aux):
     opt.step()
     torch.cuda.synchronize()
     assert torch.allclose(p, tp.detach(), atol=1e-6, rtol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["dv_r64", "dv_r32", "dw_dh", "fallback"])
+def test_gemm_pair_launch_matches_two_launches(hip, case):
+    """Two independent GEMMs held + paired into one launch equal the same GEMMs launched one by one
+    (including a split-K second GEMM and a pair with no fused instantiation)."""
+    torch.manual_seed(3)
+    if case == "dv_r64":      # weight gradient (64-tile) + split-K NT product with a mask epilogue
+        A, X, W = mat(150, 256, seed=70), mat(150, 6280, seed=71), mat(256, 6280, seed=72)
+        ms = (torch.rand(50, 256, device=DEV) > 0.5).float() * 2
+        jobs = [dict(a=A, b=X, c=torch.zeros(256, 6280, device=DEV), ta=True),
+                dict(a=X[:50], b=W, c=torch.zeros(50, 256, device=DEV), tb=True, epi=2, ms=ms)]
+    elif case == "dv_r32":
+        A, D0, W = mat(150, 256, seed=73), mat(150, 256, seed=74), mat(256, 256, seed=75)
+        jobs = [dict(a=A, b=D0, c=torch.zeros(256, 256, device=DEV), ta=True),
+                dict(a=D0[:50], b=W, c=torch.zeros(50, 256, device=DEV), tb=True)]
+    elif case == "dw_dh":     # weight gradient + NN product accumulating into its output (beta = 1)
+        G, H, W = mat(500, 325, seed=76), mat(500, 943, seed=77), mat(325, 512, seed=78)
+        jobs = [dict(a=G, b=H, c=torch.zeros(325, 943, device=DEV), ta=True),
+                dict(a=G, b=W, c=mat(500, 512, seed=79), beta=1.0)]
+    else:                     # NN first: no fused instantiation, runs as two launches
+        P, Q = mat(200, 300, seed=80), mat(300, 100, seed=81)
+        jobs = [dict(a=P, b=Q, c=torch.zeros(200, 100, device=DEV)),
+                dict(a=P, b=Q, c=torch.zeros(200, 100, device=DEV), beta=1.0)]
+    refs = []
+    for j in jobs:
+        j2 = dict(j)
+        j2["c"] = j["c"].clone()
+        hip.gemm(**j2)
+        refs.append(j2["c"])
+    hip.gemm(**jobs[0], group=1)
+    hip.gemm(**jobs[1], group=2)
+    torch.cuda.synchronize()
+    for j, r in zip(jobs, refs):
+        assert torch.allclose(j["c"], r, atol=1e-5, rtol=1e-5)

@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
     ap.add_argument("--adam-sweep", action="store_true", help="Adam store policy: plain / nt / sc1")
     ap.add_argument("--store-sweep", action="store_true", help="GEMM output stores: plain / write-through")
+    ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -143,6 +144,12 @@ def main():
                 print(f"{name:28s} t{tile} " + "  ".join(row), flush=True)
             o.split_override = None
             o.tile_override = None
+        return
+    if args.pair_sweep:
+        for pr in (0, 1, 0, 1):
+            prev = torch.ops.fedtgan.set_tuning("gemm_pairs", pr)
+            print(f"gemm_pairs={pr}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
+            torch.ops.fedtgan.set_tuning("gemm_pairs", prev)
         return
     if args.store_sweep:
         for wt in (0, 1, 0, 1):
