@@ -289,9 +289,11 @@ void d_head(const Tensor& d, const Tensor& ms, const Tensor& v, const Tensor& e,
                          ld_of(a), (int)rows, (int)cols, fp(loss), cur_stream());
 }
 
-void colsum_ex(at::TensorList srcs, const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
-               const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
-               const c10::List<optional<Tensor>>& dot_out) {
+std::vector<fedtgan::ColsumJob> colsum_jobs(at::TensorList srcs, const c10::List<optional<Tensor>>& outs,
+                                            const c10::List<optional<Tensor>>& w,
+                                            const c10::List<optional<Tensor>>& dot_v,
+                                            const c10::List<optional<Tensor>>& dot_e,
+                                            const c10::List<optional<Tensor>>& dot_out) {
   const size_t n = srcs.size();
   TORCH_CHECK(n <= 8 && outs.size() == n && w.size() == n && dot_v.size() == n && dot_e.size() == n &&
                   dot_out.size() == n, "colsum_ex: up to 8 jobs, one entry per job in every list");
@@ -317,6 +319,13 @@ void colsum_ex(at::TensorList srcs, const c10::List<optional<Tensor>>& outs, con
     }
     jobs.push_back(j);
   }
+  return jobs;
+}
+
+void colsum_ex(at::TensorList srcs, const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
+               const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
+               const c10::List<optional<Tensor>>& dot_out) {
+  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out);
   fedtgan::launch_colsum(jobs.data(), (int)jobs.size(), cur_stream());
 }
 
@@ -372,6 +381,49 @@ void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, co
   if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
   fedtgan::launch_adam(fp(p), cfp(g), fp(m), fp(v), cfp(step), p.numel(), (float)lr, (float)b1, (float)b2, (float)eps,
                        (float)wd, bump, cur_stream());
+}
+
+// adam + colsum_ex jobs in one launch.  A job whose output lies in g owns ceil4(cols) elements
+// there (16-B aligned start; the flat layout pads every tensor to 4 floats) and gets its Adam
+// update from the reduced sums; outputs elsewhere (metrics) are just written.
+void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& step, double lr,
+             double b1, double b2, double eps, double wd, const optional<Tensor>& rng_bump, at::TensorList srcs,
+             const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
+             const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
+             const c10::List<optional<Tensor>>& dot_out) {
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam_cs: contiguous");
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam_cs: sizes");
+  TORCH_CHECK(p.numel() % 4 == 0, "adam_cs: buffer length must be a multiple of 4");
+  for (const Tensor* t : {&p, &g, &m, &v})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "adam_cs: buffers must be 16-byte aligned");
+  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out);
+  fedtgan::AdamColsum cs{};
+  cs.n_jobs = (int)jobs.size();
+  const float* g0 = cfp(g);
+  const int64_t n = g.numel();
+  for (int k = 0; k < cs.n_jobs; ++k) {
+    cs.jobs[k] = jobs[k];
+    cs.own_lo[k] = cs.own_hi[k] = 0;
+    const int c4 = (jobs[k].cols + 3) / 4 * 4;
+    cs.vec[k] = (reinterpret_cast<uintptr_t>(jobs[k].a) & 15) == 0 && jobs[k].lda % 4 == 0 &&
+                (jobs[k].rows <= 1 || jobs[k].lda >= c4) &&
+                srcs[k].storage().nbytes() >= (size_t)((char*)jobs[k].a - (char*)srcs[k].storage().data()) +
+                    ((size_t)(jobs[k].rows - 1) * jobs[k].lda + c4) * sizeof(float);
+    const float* o = jobs[k].out;
+    if (o && o >= g0 && o < g0 + n) {
+      const int64_t off = o - g0, len = ((int64_t)jobs[k].cols + 3) / 4 * 4;
+      TORCH_CHECK(off % 4 == 0 && off + len <= n, "adam_cs: a job output inside the gradient buffer must start "
+                  "4-aligned and own ceil4(cols) elements");
+      for (int q = 0; q < k; ++q)
+        TORCH_CHECK(off >= cs.own_hi[q] || off + len <= cs.own_lo[q], "adam_cs: overlapping job outputs");
+      cs.own_lo[k] = off;
+      cs.own_hi[k] = off + len;
+    }
+  }
+  uint64_t* bump = nullptr;
+  if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
+  fedtgan::launch_adam_colsum(fp(p), cfp(g), fp(m), fp(v), cfp(step), p.numel(), (float)lr, (float)b1, (float)b2,
+                              (float)eps, (float)wd, bump, cs, cur_stream());
 }
 
 void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, const Tensor& start,
@@ -581,6 +633,10 @@ TORCH_LIBRARY(fedtgan, m) {
       "adam(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, "
       "float wd, Tensor(d!)? rng_bump) -> ()");
   m.def(
+      "adam_cs(Tensor(a!) p, Tensor(e!) g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, "
+      "float eps, float wd, Tensor(d!)? rng_bump, Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, "
+      "Tensor?[] dot_e, Tensor?[] dot_out) -> ()");
+  m.def(
       "sample_decode(Tensor logits, Tensor(a!) out, Tensor kind, Tensor start, Tensor width, Tensor cont, "
       "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def("rng_bump(Tensor(a!) ctr) -> ()");
@@ -612,6 +668,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("bn_relu_train", &bn_relu_train);
   m.impl("bn_relu_bwd", &bn_relu_bwd);
   m.impl("adam", &adam);
+  m.impl("adam_cs", &adam_cs);
   m.impl("sample_decode", &sample_decode);
   m.impl("rng_bump", &rng_bump);
   m.impl("vgm_encode", &vgm_encode);

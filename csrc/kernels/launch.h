@@ -134,6 +134,21 @@ struct ColsumJob {
 };
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
+// Adam over a flat buffer with up to 8 column-sum jobs folded into the same launch; a job whose
+// output lies in the gradient buffer owns [own_lo, own_hi) (elements, 4-aligned) and the Adam
+// update of those elements is applied from the freshly reduced sums.
+constexpr int ACS_COLS = 16, ACS_GROUPS = 64;
+struct AdamColsum {
+  ColsumJob jobs[8];
+  int n_jobs;
+  int vec[8];         // rows 16-B aligned and padded to >= ceil4(cols): float4 loads
+  int blk_start[9];   // filled by the launcher
+  int64_t own_lo[8], own_hi[8];
+};
+void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
+                        float b2, float eps, float wd, uint64_t* rng_ctr_bump, const AdamColsum& cs,
+                        hipStream_t stream);
+
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)

@@ -537,17 +537,29 @@ class CTGANEngine:
                    group=2 if pair else 0)
             inp = self.dl[i][I]
             prev = self.dl[i]
-        fr = self.rows_fr
-        # bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN loss value, one launch.
-        # (dl[L-1][I] holds R_{L-1} by now: coef = 1 there gives dpen/dv; wloss = 0 there.)
-        src, out, w, dot = self._wgan_job(allr, self.wloss3, self.metrics[0:1])
-        o.colsum_many([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src, self.pen_rows.view(-1, 1)],
-                      [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out, self.metrics[1:2]],
-                      weights=[None] * L + [self.coef3, w, None], dots=[None] * (L + 1) + [dot, None])
+        # (the column sums are folded into the Adam launch: those workgroups update the bias / head
+        # entries themselves)
+        jobs = self._d_colsum_jobs()
         self._join(1, 2)
         # d(loss)/d(e_out) = sum of the +-1/n_packs seeds = 0 (stays zero from allocation)
         b1, b2 = self.cfg.betas
-        o.adam(self.flatD, self.gradD, self.mD, self.vD, self.stepD, self.cfg.lr, b1, b2, self.cfg.adam_eps, 0.0)
+        o.adam(self.flatD, self.gradD, self.mD, self.vD, self.stepD, self.cfg.lr, b1, b2, self.cfg.adam_eps, 0.0,
+               jobs=jobs)
+
+    def _d_colsum_jobs(self):
+        """Bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN and penalty values.
+        (dl[L-1][I] holds R_{L-1} by then: coef = 1 there gives dpen/dv; wloss = 0 there.)"""
+        L, fr = len(self.ddims), self.rows_fr
+        src, out, w, dot = self._wgan_job(slice(0, 3 * self.nP), self.wloss3, self.metrics[0:1])
+        return ([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src, self.pen_rows.view(-1, 1)],
+                [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out, self.metrics[1:2]],
+                [None] * L + [self.coef3, w, None], [None] * (L + 1) + [dot, None])
+
+    def _g_colsum_jobs(self):
+        """G.out bias grad + the G-phase WGAN value (-mean D(fake)) + the cond CE sum."""
+        src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
+        return ([self.dlogits, src, self.ce_rows.view(-1, 1)], [self.g["G.out.b"], out, self.metrics[3:4]],
+                [None, w, None], [None, dot, None])
 
     def _g_step(self):
         self._g_prepare()
@@ -562,8 +574,7 @@ class CTGANEngine:
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
         self._g_dlogits()
-        self._g_backward()
-        self._g_adam()
+        self._g_adam(self._g_backward(fold_colsum=True))
 
     def _g_dlogits(self):
         """G loss (-mean D(fake) + cond CE) back to the generator's logits: self.dlogits."""
@@ -577,8 +588,10 @@ class CTGANEngine:
         o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
                      self.opt, self.dlogits, self.ce_rows, self.cfg.tau)
 
-    def _g_backward(self):
-        """self.dlogits -> G parameter gradients (self.gradG), through the saved forward buffers."""
+    def _g_backward(self, fold_colsum: bool = False):
+        """self.dlogits -> G parameter gradients (self.gradG), through the saved forward buffers.
+        fold_colsum: return the G.out bias / metrics column-sum jobs for the Adam launch instead of
+        launching them (the gradient is then complete only after _g_adam(jobs))."""
         o = self.ops
         # generator backward: the dH chain on the main lane, weight gradients on side lanes
         Lg = len(self.gdims)
@@ -589,10 +602,9 @@ class CTGANEngine:
             o.gemm(self.dlogits, x, dW, ta=True, group=1 if pair else 0)
             if pair:
                 o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top], group=2)
-            # G.out bias grad + the G-phase WGAN value (-mean D(fake)) + the cond CE sum in one launch
-            src, out, w, dot = self._wgan_job(slice(0, self.nP), self.coefg, self.metrics[2:3])
-            o.colsum_many([self.dlogits, src, self.ce_rows.view(-1, 1)], [self.g["G.out.b"], out, self.metrics[3:4]],
-                          weights=[None, w, None], dots=[None, dot, None])
+            jobs = self._g_colsum_jobs()
+            if not fold_colsum:
+                o.colsum_many(*jobs)
         if Lg and not pair:
             o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
         for i in range(Lg - 1, -1, -1):
@@ -611,11 +623,12 @@ class CTGANEngine:
                 x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
                 o.gemm(self.da[i], x, dW, ta=True)
         self._join(1, 2, 3)
+        return jobs if fold_colsum else None
 
-    def _g_adam(self):
+    def _g_adam(self, jobs=None):
         b1, b2 = self.cfg.betas
         self.ops.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
-                      self.cfg.l2scale, last_in_step=True)
+                      self.cfg.l2scale, last_in_step=True, jobs=jobs)
 
     # ================================================================= split roles (MD-GAN)
     G_BUFFERS = ("H", "abuf", "nhat", "bn_mean", "bn_invstd", "da", "logits", "dlogits", "dH")

@@ -239,9 +239,20 @@ class HipOps:
         self.L.colsum(list(srcs), list(outs))
 
     # ------------------------------------------------------------------ optimizer
-    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False):
-        self.L.adam(p, g, m, v, step, float(lr), float(b1), float(b2), float(eps), float(wd),
-                    self.ctr if last_in_step else None)
+    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False, jobs=None):
+        """Adam over a flat buffer.  jobs = (srcs, outs, weights, dots) as for colsum_many: the column
+        sums run in the same launch, and outputs inside g get their Adam update from the sums."""
+        bump = self.ctr if last_in_step else None
+        if jobs is None:
+            self.L.adam(p, g, m, v, step, float(lr), float(b1), float(b2), float(eps), float(wd), bump)
+            return
+        srcs, outs, weights, dots = jobs
+        n = len(srcs)
+        weights = weights or [None] * n
+        dots = dots or [None] * n
+        self.L.adam_cs(p, g, m, v, step, float(lr), float(b1), float(b2), float(eps), float(wd), bump, list(srcs),
+                       list(outs), list(weights), [d[0] if d else None for d in dots],
+                       [d[1] if d else None for d in dots], [d[2] if d else None for d in dots])
 
     # ------------------------------------------------------------------ generation decode
     def _decode_tables(self, tabs):

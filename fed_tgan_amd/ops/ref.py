@@ -261,8 +261,11 @@ class TorchOps:
                 loss.add_((s * v.view(-1)).sum() + e.view(-1)[0] * wsum)
 
     # ------------------------------------------------------------------ optimizer
-    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False):
-        """torch.optim.Adam (L2 weight decay added to the gradient, not AdamW); step is a device counter."""
+    def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False, jobs=None):
+        """torch.optim.Adam (L2 weight decay added to the gradient, not AdamW); step is a device counter.
+        jobs: colsum_many arguments computed first (the HIP backend folds them into the launch)."""
+        if jobs is not None:
+            self.colsum_many(*jobs)
         step.add_(1)
         if wd != 0.0:
             g = g + wd * p

@@ -556,3 +556,43 @@ def test_gemm_pair_launch_matches_two_launches(hip, case):
     torch.cuda.synchronize()
     for j, r in zip(jobs, refs):
         assert torch.allclose(j["c"], r, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("aux", [0, 16])
+def test_adam_with_folded_colsum_matches_two_launches(hip, aux):
+    """adam(jobs=...) == colsum_many + adam: bias sums written into the gradient buffer (a 325-wide
+    one with padding, 4-aligned), a weighted dot job into a metric, a sum outside the buffer."""
+    n = 4 * 5000
+    p0, g0 = mat(n, seed=90), mat(n, seed=91)
+    src1, src2, src3 = mat(500, 328, seed=92)[:, :325], mat(150, 256, seed=93), mat(150, 325, seed=94)[:, :256]
+    src0 = mat(77, 37, seed=99)     # unaligned rows: the scalar-load path
+    w3, dv, de = mat(150, seed=95), mat(256, seed=96), mat(1, seed=97)
+    rows = mat(50, 1, seed=98)
+    step = torch.full((1,), 3.0, device=DEV)
+    res = []
+    for fused in (False, True):
+        p, g = p0.clone(), g0.clone()
+        g[1000:1004] = 0.0
+        g[1000 + 325:1000 + 328] = 0.0     # ceil4 padding of the 325-wide output
+        g[8037:8040] = 0.0
+        m, v = torch.full_like(p, 0.01), torch.full_like(p, 0.02)
+        met = torch.zeros(4, device=DEV)
+        jobs = ([src1, src2, src3, rows, src0], [g[1000:1325], g[4096:4352], None, met[1:2], g[8000:8037]],
+                [None, None, w3, None, None], [None, None, (dv, de, met[0:1]), None, None])
+        prev = torch.ops.fedtgan.set_tuning("adam_store", aux)
+        try:
+            if fused:
+                hip.adam(p, g, m, v, step, 2e-4, 0.5, 0.9, 1e-8, 1e-6, jobs=jobs)
+            else:
+                hip.colsum_many(*jobs)
+                hip.adam(p, g, m, v, step, 2e-4, 0.5, 0.9, 1e-8, 1e-6)
+        finally:
+            torch.ops.fedtgan.set_tuning("adam_store", prev)
+        torch.cuda.synchronize()
+        res.append((p, g, m, v, met))
+    # (column sums in a different order: the gradient sums agree to fp32 rounding)
+    for name, a, b, tol in zip("pgmvM", *res, (1e-6, 1e-4, 1e-6, 1e-6, 1e-3)):
+        err = (a - b).abs().max().item()
+        assert torch.allclose(a, b, atol=tol, rtol=1e-5), (name, err)
+    assert torch.allclose(res[1][1][1000:1325], src1.sum(0), atol=1e-4, rtol=1e-5)
+    assert torch.allclose(res[1][1][8000:8037], src0.sum(0), atol=1e-4, rtol=1e-5)

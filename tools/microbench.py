@@ -91,6 +91,7 @@ def main():
     ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
     ap.add_argument("--adam-sweep", action="store_true", help="Adam store policy: plain / nt / sc1")
     ap.add_argument("--store-sweep", action="store_true", help="GEMM output stores: plain / write-through")
+    ap.add_argument("--fold-sweep", action="store_true", help="column sums: own launch / folded into Adam")
     ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
@@ -150,6 +151,19 @@ def main():
             prev = torch.ops.fedtgan.set_tuning("gemm_pairs", pr)
             print(f"gemm_pairs={pr}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
             torch.ops.fedtgan.set_tuning("gemm_pairs", prev)
+        return
+    if args.fold_sweep:
+        for rep in range(2):
+            for tag, fl, p_, g_, m_, v_, st, wd, jobs in (
+                    ("D", eng.flatD, eng.flatD, eng.gradD, eng.mD, eng.vD, eng.stepD, 0.0, eng._d_colsum_jobs()),
+                    ("G", eng.flatG, eng.flatG, eng.gradG, eng.mG, eng.vG, eng.stepG, 1e-6, eng._g_colsum_jobs())):
+                t_cs = per_call(lambda: o.colsum_many(*jobs), dev)
+                t_ad = per_call(lambda: o.adam(p_, g_, m_, v_, st, 2e-4, 0.5, 0.9, 1e-8, wd), dev)
+                t_two = per_call(lambda: (o.colsum_many(*jobs), o.adam(p_, g_, m_, v_, st, 2e-4, 0.5, 0.9, 1e-8, wd)),
+                                 dev)
+                t_f = per_call(lambda: o.adam(p_, g_, m_, v_, st, 2e-4, 0.5, 0.9, 1e-8, wd, jobs=jobs), dev)
+                print(f"{tag}: colsum {t_cs:6.2f}  adam {t_ad:6.2f}  colsum+adam {t_two:6.2f}  folded {t_f:6.2f} us",
+                      flush=True)
         return
     if args.store_sweep:
         for wt in (0, 1, 0, 1):
