@@ -293,15 +293,17 @@ std::vector<fedtgan::ColsumJob> colsum_jobs(at::TensorList srcs, const c10::List
                                             const c10::List<optional<Tensor>>& w,
                                             const c10::List<optional<Tensor>>& dot_v,
                                             const c10::List<optional<Tensor>>& dot_e,
-                                            const c10::List<optional<Tensor>>& dot_out) {
+                                            const c10::List<optional<Tensor>>& dot_out,
+                                            const c10::List<optional<Tensor>>& dot_w) {
   const size_t n = srcs.size();
   TORCH_CHECK(n <= 8 && outs.size() == n && w.size() == n && dot_v.size() == n && dot_e.size() == n &&
-                  dot_out.size() == n, "colsum_ex: up to 8 jobs, one entry per job in every list");
+                  dot_out.size() == n && dot_w.size() == n, "colsum_ex: up to 8 jobs, one entry per job in every list");
   std::vector<fedtgan::ColsumJob> jobs;
   for (size_t i = 0; i < n; ++i) {
     check_f32_2d(srcs[i], "colsum src");
     const int64_t rows = srcs[i].size(0), cols = srcs[i].size(1);
-    fedtgan::ColsumJob j{cfp(srcs[i]), ld_of(srcs[i]), (int)rows, (int)cols, nullptr, nullptr, nullptr, nullptr, nullptr};
+    fedtgan::ColsumJob j{cfp(srcs[i]), ld_of(srcs[i]), (int)rows, (int)cols, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         nullptr};
     const optional<Tensor> o = outs[i], wi = w[i], dv = dot_v[i], de = dot_e[i], dout = dot_out[i];
     if (o.has_value() && o->defined()) {
       TORCH_CHECK(o->numel() == cols && o->is_contiguous(), "colsum_ex: out");
@@ -316,6 +318,11 @@ std::vector<fedtgan::ColsumJob> colsum_jobs(at::TensorList srcs, const c10::List
       j.dot_v = cfp(*dv);
       j.dot_out = fp(*dout);
       if (de.has_value() && de->defined()) j.dot_e = cfp(*de);
+      const optional<Tensor> dw = dot_w[i];
+      if (dw.has_value() && dw->defined()) {
+        TORCH_CHECK(dw->numel() == rows && dw->is_contiguous(), "colsum_ex: dot row weights");
+        j.dot_w = cfp(*dw);
+      }
     }
     jobs.push_back(j);
   }
@@ -324,8 +331,8 @@ std::vector<fedtgan::ColsumJob> colsum_jobs(at::TensorList srcs, const c10::List
 
 void colsum_ex(at::TensorList srcs, const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
                const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
-               const c10::List<optional<Tensor>>& dot_out) {
-  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out);
+               const c10::List<optional<Tensor>>& dot_out, const c10::List<optional<Tensor>>& dot_w) {
+  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out, dot_w);
   fedtgan::launch_colsum(jobs.data(), (int)jobs.size(), cur_stream());
 }
 
@@ -390,13 +397,13 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
              double b1, double b2, double eps, double wd, const optional<Tensor>& rng_bump, at::TensorList srcs,
              const c10::List<optional<Tensor>>& outs, const c10::List<optional<Tensor>>& w,
              const c10::List<optional<Tensor>>& dot_v, const c10::List<optional<Tensor>>& dot_e,
-             const c10::List<optional<Tensor>>& dot_out) {
+             const c10::List<optional<Tensor>>& dot_out, const c10::List<optional<Tensor>>& dot_w) {
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam_cs: contiguous");
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam_cs: sizes");
   TORCH_CHECK(p.numel() % 4 == 0, "adam_cs: buffer length must be a multiple of 4");
   for (const Tensor* t : {&p, &g, &m, &v})
     TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "adam_cs: buffers must be 16-byte aligned");
-  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out);
+  const auto jobs = colsum_jobs(srcs, outs, w, dot_v, dot_e, dot_out, dot_w);
   fedtgan::AdamColsum cs{};
   cs.n_jobs = (int)jobs.size();
   const float* g0 = cfp(g);
@@ -419,6 +426,13 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
       cs.own_lo[k] = off;
       cs.own_hi[k] = off + len;
     }
+    // a dot over parameters this launch updates must be this job's own (read pre-update by
+    // the updating lane); any other overlap with p would race with the update
+    const float* p0 = cfp(p);
+    const float* dv = jobs[k].dot_v;
+    cs.dot_self[k] = dv && cs.own_hi[k] > cs.own_lo[k] && dv == p0 + cs.own_lo[k];
+    TORCH_CHECK(!dv || cs.dot_self[k] || dv + jobs[k].cols <= p0 || dv >= p0 + n,
+                "adam_cs: a dot over parameters updated by this launch must belong to the same job");
   }
   uint64_t* bump = nullptr;
   if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
@@ -565,6 +579,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_bn_cols = (int)value;
     return prev;
   }
+  if (key == "act_row_mode") {
+    TORCH_CHECK(value == 0 || value == 1, "act_row_mode: 0 or 1");
+    const int prev = fedtgan::g_act_row_mode;
+    fedtgan::g_act_row_mode = (int)value;
+    return prev;
+  }
   if (key == "adam_store") {
     TORCH_CHECK(value == 0 || value == 2 || value == 16, "adam_store: 0 plain, 2 nt, 16 sc1");
     const int64_t prev = fedtgan::g_adam_store;
@@ -622,7 +642,9 @@ TORCH_LIBRARY(fedtgan, m) {
       "d_head(Tensor d, Tensor ms, Tensor v, Tensor e, Tensor coef, Tensor wloss, Tensor(a!) y, Tensor(b!) a, "
       "Tensor(c!) loss) -> ()");
   m.def("colsum(Tensor[] srcs, Tensor(a!)[] outs) -> ()");
-  m.def("colsum_ex(Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, Tensor?[] dot_e, Tensor?[] dot_out) -> ()");
+  m.def(
+      "colsum_ex(Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, Tensor?[] dot_e, Tensor?[] dot_out, "
+      "Tensor?[] dot_w) -> ()");
   m.def(
       "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
       "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
@@ -635,7 +657,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "adam_cs(Tensor(a!) p, Tensor(e!) g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, "
       "float eps, float wd, Tensor(d!)? rng_bump, Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, "
-      "Tensor?[] dot_e, Tensor?[] dot_out) -> ()");
+      "Tensor?[] dot_e, Tensor?[] dot_out, Tensor?[] dot_w) -> ()");
   m.def(
       "sample_decode(Tensor logits, Tensor(a!) out, Tensor kind, Tensor start, Tensor width, Tensor cont, "
       "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");

@@ -185,6 +185,7 @@ __device__ __forceinline__ void slerp_weights(float saa, float sbb, float sab, f
   }
 }
 
+int g_act_row_mode = 1;   // wide rows: one 512-thread workgroup per row (set_tuning("act_row_mode"))
 constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
 constexpr int ACT_PF = 8;      // logits prefetched per lane (rows up to 512 wide)
 constexpr int ACT_PFS = 12;    // slerp real-row values prefetched per lane (rows up to 768 wide)
@@ -376,6 +377,239 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
   }
 }
 
+// ---- wide rows (data_dim > ACT_PF * 64): one 512-thread workgroup per row.  The span tables
+// are staged once per row instead of once per 1-2 rows, 8 waves share the row's span statistics
+// (the same LDS atomics, workgroup barriers instead of wave syncs), and the grid has one
+// workgroup per row.  Wave w takes groups of 4 consecutive 64-column blocks (4w, 4w+1, ..),
+// striding by 32 blocks, so every element draws the same Philox word as in the narrow kernel
+// (counter (row, block / 4, lane), component block % 4): the two kernels are interchangeable.
+constexpr int ROW_WAVES = 8;
+
+__device__ __forceinline__ float3 block_sum3(float a, float b, float c, float* sh) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[3 * wv] = a;
+    sh[3 * wv + 1] = b;
+    sh[3 * wv + 2] = c;
+  }
+  __syncthreads();
+  float3 r = make_float3(0.f, 0.f, 0.f);
+#pragma unroll
+  for (int w = 0; w < ROW_WAVES; ++w) {
+    r.x += sh[3 * w];
+    r.y += sh[3 * w + 1];
+    r.z += sh[3 * w + 2];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const float* __restrict__ logits, int ldl,
+                                                                      float* __restrict__ out, int ldo, int rows,
+                                                                      SpanTables sp, float inv_tau, uint64_t seed,
+                                                                      const uint64_t* ctr, uint32_t stream_id,
+                                                                      SlerpFuse sl) {
+  // LDS holds only the row image and the span statistics; the element -> span map (the first D
+  // words of the packed table, shared by every row and L2-resident) is read next to the logits
+  extern __shared__ float act_smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = blockIdx.x;
+  const int D = sp.dim, S = sp.n_span;
+  const float* x = logits + (size_t)r * ldl;
+  const int* einfo = sp.packed;
+  float* v = act_smem;
+  uint32_t* smax = reinterpret_cast<uint32_t*>(v + D);
+  float* ssum = v + D + S;
+  float* red = v + D + 2 * S;   // [ROW_WAVES * 3] slerp partial sums
+  float* y = out + (size_t)r * ldo;
+  const uint64_t step = ctr ? *ctr : 0ull;
+  RngArgs rng{seed, ctr, stream_id};
+  const uint64_t base = (uint64_t)r << 20;
+  for (int s2 = tid; s2 < S; s2 += blockDim.x) {
+    smax[s2] = 0u;
+    ssum[s2] = 0.f;
+  }
+  __syncthreads();
+  const int NB = (D + 63) / 64;
+  for (int g0 = 4 * wv; g0 < NB; g0 += 4 * ROW_WAVES) {
+    float xc[4];
+    int ic[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = min((g0 + q) * 64 + lane, D - 1);
+      xc[q] = x[j];
+      ic[q] = einfo[j];
+    }
+    const uint4 u4 = rng4(rng, step, base + (uint64_t)(g0 >> 2) * 64u + (uint64_t)lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (g0 + q) * 64 + lane;
+      if (j >= D) break;
+      const uint32_t u = q == 0 ? u4.x : q == 1 ? u4.y : q == 2 ? u4.z : u4.w;
+      if (!(ic[q] & EI_SOFTMAX)) {
+        const float th = tanhf(xc[q]);
+        y[j] = th;
+        v[j] = th;
+      } else {
+        const float gv = (xc[q] + gumbel(u)) * inv_tau;
+        v[j] = gv;
+        atomicMax(&smax[ic[q] & (EI_SOFTMAX - 1)], f2ord(gv));
+      }
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < D; j += blockDim.x) {
+    const int info = einfo[j];
+    if (info & EI_SOFTMAX) {
+      const int s2 = info & (EI_SOFTMAX - 1);
+      const float e = __expf(v[j] - ord2f(smax[s2]));
+      v[j] = e;
+      atomicAdd(&ssum[s2], e);
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < D; j += blockDim.x) {
+    const int info = einfo[j];
+    if (info & EI_SOFTMAX) {
+      const float o = v[j] / ssum[info & (EI_SOFTMAX - 1)];
+      y[j] = o;
+      v[j] = o;
+    }
+  }
+  if (sl.real == nullptr || r >= sl.rows) return;   // (uniform over the workgroup)
+  __syncthreads();   // every element of the row image (tanh and softmax) is final
+  const float* a = sl.real + (size_t)r * sl.ld;
+  float saa = 0.f, sbb = 0.f, sab = 0.f;
+  for (int j = tid; j < sl.cols; j += blockDim.x) {
+    const float ra = a[j], fb = j < D ? v[j] : y[j];
+    saa += ra * ra;
+    sbb += fb * fb;
+    sab += ra * fb;
+  }
+  const float3 tot = block_sum3(saa, sbb, sab, red);
+  RngArgs srng{seed, ctr, sl.stream};
+  const float alpha = u01(rng4(srng, step, (uint64_t)r).x);
+  float wa, wb;
+  slerp_weights(tot.x, tot.y, tot.z, alpha, wa, wb);
+  float* o = sl.out + (size_t)r * sl.ld;
+  for (int j = tid; j < sl.cols; j += blockDim.x) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
+}
+
+__global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const float* __restrict__ dact, int ldd,
+                                                                        const float* __restrict__ act, int lda,
+                                                                        const float* __restrict__ logits, int ldl,
+                                                                        SpanTables sp, const int* __restrict__ col,
+                                                                        const int* __restrict__ opt,
+                                                                        float* __restrict__ dl, int ldg, int rows,
+                                                                        float inv_tau, float* loss, int loss_per_row) {
+  extern __shared__ float act_smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = blockIdx.x;
+  const int D = sp.dim, S = sp.n_span;
+  const float* g = dact + (size_t)r * ldd;
+  const float* y = act + (size_t)r * lda;
+  const float* x = logits + (size_t)r * ldl;
+  const int cr = col[r];
+  const int orow = opt[r];
+  const ActSmem t = act_stage_tables(sp, act_smem);
+  float* xs = t.rows;                                       // [D] the row's logits
+  float* stat = xs + D;                                     // [S] per-span sum of g*y
+  int* cspan = reinterpret_cast<int*>(stat + S);            // the conditioned span
+  float* lse_sh = stat + S + 1;
+  float* d = dl + (size_t)r * ldg;
+  for (int s2 = tid; s2 < S; s2 += blockDim.x) stat[s2] = 0.f;
+  if (tid == 0) *cspan = -1;
+  __syncthreads();
+  for (int s2 = tid; s2 < S; s2 += blockDim.x)
+    if (t.kind[s2] != 0 && t.cidx[s2] == cr) *cspan = s2;   // exactly one span matches
+  constexpr int U = 4;   // loads in flight per thread
+  for (int c0 = 0; c0 < D; c0 += U * ROW_WAVES * 64) {
+    float gc[U], yc[U], xc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(c0 + u * ROW_WAVES * 64 + tid, D - 1);
+      gc[u] = g[j];
+      yc[u] = y[j];
+      xc[u] = x[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = c0 + u * ROW_WAVES * 64 + tid;
+      if (j < D) {
+        const int info = t.einfo[j];
+        xs[j] = xc[u];
+        if (info & EI_SOFTMAX) atomicAdd(&stat[info & (EI_SOFTMAX - 1)], gc[u] * yc[u]);
+      }
+    }
+  }
+  __syncthreads();
+  const int cs = *cspan;
+  int cst = 0, cw = 0;
+  if (cs >= 0) {
+    cst = t.start[cs];
+    cw = t.width[cs];
+  }
+  if (wv == 0) {   // log-sum-exp over the conditioned span (one wave)
+    float lse = 0.f;
+    if (cs >= 0) {
+      float m = -INFINITY;
+      for (int i = lane; i < cw; i += 64) m = fmaxf(m, xs[cst + i]);
+      m = wave_max(m);
+      float sm = 0.f;
+      for (int i = lane; i < cw; i += 64) sm += __expf(xs[cst + i] - m);
+      sm = wave_sum(sm);
+      lse = m + __logf(sm);
+      if (lane == 0) {
+        const float term = (lse - xs[cst + min(orow, cw - 1)]) / (float)rows;
+        if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+      }
+    } else if (lane == 0 && loss_per_row) {
+      loss[r] = 0.f;
+    }
+    if (lane == 0) *lse_sh = lse;
+  }
+  __syncthreads();
+  const float lse = *lse_sh;
+  const int ot = cst + min(orow, max(cw - 1, 0));
+  const float invB = 1.f / (float)rows;
+  for (int c0 = 0; c0 < D; c0 += U * ROW_WAVES * 64) {
+    float gc[U], yc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(c0 + u * ROW_WAVES * 64 + tid, D - 1);
+      gc[u] = g[j];
+      yc[u] = y[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = c0 + u * ROW_WAVES * 64 + tid;
+      if (j < D) {
+        const int info = t.einfo[j];
+        float vv;
+        if (!(info & EI_SOFTMAX)) {
+          vv = gc[u] * (1.f - yc[u] * yc[u]);
+        } else {
+          vv = yc[u] * (gc[u] - stat[info & (EI_SOFTMAX - 1)]) * inv_tau;
+          if (j >= cst && j < cst + cw) vv += (__expf(xs[j] - lse) - (j == ot ? 1.f : 0.f)) * invB;
+        }
+        d[j] = vv;
+      }
+    }
+  }
+}
+
+// LDS of the row kernels: tables + one row image [D + 2S] + ROW_WAVES * 3 reduction slots
+static size_t act_row_smem_bytes(const SpanTables& sp) {
+  return (size_t)span_packed_len(sp.dim, sp.n_span) * sizeof(int) +
+         (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
+}
+static size_t act_row_fwd_smem_bytes(const SpanTables& sp) {   // activate_row_kernel: no staged tables
+  return (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
+}
+static bool act_row_mode(const SpanTables& sp) { return sp.dim > ACT_PF * 64 && g_act_row_mode; }
+
 static size_t act_smem_bytes(const SpanTables& sp, int waves) {
   return (size_t)span_packed_len(sp.dim, sp.n_span) * sizeof(int) +
          (size_t)waves * (sp.dim + 2 * sp.n_span) * sizeof(float);
@@ -399,6 +633,13 @@ static void allow_big_lds(K kernel, size_t bytes) {
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, SlerpFuse sl, hipStream_t stream) {
   if (rows == 0) return;
+  if (act_row_mode(sp)) {
+    const size_t lds = act_row_fwd_smem_bytes(sp);
+    allow_big_lds(activate_row_kernel, lds);
+    hipLaunchKernelGGL(activate_row_kernel, dim3(rows), dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out, ldo, rows,
+                       sp, 1.f / tau, seed, ctr, stream_id, sl);
+    return;
+  }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(activate_kernel, lds);
@@ -537,6 +778,13 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
                        int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
+  if (act_row_mode(sp)) {
+    const size_t lds = act_row_smem_bytes(sp);
+    allow_big_lds(act_bwd_ce_row_kernel, lds);
+    hipLaunchKernelGGL(act_bwd_ce_row_kernel, dim3(rows), dim3(ROW_WAVES * 64), lds, stream, dact, ldd, act, lda,
+                       logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row);
+    return;
+  }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(act_bwd_ce_kernel, lds);
@@ -544,7 +792,9 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
                      1.f / tau, loss, loss_per_row);
 }
 
-size_t activation_smem_bytes(const SpanTables& sp) { return act_smem_bytes(sp, act_waves(sp)); }
+size_t activation_smem_bytes(const SpanTables& sp) {
+  return act_row_mode(sp) ? act_row_smem_bytes(sp) : act_smem_bytes(sp, act_waves(sp));
+}
 
 // ============================================================================ gradient penalty pieces
 // one wave per row
@@ -728,26 +978,35 @@ struct ColsumBatch {
 };
 
 __global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch bt) {
-  __shared__ float part[CS_GROUPS][CS_COLS + 1];
+  __shared__ float part[2][CS_GROUPS][CS_COLS + 1];
   const ColsumJob jb = bt.jobs[blockIdx.y];
   const int c = blockIdx.x * CS_COLS + (threadIdx.x % CS_COLS);
   const int grp = threadIdx.x / CS_COLS;
   if ((int)(blockIdx.x * CS_COLS) >= jb.cols) return;
   const int cc = min(c, jb.cols - 1);
-  float s = 0.f;
+  const float* uw = jb.dot_w ? jb.dot_w : jb.w;   // the dot's row weights
+  float s = 0.f, s2 = 0.f;
 #pragma unroll 8
-  for (int r = grp; r < jb.rows; r += CS_GROUPS) s += (jb.w ? jb.w[r] : 1.f) * jb.a[(size_t)r * jb.lda + cc];
-  part[grp][threadIdx.x % CS_COLS] = s;
+  for (int r = grp; r < jb.rows; r += CS_GROUPS) {
+    const float a = jb.a[(size_t)r * jb.lda + cc];
+    s += (jb.w ? jb.w[r] : 1.f) * a;
+    if (jb.dot_w) s2 += jb.dot_w[r] * a;
+  }
+  part[0][grp][threadIdx.x % CS_COLS] = s;
+  part[1][grp][threadIdx.x % CS_COLS] = s2;
   __syncthreads();
   if (grp == 0) {   // one wave: the block's 64 columns
-    float t = 0.f;
-    for (int i = 0; i < CS_GROUPS; ++i) t += part[i][threadIdx.x];
+    float t = 0.f, t2 = 0.f;
+    for (int i = 0; i < CS_GROUPS; ++i) {
+      t += part[0][i][threadIdx.x];
+      t2 += part[1][i][threadIdx.x];
+    }
     if (c < jb.cols && jb.out) jb.out[c] = t;
     if (jb.dot_v) {
-      float d = c < jb.cols ? t * jb.dot_v[c] : 0.f;
-      if (blockIdx.x == 0 && jb.dot_e) {   // + e * sum_r w[r], once per job
+      float d = c < jb.cols ? (jb.dot_w ? t2 : t) * jb.dot_v[c] : 0.f;
+      if (blockIdx.x == 0 && jb.dot_e) {   // + e * sum_r u[r], once per job
         float ws = 0.f;
-        for (int r = threadIdx.x; r < jb.rows; r += 64) ws += jb.w ? jb.w[r] : 1.f;
+        for (int r = threadIdx.x; r < jb.rows; r += 64) ws += uw ? uw[r] : 1.f;
         d += wave_sum(ws) * (threadIdx.x == 0 ? jb.dot_e[0] : 0.f);
       }
       d = wave_sum(d);
@@ -1064,7 +1323,7 @@ __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, con
   const int nb = cs.blk_start[cs.n_jobs];
   if ((int)blockIdx.x < nb) {
     // 4 float4 column quads x 64 row groups; a 500-row job is 8 loads per thread
-    __shared__ float part[ACS_GROUPS][ACS_COLS + 1];
+    __shared__ float part[2][ACS_GROUPS][ACS_COLS + 1];
     int j = 0;
     while (j + 1 < cs.n_jobs && (int)blockIdx.x >= cs.blk_start[j + 1]) ++j;
     const ColsumJob jb = cs.jobs[j];
@@ -1081,49 +1340,76 @@ __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, con
       me = m[e];
       ve = v[e];
     }
-    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool two = jb.dot_w != nullptr;   // a second column sum with the dot's row weights
     if (cs.vec[j]) {   // 16-B aligned rows padded to >= ceil4(cols): whole quads are in bounds
       const int cq = min(c0, ((jb.cols + 3) & ~3) - 4);
 #pragma unroll 4
       for (int r = grp; r < jb.rows; r += ACS_GROUPS) {
         const float wr = jb.w ? jb.w[r] : 1.f;
+        const float ur = two ? jb.dot_w[r] : 0.f;
         const float4 x = *reinterpret_cast<const float4*>(jb.a + (size_t)r * jb.lda + cq);
         s4.x += wr * x.x;
         s4.y += wr * x.y;
         s4.z += wr * x.z;
         s4.w += wr * x.w;
+        d4.x += ur * x.x;
+        d4.y += ur * x.y;
+        d4.z += ur * x.z;
+        d4.w += ur * x.w;
       }
     } else {
       const int last = jb.cols - 1;
       for (int r = grp; r < jb.rows; r += ACS_GROUPS) {
         const float wr = jb.w ? jb.w[r] : 1.f;
+        const float ur = two ? jb.dot_w[r] : 0.f;
         const float* ar = jb.a + (size_t)r * jb.lda;
-        s4.x += wr * ar[min(c0, last)];
-        s4.y += wr * ar[min(c0 + 1, last)];
-        s4.z += wr * ar[min(c0 + 2, last)];
-        s4.w += wr * ar[min(c0 + 3, last)];
+        const float x0 = ar[min(c0, last)], x1 = ar[min(c0 + 1, last)];
+        const float x2 = ar[min(c0 + 2, last)], x3 = ar[min(c0 + 3, last)];
+        s4.x += wr * x0;
+        s4.y += wr * x1;
+        s4.z += wr * x2;
+        s4.w += wr * x3;
+        d4.x += ur * x0;
+        d4.y += ur * x1;
+        d4.z += ur * x2;
+        d4.w += ur * x3;
       }
     }
-    part[grp][qd * 4 + 0] = s4.x;
-    part[grp][qd * 4 + 1] = s4.y;
-    part[grp][qd * 4 + 2] = s4.z;
-    part[grp][qd * 4 + 3] = s4.w;
+    part[0][grp][qd * 4 + 0] = s4.x;
+    part[0][grp][qd * 4 + 1] = s4.y;
+    part[0][grp][qd * 4 + 2] = s4.z;
+    part[0][grp][qd * 4 + 3] = s4.w;
+    part[1][grp][qd * 4 + 0] = d4.x;
+    part[1][grp][qd * 4 + 1] = d4.y;
+    part[1][grp][qd * 4 + 2] = d4.z;
+    part[1][grp][qd * 4 + 3] = d4.w;
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;   // wave 0: lane = column (lane & 15) x quarter of the row groups
-    float tsum = 0.f;
+    float tsum = 0.f, tdot = 0.f;
 #pragma unroll
-    for (int i = 0; i < ACS_GROUPS / 4; ++i) tsum += part[(lane >> 4) * (ACS_GROUPS / 4) + i][lane & 15];
+    for (int i = 0; i < ACS_GROUPS / 4; ++i) {
+      tsum += part[0][(lane >> 4) * (ACS_GROUPS / 4) + i][lane & 15];
+      tdot += part[1][(lane >> 4) * (ACS_GROUPS / 4) + i][lane & 15];
+    }
     tsum += __shfl_xor(tsum, 16);
     tsum += __shfl_xor(tsum, 32);
+    tdot += __shfl_xor(tdot, 16);
+    tdot += __shfl_xor(tdot, 32);
+    if (!two) tdot = tsum;
     const int col = cb * ACS_COLS + lane;
     const bool live = lane < ACS_COLS && col < jb.cols;
     if (live && jb.out) jb.out[col] = tsum;
     if (jb.dot_v) {
-      float d = live ? tsum * jb.dot_v[col] : 0.f;
-      if (cb == 0 && jb.dot_e) {   // + e * sum_r w[r], once per job
+      // a dot over this job's own parameters reads them as they were before this launch (the
+      // prefetched value of the lane that updates them): no other workgroup writes them
+      const float vc = live ? (cs.dot_self[j] ? pe : jb.dot_v[col]) : 0.f;
+      float d = tdot * vc;
+      if (cb == 0 && jb.dot_e) {   // + e * sum_r u[r], once per job
+        const float* uw = two ? jb.dot_w : jb.w;
         float ws = 0.f;
-        for (int r = lane; r < jb.rows; r += 64) ws += jb.w ? jb.w[r] : 1.f;
+        for (int r = lane; r < jb.rows; r += 64) ws += uw ? uw[r] : 1.f;
         d += wave_sum(ws) * (lane == 0 ? jb.dot_e[0] : 0.f);
       }
       d = wave_sum(d);

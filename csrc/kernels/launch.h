@@ -121,8 +121,10 @@ void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const flo
                    hipStream_t stream);
 
 // out[c] = sum_r w[r] a[r, c] (w nullable = 1; out nullable); with dot_v, additionally
-// *dot_out += sum_c dot_v[c] * (that column sum) + dot_e[0] * sum_r w[r]  (the WGAN loss
-// sum_r w[r] (d_r . v + e) of the D head, folded into the bias-gradient launch)
+// *dot_out += sum_c dot_v[c] * (sum_r u[r] a[r, c]) + dot_e[0] * sum_r u[r], u = dot_w (or w
+// when dot_w is null): the WGAN loss sum_r u[r] (d_r . v + e) of the D head, folded into the
+// bias-gradient launch.  With dot_w, one job gives the head's weight gradient (weights w) and
+// the loss (weights dot_w) from one pass over the rows.
 struct ColsumJob {
   const float* a;
   int lda, rows, cols;
@@ -131,6 +133,7 @@ struct ColsumJob {
   const float* dot_v;
   const float* dot_e;
   float* dot_out;
+  const float* dot_w;
 };
 void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream);
 
@@ -144,6 +147,7 @@ struct AdamColsum {
   int vec[8];         // rows 16-B aligned and padded to >= ceil4(cols): float4 loads
   int blk_start[9];   // filled by the launcher
   int64_t own_lo[8], own_hi[8];
+  int dot_self[8];    // dot_v is this job's own output's parameters: use the pre-update values
 };
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
                         float b2, float eps, float wd, uint64_t* rng_ctr_bump, const AdamColsum& cs,
@@ -153,6 +157,7 @@ extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
+extern int g_act_row_mode;   // activation kernels on rows wider than 512: one workgroup per row (1) or per 1-4 rows
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,

@@ -548,12 +548,15 @@ class CTGANEngine:
 
     def _d_colsum_jobs(self):
         """Bias grads + the head's weight grad (sum_r coef[r] d_r) + the WGAN and penalty values.
-        (dl[L-1][I] holds R_{L-1} by then: coef = 1 there gives dpen/dv; wloss = 0 there.)"""
+        (dl[L-1][I] holds R_{L-1} by then: coef = 1 there gives dpen/dv; wloss = 0 there.)
+        The head's gradient and the WGAN value are one job (row weights coef / wloss over the
+        same rows): in the folded Adam launch the WGAN dot then reads each head weight in the
+        lane that updates it, before the update."""
         L, fr = len(self.ddims), self.rows_fr
-        src, out, w, dot = self._wgan_job(slice(0, 3 * self.nP), self.wloss3, self.metrics[0:1])
-        return ([self.A[i][fr] for i in range(L)] + [self.dl[L - 1], src, self.pen_rows.view(-1, 1)],
-                [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), out, self.metrics[1:2]],
-                [None] * L + [self.coef3, w, None], [None] * (L + 1) + [dot, None])
+        src, _, w, dot = self._wgan_job(slice(0, 3 * self.nP), self.wloss3, self.metrics[0:1])
+        return ([self.A[i][fr] for i in range(L)] + [src, self.pen_rows.view(-1, 1)],
+                [self.g[f"D.{i}.b"] for i in range(L)] + [self.g["D.out.W"].view(-1), self.metrics[1:2]],
+                [None] * L + [self.coef3, None], [None] * L + [(*dot, w), None])
 
     def _g_colsum_jobs(self):
         """G.out bias grad + the G-phase WGAN value (-mean D(fake)) + the cond CE sum."""

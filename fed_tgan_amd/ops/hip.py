@@ -33,8 +33,10 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
       * >= 256 64x64 tiles: 64x64, no split (the grid already covers the chip);
       * short K (<= 8 bursts): 32x32 tiles, no split (4x the workgroups, no epilogue) --
         e.g. 500x256x432: 5.5 us vs 7.7 us for 64x64 split 4;
-      * long K: 32x32 tiles split ~512 workgroups deep (one CU pulls only ~60-100 GB/s), at
-        most 2 bursts per split, fp32 slabs capped at ~6 MB.
+      * long K: 32x32 tiles split ~512 workgroups deep (one CU pulls only ~60-100 GB/s), and
+        deeper where that would leave more than ~8 bursts per split (wide tables: D0's K is
+        137,800 -- 83 serial bursts at 13 splits); at least 2 bursts per split, fp32 slabs
+        capped at ~6 MB.  (Every Intrusion shape keeps its measured split.)
     """
     t128 = -(-M // 128) * -(-N // 128)
     t64 = -(-M // 64) * -(-N // 64)
@@ -47,7 +49,8 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
     if bursts <= 8:
         return 32, 1
     cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
-    return 32, int(max(1, min(-(-512 // t32), -(-bursts // 2), cap_ws)))
+    want = max(-(-512 // t32), -(-bursts // 8))
+    return 32, int(max(1, min(want, -(-bursts // 2), cap_ws)))
 
 
 GEMM_MAX_SPLITS = 64   # gemm.hip: the split-K epilogue keeps every slab value in registers
@@ -226,15 +229,20 @@ class HipOps:
             raise NotImplementedError
         self.L.colsum([a], [out])
 
+    @staticmethod
+    def _dot_lists(dots, n):
+        dots = dots or [None] * n
+        return ([d[0] if d else None for d in dots], [d[1] if d else None for d in dots],
+                [d[2] if d else None for d in dots], [d[3] if d and len(d) > 3 else None for d in dots])
+
     def colsum_many(self, srcs, outs, weights=None, dots=None):
-        """out_i = sum_r w_i[r] src_i[r, :] (out_i may be None); dots[i] = (v, e, loss): loss +=
-        sum_r w_i[r] (src_i[r] . v + e) in the same launch (the WGAN term of the D head)."""
+        """out_i = sum_r w_i[r] src_i[r, :] (out_i may be None); dots[i] = (v, e, loss[, u]): loss +=
+        sum_r u[r] (src_i[r] . v + e) in the same launch (the WGAN term of the D head), u = w_i
+        unless given."""
         if weights is not None or dots is not None:
             n = len(srcs)
             weights = weights or [None] * n
-            dots = dots or [None] * n
-            self.L.colsum_ex(list(srcs), list(outs), list(weights), [d[0] if d else None for d in dots],
-                             [d[1] if d else None for d in dots], [d[2] if d else None for d in dots])
+            self.L.colsum_ex(list(srcs), list(outs), list(weights), *self._dot_lists(dots, n))
             return
         self.L.colsum(list(srcs), list(outs))
 
@@ -249,10 +257,8 @@ class HipOps:
         srcs, outs, weights, dots = jobs
         n = len(srcs)
         weights = weights or [None] * n
-        dots = dots or [None] * n
         self.L.adam_cs(p, g, m, v, step, float(lr), float(b1), float(b2), float(eps), float(wd), bump, list(srcs),
-                       list(outs), list(weights), [d[0] if d else None for d in dots],
-                       [d[1] if d else None for d in dots], [d[2] if d else None for d in dots])
+                       list(outs), list(weights), *self._dot_lists(dots, n))
 
     # ------------------------------------------------------------------ generation decode
     def _decode_tables(self, tabs):

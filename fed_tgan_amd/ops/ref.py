@@ -256,9 +256,11 @@ class TorchOps:
             if o is not None:
                 o.copy_(s)
             if d is not None:
-                v, e, loss = d
-                wsum = w.sum() if w is not None else torch.tensor(float(a.shape[0]), device=a.device)
-                loss.add_((s * v.view(-1)).sum() + e.view(-1)[0] * wsum)
+                v, e, loss = d[:3]
+                u = d[3] if len(d) > 3 and d[3] is not None else w
+                su = (a * u.view(-1, 1)).sum(0) if u is not None else a.sum(0)
+                usum = u.sum() if u is not None else torch.tensor(float(a.shape[0]), device=a.device)
+                loss.add_((su * v.view(-1)).sum() + e.view(-1)[0] * usum)
 
     # ------------------------------------------------------------------ optimizer
     def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False, jobs=None):

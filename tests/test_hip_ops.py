@@ -596,3 +596,64 @@ def test_adam_with_folded_colsum_matches_two_launches(hip, aux):
         assert torch.allclose(a, b, atol=tol, rtol=1e-5), (name, err)
     assert torch.allclose(res[1][1][1000:1325], src1.sum(0), atol=1e-4, rtol=1e-5)
     assert torch.allclose(res[1][1][8000:8037], src0.sum(0), atol=1e-4, rtol=1e-5)
+
+
+def test_wide_row_kernels_match_per_wave_kernels(hip):
+    """Rows wider than 512: the one-workgroup-per-row kernels draw the same Philox words as the
+    per-wave kernels, so activation (+ fused slerp) and its backward agree element for element."""
+    spans, cond, D = _wide_spans(D_min=2300, seed=4)
+    rows, nc = 600, 45
+    Din = D + nc
+    logits = mat(rows, D, seed=52) * 2
+    real = mat(rows, Din, seed=53)
+    cond_cols = mat(rows, nc, seed=54)
+    res = []
+    for mode in (0, 1):
+        fake = torch.zeros(rows, Din, device=DEV)
+        fake[:, D:] = cond_cols
+        interp = torch.zeros(rows // 3, Din, device=DEV)
+        prev = torch.ops.fedtgan.set_tuning("act_row_mode", mode)
+        try:
+            hip.activate(logits, fake[:, :D], spans, 0.2, stream_id=2, slerp=(real[:rows // 3], fake, interp, 3))
+            dact = mat(rows, D, seed=55)
+            col = (torch.arange(rows, device=DEV) % len(cond)).to(torch.int32)
+            w = torch.tensor([w for _, w in cond], device=DEV)[col.long()]
+            opt = ((torch.arange(rows, device=DEV) * 7) % w).to(torch.int32)
+            d = torch.zeros_like(logits)
+            loss = torch.zeros(rows, device=DEV)
+            hip.act_bwd_ce(dact, fake[:, :D], logits, spans, cond, col, opt, d, loss, 0.2)
+        finally:
+            torch.ops.fedtgan.set_tuning("act_row_mode", prev)
+        torch.cuda.synchronize()
+        res.append((fake, interp, d, loss))
+    for name, a, b in zip(("act", "slerp", "dlogits", "ce"), *res):
+        err = (a - b).abs().max().item()
+        assert torch.allclose(a, b, atol=2e-5, rtol=1e-4), (name, err)
+
+
+
+def test_adam_folded_dot_over_own_parameters_reads_pre_update_values(hip):
+    """The D head job: gradient (row weights w) and the WGAN value (row weights u) in one job whose
+    dot runs over the very parameters the launch updates -- the value uses the old weights."""
+    n = 4 * 3000
+    p0, g0 = mat(n, seed=100), mat(n, seed=101)
+    src, w, u, e = mat(150, 256, seed=102), mat(150, seed=103), mat(150, seed=104), mat(1, seed=105)
+    step = torch.full((1,), 2.0, device=DEV)
+    res = []
+    for fused in (False, True):
+        p, g = p0.clone(), g0.clone()
+        m, v = torch.full_like(p, 0.01), torch.full_like(p, 0.02)
+        met = torch.zeros(2, device=DEV)
+        jobs = ([src], [g[2048:2304]], [w], [(p[2048:2304], e, met[0:1], u)])
+        if fused:
+            hip.adam(p, g, m, v, step, 2e-4, 0.5, 0.9, 1e-8, 0.0, jobs=jobs)
+        else:
+            hip.colsum_many(*jobs)
+            hip.adam(p, g, m, v, step, 2e-4, 0.5, 0.9, 1e-8, 0.0)
+        torch.cuda.synchronize()
+        res.append((p, g, met))
+    want = (src * u[:, None]).sum(0) @ p0[2048:2304] + e[0] * u.sum()
+    assert torch.allclose(res[1][2][0], want, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(res[0][2][0], want, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(res[1][1][2048:2304], (src * w[:, None]).sum(0), rtol=1e-5, atol=1e-4)
+    assert torch.allclose(res[0][0], res[1][0], atol=1e-6, rtol=1e-5)
