@@ -42,6 +42,11 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int NT = 256;
 
+// largest tile (rows) that keeps two K-bursts in flight (see Cfg::DEPTH)
+#ifndef FEDTGAN_GEMM_DEPTH2_MAX_TM
+#define FEDTGAN_GEMM_DEPTH2_MAX_TM 64
+#endif
+
 // output / split-K slab store: plain, or write-through (sc1) so the kernel boundary finds no dirty
 // L2 lines to write back (MI355X_MICROARCH.md "boundary": + bytes / 6 TB/s)
 __device__ __forceinline__ void st_out(float* base, size_t idx, float v, int wt) {
@@ -220,6 +225,8 @@ struct Cfg {
   static constexpr int LD = F32 ? KC + 1 : KC + 8;            // LDS row stride (elements)
   static constexpr int ESZ = F32 ? 4 : 2;
   static constexpr int STAGE = (TM + TN) * LD * ESZ;          // bytes per stage (A image + B image)
+  // bursts in flight: 2 where the second register slot fits next to the fragments (bf16 path)
+  static constexpr int DEPTH = (!F32 && TM <= FEDTGAN_GEMM_DEPTH2_MAX_TM) ? 2 : 1;
 };
 
 // TM x TN output tile (64x64; 32x32 for short-K GEMMs that would otherwise need split-K; 128x128
@@ -319,13 +326,47 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   // per burst: stage the landed burst into LDS buffer st, issue the next burst, multiply.  One
   // barrier per burst: buffer st was last read two bursts ago, before the previous barrier.
   int st = 0;
-  issue(kb);
-  for (int k0 = kb; k0 < ke; k0 += KC) {
-    stage(st);
-    __syncthreads();
-    if (k0 + KC < ke) issue(k0 + KC);
-    compute(st, min(KC, ke - k0));
-    st ^= 1;
+  if constexpr (C::DEPTH == 2) {
+    // two bursts in flight: register slots 0 / 1 alternate, the loop unrolled by two so each
+    // slot stays a static register set; a burst's loads are issued two bursts ahead of its use,
+    // so a B-burst GEMM costs ~B/2 memory round trips instead of ~B (the compiler's counted
+    // vmcnt waits only for the older slot when staging it)
+    Chunk<KC, !TA, TM> ca2;
+    Chunk<KC, TB, TN> cb2;
+    auto issue2 = [&](int k0) {
+      ca2.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
+      cb2.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
+    };
+    auto stage2 = [&](int s) {
+      unsigned char* base = smem + s * C::STAGE;
+      ca2.store_bf16(reinterpret_cast<uint16_t*>(base));
+      cb2.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
+    };
+    issue(kb);
+    if (kb + KC < ke) issue2(kb + KC);
+    for (int k0 = kb; k0 < ke; k0 += 2 * KC) {
+      stage(st);
+      __syncthreads();
+      if (k0 + 2 * KC < ke) issue(k0 + 2 * KC);
+      compute(st, min(KC, ke - k0));
+      st ^= 1;
+      if (k0 + KC < ke) {
+        stage2(st);
+        __syncthreads();
+        if (k0 + 3 * KC < ke) issue2(k0 + 3 * KC);
+        compute(st, min(KC, ke - k0 - KC));
+        st ^= 1;
+      }
+    }
+  } else {
+    issue(kb);
+    for (int k0 = kb; k0 < ke; k0 += KC) {
+      stage(st);
+      __syncthreads();
+      if (k0 + KC < ke) issue(k0 + KC);
+      compute(st, min(KC, ke - k0));
+      st ^= 1;
+    }
   }
 
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
