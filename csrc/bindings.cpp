@@ -442,7 +442,8 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
 
 void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, const Tensor& start,
                    const Tensor& width, const Tensor& cont, const Tensor& code_off, const Tensor& codes,
-                   const Tensor& mu, const Tensor& sd, int64_t seed, const Tensor& rng_ctr, int64_t stream) {
+                   const Tensor& mu, const Tensor& sd, int64_t seed, const Tensor& rng_ctr, int64_t stream,
+                   const optional<Tensor>& ecol) {
   check_f32_2d(logits, "logits");
   TORCH_CHECK(out.scalar_type() == at::kDouble && out.is_contiguous() && out.dim() == 2, "decode: out f64");
   TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) == kind.numel(), "decode: shapes");
@@ -466,6 +467,13 @@ void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, 
   a.seed = (uint64_t)seed;
   a.rng_ctr = ctr_ptr(rng_ctr);
   a.rng_stream = (uint32_t)stream;
+  a.dim = (int)logits.size(1);
+  if (ecol.has_value() && ecol->defined()) {
+    TORCH_CHECK(ecol->scalar_type() == at::kInt && ecol->is_contiguous() && ecol->numel() == logits.size(1),
+                "decode: ecol must be int32 [data_dim]");
+    // the row kernel keeps one 8-byte maximum per output column and wave in LDS
+    if (a.n_cols * 4 * 8 <= 64 * 1024) a.ecol = ecol->data_ptr<int>();
+  }
   fedtgan::launch_sample_decode(a, cur_stream());
 }
 
@@ -579,6 +587,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_bn_cols = (int)value;
     return prev;
   }
+  if (key == "decode_rows") {
+    TORCH_CHECK(value == 0 || value == 1, "decode_rows: 0 or 1");
+    const int prev = fedtgan::g_decode_rows;
+    fedtgan::g_decode_rows = (int)value;
+    return prev;
+  }
   if (key == "act_row_mode") {
     TORCH_CHECK(value == 0 || value == 1, "act_row_mode: 0 or 1");
     const int prev = fedtgan::g_act_row_mode;
@@ -660,7 +674,8 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor?[] dot_e, Tensor?[] dot_out, Tensor?[] dot_w) -> ()");
   m.def(
       "sample_decode(Tensor logits, Tensor(a!) out, Tensor kind, Tensor start, Tensor width, Tensor cont, "
-      "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream) -> ()");
+      "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream, "
+      "Tensor? ecol=None) -> ()");
   m.def("rng_bump(Tensor(a!) ctr) -> ()");
   m.def(
       "vgm_estep(Tensor x, Tensor n_rows, Tensor consts, Tensor means, Tensor prec, Tensor(a!) partial, "

@@ -1532,9 +1532,77 @@ __global__ __launch_bounds__(256) void sample_decode_kernel(DecodeArgs a) {
   a.out[(size_t)r * a.n_cols + j] = val;
 }
 
+// One wave per row: every lane draws the Gumbel noise of its own logits -- the same Philox word
+// per element as sample_decode_kernel (counter (row << 20) + span offset + the 4-aligned position
+// in the span, component = position % 4) -- and folds (noisy logit, first index) into its
+// column's 64-bit LDS maximum (ds_max_u64: ordered float in the high word, ~index in the low
+// word, so ties keep the first index like the serial scan).  Lanes then decode one column each.
+// The serial kernel walked each span in one thread: a 70-wide categorical was ~18 dependent
+// round trips for one lane of the wave.
+constexpr int DEC_WAVES = 4;
+__global__ __launch_bounds__(DEC_WAVES * 64) void sample_decode_row_kernel(DecodeArgs a) {
+  extern __shared__ unsigned long long dec_best[];   // [DEC_WAVES][n_cols]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * DEC_WAVES + wv;
+  if (r >= a.rows) return;   // (wave-uniform; only wave-level LDS syncs below)
+  unsigned long long* best = dec_best + (size_t)wv * a.n_cols;
+  for (int j = lane; j < a.n_cols; j += 64) best[j] = 0ull;
+  wave_lds_sync();
+  const float* x = a.logits + (size_t)r * a.ldl;
+  const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
+  RngArgs rng{a.seed, a.rng_ctr, a.rng_stream};
+  const uint64_t rbase = (uint64_t)r << 20;
+  constexpr int U = 4;   // elements per lane per round trip
+  for (int p0 = 0; p0 < a.dim; p0 += U * 64) {
+    float xv[U];
+    int jc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = min(p0 + u * 64 + lane, a.dim - 1);
+      xv[u] = x[p];
+      jc[u] = a.ecol[p];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * 64 + lane;
+      const int j = jc[u];
+      if (p >= a.dim || j < 0) continue;
+      const int off = a.start[j] + (a.kind[j] == 0 ? 1 : 0);
+      const int i = p - off;
+      const uint4 rw = rng4(rng, step, rbase + (uint64_t)(off + (i & ~3)));
+      const uint32_t uu = (i & 3) == 0 ? rw.x : (i & 3) == 1 ? rw.y : (i & 3) == 2 ? rw.z : rw.w;
+      const float v = xv[u] + gumbel(uu);
+      atomicMax(&best[j], ((unsigned long long)f2ord(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)i));
+    }
+  }
+  wave_lds_sync();
+  for (int j = lane; j < a.n_cols; j += 64) {
+    const unsigned long long k = best[j];
+    const int bi = k ? (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0;
+    double val;
+    if (a.kind[j] == 0) {
+      double al = (double)tanhf(x[a.start[j]]);
+      al = al < -1.0 ? -1.0 : (al > 1.0 ? 1.0 : al);
+      const int c = a.cont[j];
+      val = al * 4.0 * a.sd[(size_t)c * a.K + bi] + a.mu[(size_t)c * a.K + bi];
+    } else {
+      val = a.codes[a.code_off[j] + bi];
+    }
+    a.out[(size_t)r * a.n_cols + j] = val;
+  }
+}
+
+int g_decode_rows = 1;   // generation decode: one wave per row (1) or one thread per cell (0)
+
 void launch_sample_decode(const DecodeArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.rows * a.n_cols;
   if (n == 0) return;
+  if (g_decode_rows && a.ecol) {
+    const size_t lds = (size_t)DEC_WAVES * a.n_cols * sizeof(unsigned long long);
+    hipLaunchKernelGGL(sample_decode_row_kernel, dim3((unsigned)((a.rows + DEC_WAVES - 1) / DEC_WAVES)),
+                       dim3(DEC_WAVES * 64), lds, stream, a);
+    return;
+  }
   hipLaunchKernelGGL(sample_decode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
 }
 

@@ -158,6 +158,7 @@ extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
 extern int g_act_row_mode;   // activation kernels on rows wider than 512: one workgroup per row (1) or per 1-4 rows
+extern int g_decode_rows;   // generation decode: one wave per row (1) or one thread per (row, column) (0)
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
@@ -186,6 +187,8 @@ struct DecodeArgs {
   uint64_t seed;
   const uint64_t* rng_ctr;
   uint32_t rng_stream;
+  int dim;              // logits per row
+  const int* ecol;      // [dim] element -> output column whose argmax it enters (-1: none, e.g. alpha)
 };
 void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
 

@@ -285,9 +285,23 @@ class HipOps:
             self._dec[key] = t
         return t
 
+    def _decode_ecol(self, tabs, dim: int):
+        """[dim] int32: output column whose Gumbel argmax each logit enters (-1: none, e.g. the
+        tanh unit of a continuous column) -- the one-wave-per-row decode kernel's element map."""
+        key = (id(tabs), int(dim))
+        e = self._dec.get(key)
+        if e is None:
+            ec = np.full(int(dim), -1, dtype=np.int32)
+            for j, (kk, s, w, _, _) in enumerate(tabs["cols"]):
+                o = s + 1 if kk == 0 else s
+                ec[o:o + w] = j
+            e = torch.from_numpy(ec).to(self.device)
+            self._dec[key] = e
+        return e
+
     def sample_decode(self, logits, out, tabs, stream_id=0):
         kind, start, width, cont, code_off, codes, mu, sd = self._decode_tables(tabs)
         self.L.sample_decode(logits, out, kind, start, width, cont, code_off, codes, mu, sd, self.seed, self.ctr,
-                             int(stream_id) * 16)
+                             int(stream_id) * 16, self._decode_ecol(tabs, logits.shape[1]))
         self.L.rng_bump(self.ctr)
         return out

@@ -657,3 +657,29 @@ def test_adam_folded_dot_over_own_parameters_reads_pre_update_values(hip):
     assert torch.allclose(res[0][2][0], want, rtol=1e-4, atol=1e-3)
     assert torch.allclose(res[1][1][2048:2304], (src * w[:, None]).sum(0), rtol=1e-5, atol=1e-4)
     assert torch.allclose(res[0][0], res[1][0], atol=1e-6, rtol=1e-5)
+
+
+def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
+    """One wave per row (LDS 64-bit max per column) draws the same Gumbel noise per logit as the
+    one-thread-per-cell decode, so both give the same table bit for bit."""
+    from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+    from fed_tgan_amd.models.samplers import CondTables
+    tr, X, spans, cond = _spans()
+    eng = CTGANEngine(tr.layout, EngineConfig(), DEV, backend="hip", seed=5)
+    eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+    rows = 1500
+    logits = mat(rows, X.shape[1], seed=120) * 3
+    logits[:7] = 0.0                      # flat spans: the choice is the Gumbel noise alone
+    res = []
+    for mode in (0, 1):
+        out = torch.zeros(rows, len(tr.meta), dtype=torch.float64, device=DEV)
+        ctr0 = eng.ops.ctr.clone()
+        prev = torch.ops.fedtgan.set_tuning("decode_rows", mode)
+        try:
+            eng.ops.sample_decode(logits, out, eng.gen_tables)
+        finally:
+            torch.ops.fedtgan.set_tuning("decode_rows", prev)
+        eng.ops.ctr.copy_(ctr0)           # same counter for both kernels
+        torch.cuda.synchronize()
+        res.append(out)
+    assert torch.equal(res[0], res[1])

@@ -63,6 +63,16 @@ def gen_only(eng, tr, X, dev):
             d2h = (time.perf_counter() - t) / 10 * 1e6
             print(f"generate_decoded(40000) chunk={chunk:6d} graph={graph!s:5}: {us:9.1f} us   "
                   f"(D2H pageable copy {d2h:8.1f} us)", flush=True)
+    # decode kernel alone on one 40000-row chunk: one thread per cell vs one wave per row
+    logits = torch.randn(40000, X.shape[1], device=dev) * 3
+    out = torch.zeros(40000, len(tr.meta), dtype=torch.float64, device=dev)
+    for mode in (0, 1):
+        prev = torch.ops.fedtgan.set_tuning("decode_rows", mode)
+        try:
+            us = per_call(lambda: eng.ops.sample_decode(logits, out, eng.gen_tables), dev, n=20, reps=10)
+        finally:
+            torch.ops.fedtgan.set_tuning("decode_rows", prev)
+        print(f"sample_decode 40000 rows, decode_rows={mode}: {us:9.1f} us", flush=True)
 
 
 def unroll_sweep(eng, dev):
