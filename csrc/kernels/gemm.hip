@@ -507,9 +507,12 @@ static dim3 gemm_prepare(GemmArgs& g) {
   g.wt = g_gemm_store_wt && (int64_t)g.M * g.ldc * 4 < (int64_t)INT32_MAX &&
          (int64_t)g.splitk * g.M * g.N * 4 < (int64_t)INT32_MAX;
   // measured (profiles/README.md): the XCD-contiguous order pays off on long-K tiles (G-out paired
-  // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones
+  // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones;
+  // on 128x128-tile GEMMs over >= 8192 rows (generation) the N tiles of one A row block then share
+  // an L2 whatever K is (generate_decoded(40000): 375 -> 360 us)
   g.xcd_remap = g_gemm_xcd_remap == 2 ||
-                (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768)));
+                (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768) ||
+                                           (T == 128 && tm >= 64)));
   return dim3(tn, tm, g.splitk);
 }
 

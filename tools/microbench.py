@@ -73,6 +73,22 @@ def gen_only(eng, tr, X, dev):
         finally:
             torch.ops.fedtgan.set_tuning("decode_rows", prev)
         print(f"sample_decode 40000 rows, decode_rows={mode}: {us:9.1f} us", flush=True)
+    # whole captured pass vs the GEMM tile order (the 40k-row GEMMs are K = 431 / 687 / 943)
+    eng.cfg.gen_chunk = 40960
+    for remap in (0, 1, 2, 1, 0, 2):
+        prev = torch.ops.fedtgan.set_tuning("gemm_xcd_remap", remap)
+        try:
+            eng._gen_bufs, eng._gen_graphs = None, {}
+            eng.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for _ in range(20):
+                eng.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            us = (time.perf_counter() - t) / 20 * 1e6
+        finally:
+            torch.ops.fedtgan.set_tuning("gemm_xcd_remap", prev)
+        print(f"generate_decoded(40000) graph, gemm_xcd_remap={remap}: {us:9.1f} us", flush=True)
 
 
 def unroll_sweep(eng, dev):
