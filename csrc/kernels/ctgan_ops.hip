@@ -1073,33 +1073,32 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps) {
   constexpr int GROUPS = BN_THREADS / COLS;
-  __shared__ float sh[BN_MAXG * BN_WAVES * COLS];
+  __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
   const int c = blockIdx.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   const int rpg = rows / groups;
+  // One-pass statistics around a per-batch shift (the batch's first row): sum(d) and sum(d^2) of
+  // d = x - shift reduce together, so the workgroup pays ONE cross-wave reduction instead of two
+  // (mean, then centred variance).  The shift keeps E[d^2] - E[d]^2 free of cancellation.
+  const float sh0 = a[cc], sh1 = a[(size_t)min(rpg, rows - 1) * lda + cc];
   float x[MAXR];
-  float s[BN_MAXG] = {0.f, 0.f};
+  float s[2 * BN_MAXG] = {0.f, 0.f, 0.f, 0.f};   // sum d (batch 0, 1), sum d^2 (batch 0, 1)
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * GROUPS;
     const float v = a[(size_t)min(r, rows - 1) * lda + cc];
-    x[i] = (r < rows) ? v : 0.f;
-    if (r >= rpg) s[1] += x[i]; else s[0] += x[i];
-  }
-  bn_colsum<COLS, BN_MAXG>(s, sh);
-  const float mu0 = s[0] / (float)rpg, mu1 = s[1] / (float)rpg;
-  float q[BN_MAXG] = {0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < MAXR; ++i) {
-    const int r = grp + i * GROUPS;
+    x[i] = v;
     const bool g1 = r >= rpg;
-    const float d = (r < rows) ? x[i] - (g1 ? mu1 : mu0) : 0.f;
-    if (g1) q[1] += d * d; else q[0] += d * d;
+    const float d = (r < rows) ? v - (g1 ? sh1 : sh0) : 0.f;
+    if (g1) { s[1] += d; s[3] += d * d; } else { s[0] += d; s[2] += d * d; }
   }
-  bn_colsum<COLS, BN_MAXG>(q, sh);
-  const float var0 = q[0] / (float)rpg, var1 = q[1] / (float)rpg;   // biased batch variances
+  bn_colsum<COLS, 2 * BN_MAXG>(s, sh);
+  const float m0 = s[0] / (float)rpg, m1 = s[1] / (float)rpg;
+  const float mu0 = sh0 + m0, mu1 = sh1 + m1;
+  const float var0 = fmaxf(s[2] / (float)rpg - m0 * m0, 0.f);   // biased batch variances
+  const float var1 = fmaxf(s[3] / (float)rpg - m1 * m1, 0.f);
   const float is0 = rsqrtf(var0 + eps), is1 = rsqrtf(var1 + eps);
   if (grp == 0 && ok) {
     const float unb = (float)rpg / (float)max(rpg - 1, 1);

@@ -111,25 +111,43 @@ def test_gemm_bn_eval_relu(hip):
     assert torch.allclose(out, ref, atol=2e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("rows", [500, 37])
-def test_bn_relu_train_and_bwd(hip, rows):
-    a = mat(rows, 300, seed=15) * 3 + 1
+@pytest.mark.parametrize("rows,scale,offset", [(500, 3.0, 1.0), (37, 3.0, 1.0), (500, 0.05, 50.0)])
+def test_bn_relu_train_and_bwd(hip, rows, scale, offset):
+    # the (0.05, 50) case: tiny spread around a large mean -- the one-pass shifted statistics
+    # must not lose the variance to cancellation
+    a = mat(rows, 300, seed=15) * scale + offset
     gamma, beta = torch.rand(300, device=DEV) + 0.5, mat(300, seed=16)
-    outs = {}
+    fwd = {}
     for name, ops in (("hip", hip), ("ref", REF)):
         out = torch.zeros(rows, 300, device=DEV)
         nhat = torch.zeros_like(out)
         mean, inv = torch.zeros(300, device=DEV), torch.zeros(300, device=DEV)
         rm, rv = torch.zeros(300, device=DEV), torch.ones(300, device=DEV)
         ops.bn_relu_fwd(a, gamma, beta, out, nhat, mean, inv, rm, rv, True, 0.1, 1e-5)
+        fwd[name] = (out, nhat, mean, inv, rm, rv)
+    # the backward of both runs on the SAME (reference) forward tensors: a forward output within
+    # rounding of 0 may sit on either side of the ReLU and flip its mask
+    out, nhat, _, inv, _, _ = fwd["ref"]
+    bwd = {}
+    for name, ops in (("hip", hip), ("ref", REF)):
         dr = mat(rows, 300, seed=17)
         da = torch.zeros_like(out)
         dg, db, dbias = torch.zeros(300, device=DEV), torch.zeros(300, device=DEV), torch.zeros(300, device=DEV)
         ops.bn_relu_bwd(dr, out, nhat, gamma, inv, da, dg, db, dbias)
-        outs[name] = (out, nhat, mean, inv, rm, rv, da, dg, db, dbias)
+        bwd[name] = (da, dg, db, dbias)
     torch.cuda.synchronize()
-    for x, y in zip(outs["hip"], outs["ref"]):
-        assert torch.allclose(x, y, atol=2e-4, rtol=2e-4)
+    names = ("out", "nhat", "mean", "inv", "rm", "rv", "da", "dg", "db", "dbias")
+    for nm, x, y in zip(names, fwd["hip"] + bwd["hip"], fwd["ref"] + bwd["ref"]):
+        if offset < 10:
+            assert torch.allclose(x, y, atol=2e-4, rtol=2e-4), nm
+        else:
+            # ill-conditioned input (inv std ~20 amplifies fp32 rounding of x ~ 50 in both
+            # implementations): compare against each tensor's own scale
+            # (dbias = sum_r da is ~0 by construction -- rounding noise -- so it is measured on
+            # the scale of da itself)
+            scale = (bwd["ref"][0] if nm == "dbias" else y).abs().max().clamp_min(1e-6)
+            err = float((x - y).abs().max() / scale)
+            assert err < 2e-3, (nm, err)
 
 
 def test_adam_matches_torch(hip):
@@ -478,12 +496,15 @@ def test_wide_activation_and_backward(hip):
             assert torch.allclose(o1[:, s], torch.tanh(logits[:, s]), atol=1e-6)
         else:
             assert torch.allclose(o1[:, s:s + w].sum(1), torch.ones(rows, device=DEV), atol=1e-4)
-    # identical rows: Gumbel-softmax means agree with the torch reference
+    # identical rows: Gumbel-softmax means agree with the torch reference.  Each column mean is
+    # over 3000 draws (difference std <= sqrt(2 * 0.25 / 3000) ~ 0.013); the max over the wide
+    # table's columns needs ~4.5 sigma, and the seed keeps the draw independent of test order
+    torch.manual_seed(1234)
     base = logits[:1].repeat(rows, 1)
     hip.activate(base, o1, spans, 0.2)
     REF.activate(base, o2, spans, 0.2)
     torch.cuda.synchronize()
-    assert (o1.mean(0) - o2.mean(0)).abs().max().item() < 0.03
+    assert (o1.mean(0) - o2.mean(0)).abs().max().item() < 0.06
     # backward + cond CE against the reference, per-row loss terms
     B = 500
     lg = logits[:B].contiguous()
