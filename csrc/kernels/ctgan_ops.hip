@@ -1168,13 +1168,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols) {
   constexpr int GROUPS = BN_THREADS / COLS;
-  __shared__ float sh[2 * BN_WAVES * COLS];
+  __shared__ float sh[3 * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
   const int c = blockIdx.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   float dy[MAXR], nh[MAXR];
-  float st[2] = {0.f, 0.f};
+  float st[3] = {0.f, 0.f, 0.f};   // sum dy, sum dy * nhat, sum nhat
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * GROUPS;
@@ -1189,25 +1189,23 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     nh[i] = n;
     st[0] += d;
     st[1] += d * n;
+    st[2] += n;
   }
-  bn_colsum<COLS, 2>(st, sh);
-  const float sdy = st[0], sdyn = st[1];
-  if (grp == 0 && ok) { dbeta[c] = sdy; dgamma[c] = sdyn; }
+  bn_colsum<COLS, 3>(st, sh);
+  const float sdy = st[0], sdyn = st[1], snh = st[2];
   const float k = gamma[cc] * invstd[cc];
   const float invn = 1.f / (float)rows;
-  float sda[1] = {0.f};
+  // the preceding Linear's bias gradient sum_r da_r, in closed form from the same single
+  // reduction: k * (sum dy - rows * sdy / rows - sum nhat * sdyn / rows)
+  if (grp == 0 && ok) {
+    dbeta[c] = sdy;
+    dgamma[c] = sdyn;
+    if (dbias) dbias[c] = k * (sdy - sdy * (float)rows * invn - snh * sdyn * invn);
+  }
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * GROUPS;
-    if (r < rows && ok) {
-      const float v = k * (dy[i] - sdy * invn - nh[i] * sdyn * invn);
-      da[(size_t)r * ldda + c] = v;
-      sda[0] += v;
-    }
-  }
-  if (dbias) {
-    bn_colsum<COLS, 1>(sda, sh);
-    if (grp == 0 && ok) dbias[c] = sda[0];
+    if (r < rows && ok) da[(size_t)r * ldda + c] = k * (dy[i] - sdy * invn - nh[i] * sdyn * invn);
   }
 }
 
