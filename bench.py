@@ -13,26 +13,32 @@ RCCL (``nccl``) for N > 1.
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Without ``WORLD_SIZE`` in the environment and ``--gpus N > 1`` the script is its own launcher
+(the reference's intended one-command single-node fan-out, `Server/dtds/distributed.py:956-971`):
+the parent starts N fresh rank processes before anything touches the GPU, waits for them and
+exits with the first failing rank's code; rank 0 prints the JSON line.
+
 "steps" are federated rounds (epochs).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import tempfile
 import time
-
-import numpy as np
-import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_SEC_PER_EPOCH = 24.2   # README.md:53-54 (2 clients, epoch 1); BASELINE.md
 
 
-def main():
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed federated rounds")
@@ -45,7 +51,69 @@ def main():
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--sync-csv", action="store_true", help="write each epoch CSV inside its round")
-    args = ap.parse_args()
+    ap.add_argument("--check", action="store_true",
+                    help="after the timed rounds: assert every rank holds a bit-identical aggregate and the "
+                         "last epoch CSV has n_sample rows (reported as 'consistency')")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="build real process groups even for one rank (1 GPU: the aggregation runs as an "
+                         "RCCL all-reduce on a one-rank communicator)")
+    return ap
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_gpus() -> int:
+    # device_count() does not initialise HIP on this image (is_available() would): safe in a
+    # parent that later starts the GPU ranks
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch(n: int, argv) -> int:
+    """Start N rank processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set), wait, return the exit code."""
+    ngpu = _visible_gpus()
+    if ngpu > 0 and n > ngpu:
+        print(f"bench.py: --gpus {n} but only {ngpu} GPU(s) are visible", file=sys.stderr, flush=True)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if ngpu == 0:   # CPU ranks share the host: do not oversubscribe the cores
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 8) // n)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in live:     # one rank died: the others would block in a collective
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+# ----------------------------------------------------------------------------- one rank
+def run_rank(args) -> None:
+    import numpy as np
+    import torch
 
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.fed.runtime import FedConfig, FedRuntime
@@ -54,12 +122,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    comm = Comm.from_env("auto", device)
+        if world > 1:
+            torch.set_num_threads(max(1, (os.cpu_count() or 8) // world))
+    if args.force_dist and world == 1:
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    comm = Comm.from_env("auto", device, force_dist=args.force_dist)
+    n_data = comm.data_world_size()
+    if n_data != world:
+        raise SystemExit(f"bench.py: data plane has {n_data} ranks, expected {world}")
     out = args.out or os.path.join(tempfile.gettempdir(), f"fedtgan_bench_{os.getpid()}_{rank}")
     if world > 1:
         out = comm.broadcast_object(out, src=0)
@@ -73,6 +150,7 @@ def main():
     for ep in range(args.warmup):
         rt.run_round(ep)
     rt.flush_writes()
+    rt.timer.totals.clear()          # phase breakdown over the timed rounds only
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -86,19 +164,30 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_float(elapsed)
     sec_per_epoch = elapsed / max(args.steps, 1)
+    last = os.path.join(out, f"{spec.name}_result", f"{spec.name}_synthesis_epoch_{cfg.epochs - 1}.csv")
+
+    consistency = None
+    if args.check:
+        digest = hashlib.sha256(rt.engine.flat.detach().cpu().numpy().tobytes()).hexdigest()
+        digests = comm.all_gather_object(digest)
+        consistency = {"flat_identical": len(set(digests)) == 1, "ranks": len(digests)}
+        if rank == 0:
+            with open(last) as f:
+                consistency["csv_rows"] = sum(1 for _ in f) - 1
+        if not consistency["flat_identical"]:
+            raise SystemExit(f"bench.py: ranks disagree on the aggregate: {digests}")
 
     avg_jsd = avg_wd = None
     if rank == 0 and not args.no_eval:
         from fed_tgan_amd.data.synthetic import generate
         from fed_tgan_amd.eval.similarity import stat_sim
         import pandas as pd
-        last = os.path.join(out, f"{spec.name}_result", f"{spec.name}_synthesis_epoch_{cfg.epochs - 1}.csv")
         if os.path.exists(last):
             real = pd.concat([generate(spec, args.rows, seed=i) for i in range(max(world, 1))])
             avg_jsd, avg_wd = stat_sim(real, pd.read_csv(last), spec.categorical_list)
     if rank == 0:
         rec = {
-            "metric": "sec_per_epoch", "value": round(sec_per_epoch, 6), "unit": "s/epoch", "n_gpus": world,
+            "metric": "sec_per_epoch", "value": round(sec_per_epoch, 6), "unit": "s/epoch", "n_gpus": n_data,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(sec_per_epoch * 1000.0, 3),
             "higher_is_better": False, "scaling": "weak",
             "vs_baseline": round(sec_per_epoch / BASELINE_SEC_PER_EPOCH, 6),
@@ -107,12 +196,23 @@ def main():
             "config": {"model": "Fed-TGAN CTGAN (G 256x256 residual+BN, D 256x256 pack10, WGAN-GP slerp)",
                        "global_batch": 500 * world, "seq_len": None, "parallelism": f"fed{world}",
                        "rows_per_client": args.rows, "n_sample": args.n_sample,
-                       "steps_per_epoch": args.rows // 500, "backend": rt.engine.ops.name},
+                       "steps_per_epoch": args.rows // 500, "backend": rt.engine.ops.name,
+                       "data_plane": comm.data_backend if comm.dist_active else "none"},
             "avg_jsd": avg_jsd, "avg_wd": avg_wd, "epochs_trained": cfg.epochs,
-            "phase_s": {k: round(v / max(cfg.epochs, 1), 6) for k, v in rt.timer.totals.items()},
+            "phase_s": {k: round(v / max(args.steps, 1), 6) for k, v in rt.timer.totals.items()},
         }
+        if consistency is not None:
+            rec["consistency"] = consistency
         print(json.dumps(rec), flush=True)
     comm.destroy()
+
+
+def main():
+    argv = sys.argv[1:]
+    args = build_parser().parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus, argv))
+    run_rank(args)
 
 
 if __name__ == "__main__":

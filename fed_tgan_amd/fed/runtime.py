@@ -310,8 +310,10 @@ class FedRuntime:
         c = self.comm
         wts = self.weights if alive is None else effective_weights(self.weights, alive)
         w = float(wts[c.client_index]) if self.is_client else 0.0
-        c.weighted_all_reduce(self.engine.flat, w)
-        c.share_with_federator(self.engine.flat, self.federator)
+        with self.timer.phase("allreduce", self.device):
+            c.weighted_all_reduce(self.engine.flat, w)
+        with self.timer.phase("share", self.device):
+            c.share_with_federator(self.engine.flat, self.federator)
         # num_batches_tracked: weighted average of every client's counter, truncated (reference cast)
         ep = self.engine
         counts = np.asarray([2 * s for s in self.steps], dtype=np.float64) * (self._epoch_done)
@@ -329,20 +331,26 @@ class FedRuntime:
         # stream and the writer waits for it: round r's copy + CSV overlap round r + 1's training
         # (bench.py's timed region still ends with every table on disk)
         async_copy = self.cfg.async_csv and self.device.type == "cuda"
+        tm, dev = self.timer, self.device
         if len(samplers) == 1:
             if self.rank in samplers:
-                vals = self.engine.generate_decoded(per[0])
-                share = self._host(vals) if async_copy else vals.cpu().numpy()
+                with tm.phase("generate", dev):
+                    vals = self.engine.generate_decoded(per[0])
+                with tm.phase("d2h", dev):
+                    share = self._host(vals) if async_copy else vals.cpu().numpy()
         else:
             # every client decodes its share on its GPU; one gather to the federator (RCCL over
             # xGMI when the data plane is RCCL), one device-to-host copy there
-            vals = self.engine.generate_decoded(per[samplers.index(self.rank)])
-            rows = c.gather_rows(vals, per, samplers, dst=self.federator, to_host=not async_copy)
-            if self.is_fed:
-                if rows.device.type == "cuda":
-                    share = self._host(rows)
-                else:
-                    share = rows.numpy()
+            with tm.phase("generate", dev):
+                vals = self.engine.generate_decoded(per[samplers.index(self.rank)])
+            with tm.phase("gather", dev):
+                rows = c.gather_rows(vals, per, samplers, dst=self.federator, to_host=not async_copy)
+            with tm.phase("d2h", dev):
+                if self.is_fed:
+                    if rows.device.type == "cuda":
+                        share = self._host(rows)
+                    else:
+                        share = rows.numpy()
         if self.is_fed and self.cfg.write_csv:
             self.write_epoch_csv(share, epoch)
         return share if self.is_fed else None

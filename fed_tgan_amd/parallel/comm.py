@@ -32,7 +32,7 @@ import torch.distributed as dist
 class Comm:
     def __init__(self, rank: int = 0, world_size: int = 1, client_ranks: Sequence[int] = (0,),
                  data_backend: str = "gloo", ip: str = "127.0.0.1", port: int = 7788, timeout_s: float = 600.0,
-                 device: torch.device | None = None, init: bool = True):
+                 device: torch.device | None = None, init: bool = True, force_dist: bool = False):
         self.rank = rank
         self.world_size = world_size
         self.client_ranks = list(client_ranks)
@@ -43,7 +43,11 @@ class Comm:
         self.data = None
         self.p2p = None
         self.initialized = False
-        if world_size > 1 and init:
+        # ``force_dist``: build real process groups even for one rank, so the collective branches
+        # (RCCL all-reduce / gather / send-recv) execute on a single-GPU box instead of the
+        # world-size-1 short-circuits
+        self.dist_active = (world_size > 1 or force_dist) and init
+        if self.dist_active:
             self._init(ip, port)
 
     def _init(self, ip: str, port: int):
@@ -62,14 +66,21 @@ class Comm:
             self.data = self.ctrl
 
     @classmethod
-    def from_env(cls, data_backend: str = "auto", device: torch.device | None = None) -> "Comm":
+    def from_env(cls, data_backend: str = "auto", device: torch.device | None = None,
+                 force_dist: bool = False) -> "Comm":
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         ip = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("MASTER_PORT", "29500"))
         if data_backend == "auto":
             data_backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
-        return cls(rank, ws, list(range(ws)), data_backend, ip, port, device=device)
+        return cls(rank, ws, list(range(ws)), data_backend, ip, port, device=device, force_dist=force_dist)
+
+    def data_world_size(self) -> int:
+        """Ranks in the data-plane group (the clients that take part in the all-reduce)."""
+        if not self.dist_active or self.data is None:
+            return 1
+        return dist.get_world_size(self.data)
 
     # ------------------------------------------------------------------ properties
     @property
@@ -86,34 +97,34 @@ class Comm:
 
     # ------------------------------------------------------------------ control plane
     def all_gather_object(self, obj: Any) -> List[Any]:
-        if self.world_size == 1:
+        if not self.dist_active:
             return [obj]
         out: List[Any] = [None] * self.world_size
         dist.all_gather_object(out, obj, group=self.ctrl)
         return out
 
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
-        if self.world_size == 1:
+        if not self.dist_active:
             return obj
         box = [obj if self.rank == src else None]
         dist.broadcast_object_list(box, src=src, group=self.ctrl)
         return box[0]
 
     def barrier(self):
-        if self.world_size > 1:
+        if self.dist_active:
             dist.barrier(group=self.ctrl)
 
     def heartbeat(self, timeout_s: float):
         """Failure detection: a monitored gloo barrier over the control plane.  If a rank does not
         arrive within ``timeout_s`` every live rank raises, naming the missing ranks (instead of
         hanging until the process-group timeout)."""
-        if self.world_size > 1:
+        if self.dist_active:
             dist.monitored_barrier(group=self.ctrl, timeout=datetime.timedelta(seconds=timeout_s),
                                    wait_all_ranks=True)
 
     def broadcast_tensor(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         """Broadcast a tensor over the control plane (device tensors are staged through host memory)."""
-        if self.world_size == 1:
+        if not self.dist_active:
             return t
         host = t.detach().to("cpu", copy=True) if t.device.type != "cpu" else t
         dist.broadcast(host, src=src, group=self.ctrl)
@@ -122,19 +133,19 @@ class Comm:
         return t
 
     def all_reduce_cpu(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-        if self.world_size > 1:
+        if self.dist_active:
             dist.all_reduce(t, op=op, group=self.ctrl)
         return t
 
     def max_float(self, x: float) -> float:
-        if self.world_size == 1:
+        if not self.dist_active:
             return x
         t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ctrl)
         return float(t.item())
 
     def gather_bytes(self, payload: bytes, dst: int = 0) -> Optional[List[bytes]]:
-        if self.world_size == 1:
+        if not self.dist_active:
             return [payload]
         out = [None] * self.world_size if self.rank == dst else None
         dist.gather_object(payload, out, dst=dst, group=self.ctrl)
@@ -149,7 +160,7 @@ class Comm:
         largest share, one ``gather``) and ``dst`` copies the result to the host once (or, with
         ``to_host=False``, keeps it on the device for an asynchronous copy); the gloo path gathers
         host tensors.  Returns the tensor on ``dst``, None elsewhere."""
-        if self.world_size == 1:
+        if not self.dist_active:
             return t.cpu() if to_host else t
         nccl = self.data_backend == "nccl"
         width = t.shape[1]
@@ -172,7 +183,7 @@ class Comm:
         Non-client ranks (a dedicated federator) contribute zeros and receive the sum too
         when the data plane spans every rank (gloo).
         """
-        if self.world_size == 1:
+        if not self.dist_active:
             if weight != 1.0:
                 flat.mul_(weight)
             return flat
@@ -194,7 +205,7 @@ class Comm:
 
     def share_with_federator(self, flat: torch.Tensor, federator: int = 0) -> torch.Tensor:
         """After an RCCL reduce among clients, hand the aggregate to a dataless federator rank."""
-        if self.world_size == 1 or self.data_backend != "nccl" or federator in self.client_ranks:
+        if not self.dist_active or self.data_backend != "nccl" or federator in self.client_ranks:
             return flat
         src = self.client_ranks[0]
         host = flat.detach().to("cpu", copy=True)
@@ -210,7 +221,7 @@ class Comm:
     def init_p2p(self):
         """Collective (every rank): the point-to-point group of the split (MD-GAN) mode -- RCCL over
         all ranks when the data plane is RCCL, else the gloo control plane."""
-        if self.world_size == 1:
+        if not self.dist_active:
             self.p2p = None
         elif self.data_backend == "nccl":
             self.p2p = dist.new_group(ranks=list(range(self.world_size)), backend="nccl", timeout=self.timeout)

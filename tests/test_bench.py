@@ -15,7 +15,7 @@ def _json_lines(out: str):
 
 
 def _env():
-    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
     env.pop("RANK", None); env.pop("WORLD_SIZE", None); env.pop("LOCAL_RANK", None)
     return env
 
@@ -44,3 +44,37 @@ def test_bench_torchrun_two_ranks():
     rec = lines[0]
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "fed2" and rec["scaling"] == "weak"
     assert rec["avg_jsd"] is not None and rec["avg_wd"] is not None
+
+
+def test_bench_self_launch_four_ranks():
+    """`bench.py --gpus 4` with no launcher: the script starts the 4 ranks itself (GPUs hidden -> gloo)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1", "--warmup",
+                        "1", "--rows", "1000", "--n-sample", "1500", "--quiet", "--no-eval"],
+                       capture_output=True, text=True, timeout=400, env=_env(), cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    rec = lines[0]
+    assert rec["n_gpus"] == 4 and rec["config"]["parallelism"] == "fed4"
+    for k in ("train", "allreduce", "gather", "d2h", "generate"):
+        assert k in rec["phase_s"], rec["phase_s"]
+
+
+def test_bench_eight_ranks_identical_aggregate():
+    """8 self-launched ranks: every rank holds a bit-identical aggregate after the last round and the
+    epoch CSV (sharded generation, gathered on rank 0) has all 40,000 rows."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup",
+                        "1", "--rows", "1000", "--n-sample", "40000", "--quiet", "--no-eval", "--check"],
+                       capture_output=True, text=True, timeout=600, env=_env(), cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["n_gpus"] == 8
+    assert rec["consistency"] == {"flat_identical": True, "ranks": 8, "csv_rows": 40000}
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--rows", "1000", "--quiet"], capture_output=True, text=True, timeout=120, env=env,
+                       cwd="/tmp")
+    assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)

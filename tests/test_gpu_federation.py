@@ -85,3 +85,36 @@ def test_gpu_two_process_federation_gloo_data_plane(tmp_path):
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     _check_outputs(tmp_path, 2, 3001)
+
+
+def _run(cmd, env=None, timeout=180):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.run([sys.executable] + cmd, cwd=root, env=env or dict(os.environ), capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_rccl_branches_one_rank():
+    """The nccl branches of Comm (weighted all-reduce, gather_rows, batched P2P exchange) on a one-rank
+    RCCL communicator; the RCCL debug log must show the AllReduce being enqueued."""
+    import json
+    env = dict(os.environ, NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="COLL")
+    r = _run(["tools/rccl_selftest.py"], env=env, timeout=150)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["ok"] and res["data_backend"] == "nccl" and res["data_ranks"] == 1, res
+    assert "AllReduce" in (r.stdout + r.stderr)
+
+
+def test_bench_one_gpu_rccl_data_plane():
+    """bench.py on one GPU with a real one-rank RCCL data plane (--force-dist): the round's
+    aggregation is an RCCL all-reduce; every rank (one) agrees on the aggregate, full CSV written."""
+    import json
+    r = _run(["bench.py", "--steps", "1", "--warmup", "1", "--rows", "4000", "--n-sample", "3000", "--quiet",
+              "--no-eval", "--check", "--force-dist"], timeout=170)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["config"]["data_plane"] == "nccl" and rec["n_gpus"] == 1
+    assert rec["consistency"]["flat_identical"] and rec["consistency"]["csv_rows"] == 3000
+    assert "allreduce" in rec["phase_s"]
