@@ -354,7 +354,7 @@ void bn_relu_train(const Tensor& a, const Tensor& gamma, const Tensor& beta, con
   check_f32_2d(a, "a");
   check_f32_2d(out, "out");
   check_f32_2d(nhat, "nhat");
-  TORCH_CHECK(a.size(0) <= 1024, "bn_relu_train: batch > 1024 unsupported (rows kept in registers)");
+  TORCH_CHECK(a.size(0) >= 1, "bn_relu_train: empty batch");
   TORCH_CHECK(groups == 1 || groups == 2, "bn_relu_train: 1 or 2 batches");
   TORCH_CHECK(a.size(0) % groups == 0 && a.size(0) / groups >= 1, "bn_relu_train: rows must split evenly");
   TORCH_CHECK(out.sizes() == a.sizes() && nhat.sizes() == a.sizes() && gamma.numel() == a.size(1), "bn: shapes");
@@ -371,7 +371,7 @@ void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Te
   check_f32_2d(r, "r");
   check_f32_2d(nhat, "nhat");
   check_f32_2d(da, "da");
-  TORCH_CHECK(dr.size(0) <= 1024, "bn_relu_bwd: batch > 1024 unsupported");
+  TORCH_CHECK(dr.size(0) >= 1, "bn_relu_bwd: empty batch");
   TORCH_CHECK(r.sizes() == dr.sizes() && nhat.sizes() == dr.sizes() && da.sizes() == dr.sizes(), "bn bwd: shapes");
   fedtgan::launch_bn_relu_bwd(cfp(dr), ld_of(dr), cfp(r), ld_of(r), cfp(nhat), ld_of(nhat), cfp(gamma), cfp(invstd),
                               fp(da), ld_of(da), fp(dgamma), fp(dbeta), optp<float>(dbias), (int)dr.size(0),

@@ -1131,6 +1131,63 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
   }
 }
 
+// Large batches (more rows than the register-resident kernel holds): two passes over the
+// column block, statistics first, then normalise + ReLU re-reading the GEMM output (L2-resident at
+// these sizes).  Same shifted one-pass statistics and running-stat order as above.
+template <int COLS>
+__global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
+    const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
+    float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
+    float momentum, float eps) {
+  constexpr int GROUPS = BN_THREADS / COLS;
+  __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
+  const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
+  const int c = blockIdx.x * COLS + lc;
+  const bool ok = c < cols;
+  const int cc = min(c, cols - 1);
+  const int rpg = rows / groups;
+  const float sh0 = a[cc], sh1 = a[(size_t)min(rpg, rows - 1) * lda + cc];
+  float s[2 * BN_MAXG] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = grp; r < rows; r += GROUPS) {
+    const float v = a[(size_t)r * lda + cc];
+    const bool g1 = r >= rpg;
+    const float d = v - (g1 ? sh1 : sh0);
+    if (g1) { s[1] += d; s[3] += d * d; } else { s[0] += d; s[2] += d * d; }
+  }
+  bn_colsum<COLS, 2 * BN_MAXG>(s, sh);
+  const float m0 = s[0] / (float)rpg, m1 = s[1] / (float)rpg;
+  const float mu0 = sh0 + m0, mu1 = sh1 + m1;
+  const float var0 = fmaxf(s[2] / (float)rpg - m0 * m0, 0.f);
+  const float var1 = fmaxf(s[3] / (float)rpg - m1 * m1, 0.f);
+  const float is0 = rsqrtf(var0 + eps), is1 = rsqrtf(var1 + eps);
+  if (grp == 0 && ok) {
+    const float unb = (float)rpg / (float)max(rpg - 1, 1);
+    float m = rm[c], v = rv[c];
+    mean[c] = mu0;
+    invstd[c] = is0;
+    m = (1.f - momentum) * m + momentum * mu0;
+    v = (1.f - momentum) * v + momentum * var0 * unb;
+    if (groups > 1) {
+      mean[(size_t)cols + c] = mu1;
+      invstd[(size_t)cols + c] = is1;
+      m = (1.f - momentum) * m + momentum * mu1;
+      v = (1.f - momentum) * v + momentum * var1 * unb;
+    }
+    rm[c] = m;
+    rv[c] = v;
+  }
+  if (!ok) return;
+  const float gm = gamma[c], bt = beta[c];
+  for (int r = grp; r < rows; r += GROUPS) {
+    const bool g1 = r >= rpg;
+    const float n = (a[(size_t)r * lda + c] - (g1 ? mu1 : mu0)) * (g1 ? is1 : is0);
+    nhat[(size_t)r * ldn + c] = n;
+    const float y = n * gm + bt;
+    out[(size_t)r * ldo + c] = y > 0.f ? y : 0.f;
+  }
+}
+
 template <int COLS>
 static void bn_train_cols(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
@@ -1144,7 +1201,10 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
   else if (rows <= 8 * GROUPS) BN_TRAIN_LAUNCH(8);
   else if (rows <= 16 * GROUPS) BN_TRAIN_LAUNCH(16);
   else if (rows <= 32 * GROUPS) BN_TRAIN_LAUNCH(32);
-  else BN_TRAIN_LAUNCH(64);
+  else if (rows <= 64 * GROUPS) BN_TRAIN_LAUNCH(64);
+  else
+    hipLaunchKernelGGL((bn_relu_train_stream_kernel<COLS>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo,
+                       nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps);
 #undef BN_TRAIN_LAUNCH
 }
 
@@ -1209,6 +1269,44 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
   }
 }
 
+// Large-batch backward: the three column sums in a first pass, da in a second (re-reading).
+template <int COLS>
+__global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_stream_kernel(
+    const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
+    int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols) {
+  constexpr int GROUPS = BN_THREADS / COLS;
+  __shared__ float sh[3 * BN_WAVES * COLS];
+  const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
+  const int c = blockIdx.x * COLS + lc;
+  const bool ok = c < cols;
+  const int cc = min(c, cols - 1);
+  float st[3] = {0.f, 0.f, 0.f};
+  for (int r = grp; r < rows; r += GROUPS) {
+    const size_t rr = (size_t)r;
+    const float d = r_[rr * ldr + cc] > 0.f ? dr[rr * lddr + cc] : 0.f;
+    const float n = nhat[rr * ldn + cc];
+    st[0] += d;
+    st[1] += d * n;
+    st[2] += n;
+  }
+  bn_colsum<COLS, 3>(st, sh);
+  const float sdy = st[0], sdyn = st[1], snh = st[2];
+  const float k = gamma[cc] * invstd[cc];
+  const float invn = 1.f / (float)rows;
+  if (grp == 0 && ok) {
+    dbeta[c] = sdy;
+    dgamma[c] = sdyn;
+    if (dbias) dbias[c] = k * (sdy - sdy * (float)rows * invn - snh * sdyn * invn);
+  }
+  if (!ok) return;
+  for (int r = grp; r < rows; r += GROUPS) {
+    const size_t rr = (size_t)r;
+    const float d = r_[rr * ldr + c] > 0.f ? dr[rr * lddr + c] : 0.f;
+    da[rr * ldda + c] = k * (d - sdy * invn - nhat[rr * ldn + c] * sdyn * invn);
+  }
+}
+
 template <int COLS>
 static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
@@ -1222,7 +1320,10 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
   else if (rows <= 8 * GROUPS) BN_BWD_LAUNCH(8);
   else if (rows <= 16 * GROUPS) BN_BWD_LAUNCH(16);
   else if (rows <= 32 * GROUPS) BN_BWD_LAUNCH(32);
-  else BN_BWD_LAUNCH(64);
+  else if (rows <= 64 * GROUPS) BN_BWD_LAUNCH(64);
+  else
+    hipLaunchKernelGGL((bn_relu_bwd_stream_kernel<COLS>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma,
+                       invstd, da, ldda, dgamma, dbeta, dbias, rows, cols);
 #undef BN_BWD_LAUNCH
 }
 

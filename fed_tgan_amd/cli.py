@@ -21,7 +21,8 @@ New flags: -config (dataset spec JSON or builtin name), -backend {auto,hip,torch
 -precision {bf16,fp32}, -data_backend {auto,gloo,nccl}, -synthetic_rows, -shard
 {independent,iid,dirichlet,skew}, -alpha, -n_sample, -aggregation {weighted,uniform}, -gmm
 {torch,sklearn}, -seed, -out_dir, -ckpt_every, -resume, -local_clients (single-process
-multi-client emulation), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan}.
+multi-client emulation), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan},
+-init {independent,broadcast} (initial weights; independent = the reference's per-client init).
 """
 from __future__ import annotations
 
@@ -89,6 +90,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-grad_flow", action="store_true", help="write reports/grad_flow.{csv,png} (client 0)")
     p.add_argument("-sync_csv", action="store_true",
                    help="write each epoch CSV inside its round (reference timing) instead of in the background")
+    p.add_argument("-init", type=str, default="independent", choices=["independent", "broadcast"],
+                   help="initial G/D weights: each client its own random init (reference) or client 0's on every rank")
     p.add_argument("-quiet", action="store_true")
     return p
 
@@ -120,7 +123,7 @@ def fed_config_from_args(args):
                      metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
                      e_interval=args.E_interval, grad_flow=args.grad_flow, profile_dir=args.profile_dir,
                      heartbeat_s=args.heartbeat,
-                     dump_real=args.dump_real, async_csv=not args.sync_csv)
+                     dump_real=args.dump_real, async_csv=not args.sync_csv, init=args.init)
 
 
 def pick_device(rank: int, colocated: bool, backend: str, mode: str = "fedavg") -> torch.device:

@@ -94,6 +94,11 @@ class FedConfig:
     profile_dir: Optional[str] = None       # export a torch.profiler trace of round `profile_epoch`
     profile_epoch: int = 1
     dump_real: bool = False                 # write the synthetic client shards (for the evaluators)
+    # initial G/D weights: "independent" = every client its own random init, as the reference's
+    # clients build their own modules (`Client/.../dtds/distributed.py:156-165`); the federator's copy
+    # comes from the first client (`Server/dtds/distributed.py:789`).  "broadcast" = every rank
+    # starts from the first client's weights.
+    init: str = "independent"
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -167,6 +172,8 @@ class FedRuntime:
         self.start_epoch = 0
         self.metrics = MetricsLog(cfg.metrics_log) if (cfg.metrics_log and self.is_fed) else None
         self.dump_csv = None
+        self._round_start: Dict[int, float] = {}    # epoch -> wall time its round began
+        self._csv_done: Dict[int, float] = {}       # epoch -> wall time its CSV was on disk
 
     # ================================================================= data
     def _local_frame(self) -> pd.DataFrame:
@@ -272,13 +279,28 @@ class FedRuntime:
         if self.is_client:
             self.engine.set_training_data(self.train_matrix)
         self.engine.set_generation_tables(self.gen_cond, self.transformer)
-        c.broadcast_tensor(self.engine.flat, src=c.client_ranks[0])
+        self._initial_weights()
         self.steps = [n // cfg.engine.batch_size for n in self.rows]
         if cfg.resume:
             self.load_checkpoint()
         self.csv_cols = csv_columns(merged, self.vocabs) if not spec.date_dic else None
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
+
+    def _initial_weights(self):
+        """Step F: the clients keep their own random init (reference) or adopt the first client's;
+        a dataless federator always takes the first client's copy (`Server/dtds/distributed.py:789`)."""
+        c, src = self.comm, self.comm.client_ranks[0]
+        if self.cfg.init == "broadcast":
+            c.broadcast_tensor(self.engine.flat, src=src)
+        elif self.cfg.init == "independent":
+            if not all(r in c.client_ranks for r in range(c.world_size)):
+                buf = self.engine.flat.detach().clone()
+                c.broadcast_tensor(buf, src=src)
+                if not self.is_client:
+                    self.engine.flat.copy_(buf)
+        else:
+            raise ValueError(f"init must be independent or broadcast, got {self.cfg.init!r}")
 
     def _encode_training_table(self):
         """VGM-encode the local table: on the GPU with the HIP kernel (matrix and row lists stay
@@ -319,11 +341,15 @@ class FedRuntime:
         counts = np.asarray([2 * s for s in self.steps], dtype=np.float64) * (self._epoch_done)
         ep.bn_batches = int(np.sum(wts * counts))
 
-    def sample_round(self, epoch: int):
-        """Generate n_sample rows, decode, and (federator) write the epoch CSV."""
+    def sample_round(self, epoch: int, aggregated: bool = True):
+        """Generate n_sample rows, decode, and (federator) write the epoch CSV.
+
+        After an aggregation every client holds the global model, so the rows are generated sharded
+        over the client GPUs; on a round without aggregation (-E_interval > 1) the clients' models
+        differ and the whole table comes from the federator's model alone."""
         c = self.comm
         colocated = self.federator in c.client_ranks
-        samplers = c.client_ranks if colocated else [self.federator]
+        samplers = c.client_ranks if (colocated and aggregated) else [self.federator]
         share = None
         per = [self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0)
                for i in range(len(samplers))]
@@ -380,6 +406,11 @@ class FedRuntime:
             self._writer.flush()
 
     def _write_epoch_csv(self, values, epoch: int):
+        path = self._write_epoch_csv_body(values, epoch)
+        self._csv_done[epoch] = time.time()
+        return path
+
+    def _write_epoch_csv_body(self, values, epoch: int):
         if isinstance(values, PendingHost):
             values = values.get()
         path = os.path.join(self.result_dir(), f"{self.name}_synthesis_epoch_{epoch}.csv")
@@ -396,6 +427,7 @@ class FedRuntime:
     def run_round(self, epoch: int) -> float:
         c = self.comm
         t0 = time.time()
+        self._round_start[epoch] = t0
         alive = round_alive_mask(self.cfg, epoch, c.n_clients)
         with self.timer.phase("train", self.device):
             if self.is_client and alive[c.client_index]:
@@ -406,10 +438,11 @@ class FedRuntime:
         with self.timer.phase("aggregate", self.device):
             # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
             # local epochs between aggregations (1 = aggregate every round, the reference behaviour)
-            if (epoch + 1) % max(int(self.cfg.e_interval), 1) == 0:
+            aggregated = (epoch + 1) % max(int(self.cfg.e_interval), 1) == 0
+            if aggregated:
                 self.aggregate(alive if self.cfg.drop_client_prob > 0 else None)
         with self.timer.phase("sample_dump", self.device):
-            self.sample_round(epoch)
+            self.sample_round(epoch, aggregated)
         if self.device.type == "cuda":
             stream_sync(self.device)
         dt = time.time() - t0
@@ -463,6 +496,7 @@ class FedRuntime:
                     self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,
                                         **self.timer.last()})
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
+                self.flush_writes()      # the checkpoint's per-round stamps include every CSV so far
                 self.save_checkpoint(ep + 1)
         self.flush_writes()
         if self.gradflow is not None:
@@ -475,12 +509,33 @@ class FedRuntime:
             if cfg.dump_real:
                 self.merge_real_shards()
 
+    def epoch_stamps(self) -> List[float]:
+        """Per-round entries of ``timestamp_experiment.csv``, each INCLUDING that round's CSV dump.
+
+        The reference times the round with the dump inside it (`Server/dtds/distributed.py:795-825`),
+        so the cumulative sum (``time_stamp`` in `Server/similarity_analysis.py:111-115`) is the wall
+        time at which each epoch's CSV exists.  With the background writer the dump of round r
+        overlaps round r + 1, so entry r is the time from the previous epoch's CSV completion (or
+        the first round's start) to this epoch's CSV completion: the cumulative sum again equals the
+        wall time at which epoch r's table is on disk.  Rounds without a recorded CSV keep their
+        round time."""
+        fitted = sorted(self._round_start)
+        if not fitted or any(e not in self._csv_done for e in fitted):
+            return list(self.round_times)
+        prior = list(self.round_times[:max(0, len(self.round_times) - len(fitted))])   # resumed: checkpointed rounds
+        out, prev = [], self._round_start[fitted[0]]
+        for e in fitted:
+            done = self._csv_done[e]
+            out.append(done - prev)
+            prev = done
+        return prior + out
+
     def write_timestamps(self):
         """One per-round wall time per line, no header (`Server/dtds/distributed.py:827-829`)."""
         import csv
         path = os.path.join(self.cfg.out_dir, "timestamp_experiment.csv")
         with open(path, "w", newline="") as f:
-            csv.writer(f, dialect="excel").writerows([[t] for t in self.round_times])
+            csv.writer(f, dialect="excel").writerows([[t] for t in self.epoch_stamps()])
         return path
 
     # ================================================================= checkpoint / resume
@@ -493,7 +548,7 @@ class FedRuntime:
         e = self.engine
         state = {"epoch": epoch, "flat": e.flat.cpu(), "mG": e.mG.cpu(), "vG": e.vG.cpu(), "mD": e.mD.cpu(),
                  "vD": e.vD.cpu(), "stepG": e.stepG.cpu(), "stepD": e.stepD.cpu(), "bn_batches": e.bn_batches,
-                 "round_times": list(self.round_times), "cpu_rng": torch.get_rng_state()}
+                 "round_times": self.epoch_stamps(), "cpu_rng": torch.get_rng_state()}
         if hasattr(e.ops, "ctr"):          # HIP backend: the device Philox step counter
             state["rng_ctr"] = e.ops.ctr.cpu()
         torch.save(state, self._ckpt_path())

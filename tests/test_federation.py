@@ -176,3 +176,58 @@ def test_real_csv_datapath_per_client(tmp_path):
     assert rt.rows == [1200, 700] and rt.steps == [12, 7]
     out = pd.read_csv(tmp_path / "Intrusion_result" / "Intrusion_synthesis_epoch_1.csv")
     assert out.shape == (600, 42)
+
+
+def _init_two_clients(tmp, init):
+    """Initialise a 2-client in-process federation (threads) and return both runtimes."""
+    import threading
+    from fed_tgan_amd.fed.local import LocalGroup, ThreadComm
+    g = LocalGroup(2)
+    rts = [None, None]
+
+    def run(r):
+        rt = FedRuntime(_cfg(tmp, init=init, shard_mode="iid"), ThreadComm(g, r, torch.device("cpu")),
+                        torch.device("cpu"))
+        rt.initialize()
+        rts[r] = rt
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    return rts
+
+
+def test_initial_weights_independent_by_default(tmp_path):
+    """Reference: every client builds its own randomly initialised G/D (`Client/.../distributed.py:156-165`);
+    -init broadcast gives every client the first client's weights."""
+    a, b = _init_two_clients(tmp_path / "ind", "independent")
+    assert not torch.equal(a.engine.flat, b.engine.flat)
+    a, b = _init_two_clients(tmp_path / "bc", "broadcast")
+    assert torch.equal(a.engine.flat, b.engine.flat)
+
+
+def test_timestamps_include_the_background_csv(tmp_path, monkeypatch):
+    """timestamp_experiment.csv: with the background writer each entry still ends when its epoch's CSV
+    is on disk, so the cumulative sum is the wall time at which each table exists (the reference's
+    `time_stamp`, `Server/similarity_analysis.py:111-115`)."""
+    import time as _t
+    slow = FedRuntime._write_epoch_csv_body
+
+    def delayed(self, values, epoch):
+        _t.sleep(0.4)
+        return slow(self, values, epoch)
+
+    monkeypatch.setattr(FedRuntime, "_write_epoch_csv_body", delayed)
+    rt = FedRuntime(_cfg(tmp_path, epochs=3, async_csv=True), Comm(0, 1, [0], "gloo", device=torch.device("cpu")),
+                    torch.device("cpu"))
+    rt.initialize()
+    t0 = _t.time()
+    rt.fit()
+    ts = pd.read_csv(tmp_path / "timestamp_experiment.csv", header=None).iloc[:, 0].to_numpy()
+    assert len(ts) == 3
+    # the three writes are serial: the stamps cover at least 3 x 0.4 s of CSV writing
+    assert ts.sum() >= 1.2 and (ts >= 0).all()
+    assert abs(ts.sum() - (rt._csv_done[2] - rt._round_start[0])) < 1e-6
+    assert ts.sum() <= _t.time() - t0 + 1e-3
+    for e in range(3):
+        assert abs(np.cumsum(ts)[e] - (rt._csv_done[e] - rt._round_start[0])) < 1e-6

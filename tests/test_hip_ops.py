@@ -111,7 +111,7 @@ def test_gemm_bn_eval_relu(hip):
     assert torch.allclose(out, ref, atol=2e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("rows,scale,offset", [(500, 3.0, 1.0), (37, 3.0, 1.0), (500, 0.05, 50.0)])
+@pytest.mark.parametrize("rows,scale,offset", [(500, 3.0, 1.0), (37, 3.0, 1.0), (500, 0.05, 50.0), (5000, 3.0, 1.0)])
 def test_bn_relu_train_and_bwd(hip, rows, scale, offset):
     # the (0.05, 50) case: tiny spread around a large mean -- the one-pass shifted statistics
     # must not lose the variance to cancellation
