@@ -146,3 +146,32 @@ def test_side_stream_overlap_is_race_free():
         out.append((eng.flat.clone(), eng.mG.clone(), eng.vD.clone()))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("batch", [600, 2500])
+def test_large_batches_train(batch):
+    """Batches past the register-resident BN kernels (paired 2B = 1200 / 5000 rows take the streaming
+    BN kernels at 5000): the paired generator pass matches per-batch BatchNorm of its own GEMM output,
+    and a few captured steps stay finite."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    torch.manual_seed(0)
+    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=batch), DEV, backend="hip", seed=3)
+    eng.set_training_data(X)
+    rm0 = eng.p["G.0.rm"].clone()
+    eng._prepare_paired()
+    torch.cuda.synchronize()
+    B, g0 = eng.B, eng.gdims[0]
+    a = eng.abuf2[0]
+    out = eng.H2[:, eng.off[1]:eng.off[0]]
+    for h in (slice(0, B), slice(B, 2 * B)):
+        ref = torch.relu(F.batch_norm(a[h], None, None, eng.p["G.0.gamma"], eng.p["G.0.beta"], True, 0.1, 1e-5))
+        assert torch.allclose(out[h], ref, atol=2e-4, rtol=2e-4)
+    m0, m1 = a[:B].mean(0), a[B:].mean(0)
+    want = 0.81 * rm0 + 0.09 * m0 + 0.1 * m1
+    assert torch.allclose(eng.p["G.0.rm"], want, atol=1e-5)
+    eng.train_steps(3, use_graph=True)
+    torch.cuda.synchronize()
+    assert np.isfinite(eng.losses()).all() and bool(torch.isfinite(eng.flat).all())
+    assert g0 == out.shape[1]
