@@ -577,6 +577,42 @@ void kmeans_step(const Tensor& x, const Tensor& n_rows, const Tensor& centers, c
   fedtgan::launch_kmeans_step(a, cur_stream());
 }
 
+void vgm_fit(const Tensor& x, const Tensor& n_rows, const c10::optional<Tensor>& init_centers, int64_t seed,
+             double wprior, double tol, double reg_covar, int64_t max_iter, int64_t km_iter, const Tensor& out,
+             const Tensor& info, const Tensor& lower_bound) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.stride(1) == 1, "vgm_fit: x");
+  const int64_t nc = x.size(0);
+  TORCH_CHECK(n_rows.is_cuda() && n_rows.scalar_type() == at::kInt && n_rows.is_contiguous() && n_rows.numel() == nc,
+              "vgm_fit: n_rows");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kDouble && out.is_contiguous() && out.numel() == nc * 60,
+              "vgm_fit: out must be [n_cols, 6, 10] fp64");
+  TORCH_CHECK(info.is_cuda() && info.scalar_type() == at::kInt && info.is_contiguous() && info.numel() == nc * 2,
+              "vgm_fit: info");
+  TORCH_CHECK(lower_bound.is_cuda() && lower_bound.scalar_type() == at::kDouble && lower_bound.numel() == nc,
+              "vgm_fit: lower_bound");
+  fedtgan::VgmFitAllArgs a{};
+  a.x = x.data_ptr<double>();
+  a.ldx = (int)x.stride(0);
+  a.n_cols = (int)nc;
+  a.n_rows = n_rows.data_ptr<int>();
+  if (init_centers.has_value()) {
+    TORCH_CHECK(init_centers->is_cuda() && init_centers->scalar_type() == at::kDouble &&
+                    init_centers->is_contiguous() && init_centers->numel() == nc * 10,
+                "vgm_fit: init_centers must be [n_cols, 10] fp64");
+    a.init_centers = init_centers->data_ptr<double>();
+  }
+  a.seed = (uint64_t)seed;
+  a.wprior = wprior;
+  a.tol = tol;
+  a.reg_covar = reg_covar;
+  a.max_iter = (int)max_iter;
+  a.km_iter = (int)km_iter;
+  a.out = out.data_ptr<double>();
+  a.info = info.data_ptr<int>();
+  a.lower_bound = lower_bound.data_ptr<double>();
+  fedtgan::launch_vgm_fit(a, cur_stream());
+}
+
 std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
 // kernel variant knobs for measured sweeps (tools/microbench.py); returns the previous value
@@ -682,6 +718,9 @@ TORCH_LIBRARY(fedtgan, m) {
       "int rows_per_block) -> ()");
   m.def("kmeans_step(Tensor x, Tensor n_rows, Tensor centers, Tensor(a!) partial, int rows_per_block) -> ()");
   m.def(
+      "vgm_fit(Tensor x, Tensor n_rows, Tensor? init_centers, int seed, float wprior, float tol, float reg_covar, "
+      "int max_iter, int km_iter, Tensor(a!) out, Tensor(b!) info, Tensor(c!) lower_bound) -> ()");
+  m.def(
       "vgm_encode(Tensor x, Tensor(a!) out, Tensor(b!) opt, Tensor col_kind, Tensor col_pos, Tensor col_aux, "
       "Tensor col_span, Tensor col_lut_n, Tensor consts, Tensor means, Tensor prec, Tensor stds, Tensor vrank, Tensor lut, int seed, "
       "int stream) -> ()");
@@ -711,6 +750,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("vgm_encode", &vgm_encode);
   m.impl("vgm_estep", &vgm_estep);
   m.impl("kmeans_step", &kmeans_step);
+  m.impl("vgm_fit", &vgm_fit);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CPU, m) { m.impl("write_csv", &write_csv); }

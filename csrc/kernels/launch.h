@@ -231,4 +231,19 @@ struct VgmFitArgs {
 void launch_vgm_estep(const VgmFitArgs& a, hipStream_t stream);
 void launch_kmeans_step(const VgmFitArgs& a, hipStream_t stream);
 
+// The whole fit of every column, one workgroup per column (kernels/vgm_fit.hip)
+struct VgmFitAllArgs {
+  const double* x;            // [n_cols, ldx] centred column data
+  int ldx, n_cols;
+  const int* n_rows;          // [n_cols]
+  const double* init_centers; // [n_cols, 10] k-means centres to start from, or null (k-means++ + Lloyd)
+  uint64_t seed;
+  double wprior, tol, reg_covar;
+  int max_iter, km_iter;
+  double* out;                // [n_cols, 6, 10]: stick a, stick b, beta, means, dof, covariances
+  int* info;                  // [n_cols, 2]: EM iterations, converged
+  double* lower_bound;        // [n_cols]
+};
+void launch_vgm_fit(const VgmFitAllArgs& a, hipStream_t stream);
+
 }  // namespace fedtgan

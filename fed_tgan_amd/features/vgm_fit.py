@@ -21,11 +21,11 @@ Columns may have different lengths (padded + masked).  Results are returned as a
 sklearn's (same objective, same init family); it is not bitwise identical because the
 k-means seeding draws differ.
 
-The data passes -- the E-step's responsibilities + sufficient statistics (sum r, sum r x,
-sum r x^2, sum r log r) and the k-means assignment + sums -- run as the HIP kernels of
-``csrc/kernels/vgm_fit.hip`` on a GPU (one read of the data per iteration, fp64), or as
-torch ops on the CPU (the reference implementation of the same statistics).  The M-step,
-lower bound and convergence bookkeeping are [n_cols, K]-sized torch ops shared by both.
+On a GPU the whole fit is ONE launch of ``vgm_fit_kernel`` (``csrc/kernels/vgm_fit.hip``): one
+workgroup per column runs the seeding, Lloyd, and the EM loop with its M-step, digamma/lgamma
+lower bound and convergence test on the device (fp64).  On the CPU the same algorithm runs as
+torch ops (the reference implementation); ``fused=False`` on a GPU keeps the per-pass kernels
+(E-step / k-means statistics) with the torch M-step, as a second oracle.
 Data are centred per column first (prior mean 0), and the means shifted back at the end.
 """
 from __future__ import annotations
@@ -181,18 +181,50 @@ def _lower_bound(ent, s):
     return ent - log_wishart - log_norm_weight - 0.5 * torch.log(s.beta).sum(1)
 
 
+def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: float) -> VGMBank:
+    """The whole fit as ONE launch of ``vgm_fit_kernel`` (csrc/kernels/vgm_fit.hip): one workgroup
+    per column runs seeding, Lloyd and the EM loop with its M-step, lower bound and convergence test
+    on the device."""
+    from ..ops import native
+    L = native.require()
+    nc = X.shape[0]
+    dev = X.device
+    n = W.sum(1).to(torch.int32).contiguous()
+    out = torch.empty(nc, 6, 10, dtype=torch.float64, device=dev)
+    info = torch.empty(nc, 2, dtype=torch.int32, device=dev)
+    lbs = torch.empty(nc, dtype=torch.float64, device=dev)
+    ic = None
+    if init_centers is not None:
+        ic = (torch.as_tensor(np.asarray(init_centers, dtype=np.float64), device=dev)
+              - shift.unsqueeze(1)).contiguous()
+    L.vgm_fit(X.contiguous(), n, ic, int(seed) & ((1 << 62) - 1), WEIGHT_PRIOR, float(tol), REG_COVAR, int(max_iter),
+              300, out, info, lbs)
+    o = out.cpu().numpy()
+    fit_vgm_torch.last_info = info.cpu().numpy()
+    fit_vgm_torch.last_lower_bound = lbs.cpu().numpy()
+    return VGMBank(wc_a=o[:, 0], wc_b=o[:, 1], mean_precision=o[:, 2], means=o[:, 3] + shift.cpu().numpy()[:, None],
+                   dof=o[:, 4], covariances=o[:, 5])
+
+
 def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int | None = None, device=None,
-                  max_iter: int = MAX_ITER, tol: float = TOL, use_hip: bool | None = None) -> VGMBank:
+                  max_iter: int = MAX_ITER, tol: float = TOL, use_hip: bool | None = None,
+                  init_centers=None, fused: bool = True) -> VGMBank:
+    """init_centers: optional [n_cols, K] k-means centres (original units) to start from instead of
+    k-means++ seeding + Lloyd -- e.g. sklearn ``KMeans(10, n_init=1).fit(x).cluster_centers_``, which
+    makes the fit follow sklearn's ``BayesianGaussianMixture`` from the same initialisation."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
     dt = torch.float64
     X, W = _pad(columns, dev, dt)
     gen = torch.Generator(device=dev)
-    gen.manual_seed(int(seed) if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)).item()))
+    seed = int(seed) if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    gen.manual_seed(seed)
     counts = W.sum(1)
     shift = (X * W).sum(1) / counts                       # centre every column (prior mean 0)
     X = (X - shift.unsqueeze(1)) * W
     if use_hip is None:
         use_hip = dev.type == "cuda" and n_clusters == 10
+    if use_hip and fused:
+        return _fit_vgm_device(X, W, shift, seed, init_centers, max_iter, tol)
     passes = _HipPasses(X, W) if use_hip else _TorchPasses(X, W)
     pri = _State()
     pri.wprior = WEIGHT_PRIOR
@@ -202,7 +234,10 @@ def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int
     pri.cov0 = (X ** 2 * W).sum(1) / (counts - 1).clamp_min(1)
     eps10 = 10 * torch.finfo(dt).eps
     # init: hard k-means responsibilities -> first M-step
-    centers = kmeans_1d(X, W, n_clusters, gen, passes=passes)
+    if init_centers is not None:
+        centers = torch.as_tensor(np.asarray(init_centers, dtype=np.float64), device=dev) - shift.unsqueeze(1)
+    else:
+        centers = kmeans_1d(X, W, n_clusters, gen, passes=passes)
     s = _m_step(*passes.kmeans(centers), pri, eps10)
     lb = torch.full((X.shape[0],), -float("inf"), dtype=dt, device=dev)
     active = torch.ones(X.shape[0], dtype=torch.bool, device=dev)
@@ -219,6 +254,7 @@ def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int
         active = active & ~(change < tol)
         if not bool(active.any()):
             break
+    fit_vgm_torch.last_lower_bound = lb.detach().cpu().numpy()
     cpu = lambda t: t.detach().cpu().numpy().astype(np.float64)  # noqa: E731
     return VGMBank(wc_a=cpu(s.a), wc_b=cpu(s.b), mean_precision=cpu(s.beta),
                    means=cpu(s.means + shift.unsqueeze(1)), dof=cpu(s.dof), covariances=cpu(s.cov))

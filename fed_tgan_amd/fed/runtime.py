@@ -99,6 +99,9 @@ class FedConfig:
     # comes from the first client (`Server/dtds/distributed.py:789`).  "broadcast" = every rank
     # starts from the first client's weights.
     init: str = "independent"
+    # sample + write the epoch CSV every N rounds (and after the last); 1 = every round (reference)
+    csv_every: int = 1
+    csv_epochs: Optional[List[int]] = None  # if set: sample + write only these epochs (and the last)
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -441,8 +444,14 @@ class FedRuntime:
             aggregated = (epoch + 1) % max(int(self.cfg.e_interval), 1) == 0
             if aggregated:
                 self.aggregate(alive if self.cfg.drop_client_prob > 0 else None)
-        with self.timer.phase("sample_dump", self.device):
-            self.sample_round(epoch, aggregated)
+        every = max(int(self.cfg.csv_every), 1)
+        if self.cfg.csv_epochs is not None:
+            dump = epoch in self.cfg.csv_epochs or epoch + 1 == self.cfg.epochs
+        else:
+            dump = (epoch + 1) % every == 0 or epoch + 1 == self.cfg.epochs
+        if dump:
+            with self.timer.phase("sample_dump", self.device):
+                self.sample_round(epoch, aggregated)
         if self.device.type == "cuda":
             stream_sync(self.device)
         dt = time.time() - t0

@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 DATA = os.path.join(ROOT, "data", "raw", "Intrusion_test.csv")
 
 
-def make_split(out: str, n_clients: int = 2, seed: int = 2024):
+def make_split(out: str, n_clients: int = 2, seed: int = 2024, bootstrap_rows: int = 0):
     df = pd.read_csv(DATA)
     perm = np.random.default_rng(seed).permutation(len(df))
     n_tr = int(round(0.8 * len(df)))
@@ -46,12 +46,17 @@ def make_split(out: str, n_clients: int = 2, seed: int = 2024):
     train.to_csv(os.path.join(d, "train.csv"), index=False)
     hold.to_csv(os.path.join(d, "holdout.csv"), index=False)
     bounds = np.linspace(0, len(train), n_clients + 1).astype(int)
+    rng = np.random.default_rng(seed + 1)
     for i in range(n_clients):
-        train.iloc[bounds[i]:bounds[i + 1]].to_csv(os.path.join(d, f"client{i}.csv"), index=False)
+        part = train.iloc[bounds[i]:bounds[i + 1]]
+        if bootstrap_rows:   # resample with replacement to the reference's per-client size (steps/epoch)
+            part = part.iloc[rng.integers(0, len(part), bootstrap_rows)]
+        part.to_csv(os.path.join(d, f"client{i}.csv"), index=False)
     return os.path.join(d, "train.csv"), os.path.join(d, "holdout.csv"), os.path.join(d, "client{client}.csv")
 
 
-def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, clients: int, gmm: str):
+def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, clients: int, gmm: str,
+              csv_epochs=None):
     import torch
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.fed.local import run_local_emulation
@@ -60,6 +65,8 @@ def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, c
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = FedConfig(spec=intrusion_spec(), epochs=epochs, datapath=datapath, out_dir=out, n_sample=40000,
                     gmm_backend=gmm, seed=seed, engine=EngineConfig(precision=precision), verbose=False)
+    if csv_epochs is not None:      # long runs: only the scored epochs' tables are written
+        cfg.csv_epochs = sorted(set(csv_epochs))
     t0 = time.time()
     rt = run_local_emulation(cfg, clients, backend="auto", device=dev)
     return {"rows": rt.rows, "steps": rt.steps, "weights": [float(w) for w in rt.weights],
@@ -100,15 +107,20 @@ def main():
     ap.add_argument("--utility-workers", type=int, default=8)
     ap.add_argument("--keep-csv", action="store_true")
     ap.add_argument("--eval-epochs", type=int, nargs="*", default=None, help="epochs to score (default: all)")
+    ap.add_argument("--bootstrap-rows", type=int, default=0,
+                    help="resample every client's rows (with replacement) to this many: 20000 gives the "
+                         "reference's ~40 steps per client per epoch")
+    ap.add_argument("--only-scored-csv", action="store_true", help="write only the scored epochs' CSVs")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
-    train_path, hold_path, datapath = make_split(args.out, args.clients)
+    train_path, hold_path, datapath = make_split(args.out, args.clients, bootstrap_rows=args.bootstrap_rows)
     eval_epochs = [e for e in (args.eval_epochs or range(args.epochs)) if e < args.epochs]
     runs = []
     for prec in args.precisions:
         for seed in args.seeds:
             rd = os.path.join(args.out, f"run_{prec}_s{seed}")
-            info = train_run(rd, datapath, prec, seed, args.epochs, args.clients, args.gmm)
+            info = train_run(rd, datapath, prec, seed, args.epochs, args.clients, args.gmm,
+                             eval_epochs if args.only_scored_csv else None)
             sims = similarity(train_path, rd, eval_epochs)
             rec = {"precision": prec, "seed": seed, **info, "eval_epochs": eval_epochs, "avg_jsd": [s[0] for s in sims],
                    "avg_wd": [s[1] for s in sims]}
@@ -129,7 +141,7 @@ def main():
         summary[prec] = {"avg_jsd_mean": np.mean([r["avg_jsd"] for r in rs], axis=0).round(4).tolist(),
                          "avg_wd_mean": np.mean([r["avg_wd"] for r in rs], axis=0).round(4).tolist(),
                          "f1_gap_mean": float(np.mean([r["utility_final"]["f1_gap"] for r in rs])),
-                         "eval_epochs": eval_epochs,
+                         "eval_epochs": eval_epochs, "bootstrap_rows": args.bootstrap_rows,
                          "seeds": [r["seed"] for r in rs]}
     with open(os.path.join(args.out, "real_quality.json"), "w") as f:
         json.dump({"protocol": __doc__, "runs": runs, "summary": summary}, f, indent=1)
