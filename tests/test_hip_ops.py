@@ -362,11 +362,21 @@ def test_vgm_fit_hip_passes_match_torch(hip):
     rng = np.random.default_rng(0)
     cols = [np.concatenate([rng.normal(0, 1, 3000), rng.normal(8, 0.5, 2000)]), rng.exponential(3, 4500),
             rng.normal(100, 10, 5000), np.round(rng.lognormal(2, 1, 4000))]
-    a = fit_vgm_torch(cols, seed=1, device=DEV, use_hip=True)
+    a = fit_vgm_torch(cols, seed=1, device=DEV, use_hip=True, fused=False)
     b = fit_vgm_torch(cols, seed=1, device=DEV, use_hip=False)
     for f in ("wc_a", "wc_b", "mean_precision", "means", "dof", "covariances"):
         np.testing.assert_allclose(getattr(a, f), getattr(b, f), rtol=1e-5, atol=1e-7, err_msg=f)
     np.testing.assert_allclose(a.weights, b.weights, atol=1e-6)
+    # the fused whole-fit kernel from the same k-means centres: the same EM trajectory on the device
+    cen = np.stack([np.sort(np.quantile(c, np.linspace(0.05, 0.95, 10))) + 1e-3 * np.arange(10) for c in cols])
+    f = fit_vgm_torch(cols, seed=1, device=DEV, init_centers=cen)
+    t = fit_vgm_torch(cols, seed=1, device="cpu", init_centers=cen)
+    for fld in ("wc_a", "wc_b", "mean_precision", "means", "dof", "covariances"):
+        np.testing.assert_allclose(getattr(f, fld), getattr(t, fld), rtol=1e-5, atol=1e-7, err_msg=fld)
+    # and from its own device k-means++ seeding: a converged, valid fit
+    own = fit_vgm_torch(cols, seed=1, device=DEV)
+    assert np.isfinite(own.means).all() and (own.covariances > 0).all()
+    assert np.allclose(own.weights.sum(1), 1.0)
 
 
 def test_gemm_head_seed_and_weighted_colsum(hip):
