@@ -54,6 +54,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--check", action="store_true",
                     help="after the timed rounds: assert every rank holds a bit-identical aggregate and the "
                          "last epoch CSV has n_sample rows (reported as 'consistency')")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override for A/B measurements, e.g. --engine onehot=0")
     ap.add_argument("--force-dist", action="store_true",
                     help="build real process groups even for one rank (1 GPU: the aggregation runs as an "
                          "RCCL all-reduce on a one-rank communicator)")
@@ -142,9 +144,15 @@ def run_rank(args) -> None:
         out = comm.broadcast_object(out, src=0)
     os.makedirs(out, exist_ok=True)
     spec = intrusion_spec()
+    from fed_tgan_amd.models.engine import EngineConfig
+    ecfg = EngineConfig()
+    for kv in args.engine:
+        k, v = kv.split("=", 1)
+        cur = getattr(ecfg, k)
+        setattr(ecfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
     cfg = FedConfig(spec=spec, epochs=args.warmup + args.steps, synthetic_rows=args.rows, out_dir=out,
                     n_sample=args.n_sample, backend=args.backend, gmm_backend=args.gmm, seed=0,
-                    verbose=not args.quiet, async_csv=not args.sync_csv)
+                    verbose=not args.quiet, async_csv=not args.sync_csv, engine=ecfg)
     rt = FedRuntime(cfg, comm, device)
     rt.initialize()
     for ep in range(args.warmup):
@@ -203,6 +211,8 @@ def run_rank(args) -> None:
         }
         if consistency is not None:
             rec["consistency"] = consistency
+        if args.engine:
+            rec["engine_overrides"] = args.engine
         print(json.dumps(rec), flush=True)
     comm.destroy()
 

@@ -56,7 +56,9 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
           const optional<Tensor>& bn_gamma, const optional<Tensor>& bn_beta, const optional<Tensor>& bn_rm,
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
-          const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group) {
+          const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group,
+          const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
+          const optional<Tensor>& oh_off) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -115,6 +117,20 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.ldha = ld_of(*head_a);
     g.head_coef = cfp(*head_coef);
     g.head_v = cfp(*head_v);
+  }
+  if (oh_w.has_value() && oh_w->defined()) {
+    TORCH_CHECK(tb && !ta, "gemm: the one-hot block needs C = A B^T");
+    check_f32_2d(*oh_w, "oh_w");
+    TORCH_CHECK(oh_w->size(0) == N, "gemm: oh_w must be [N, C]");
+    TORCH_CHECK(oh_col.has_value() && oh_opt.has_value() && oh_off.has_value(), "gemm: one-hot needs col / opt / off");
+    for (const auto* t : {&*oh_col, &*oh_opt, &*oh_off})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(), "gemm: one-hot int32 tables");
+    TORCH_CHECK(oh_col->numel() >= M && oh_opt->numel() >= M, "gemm: one-hot col / opt need M entries");
+    g.oh_w = cfp(*oh_w);
+    g.oh_ld = ld_of(*oh_w);
+    g.oh_col = oh_col->data_ptr<int>();
+    g.oh_opt = oh_opt->data_ptr<int>();
+    g.oh_off = oh_off->data_ptr<int>();
   }
   // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
   // must be independent -- neither reads what the other writes); group 0: launch now
@@ -673,7 +689,8 @@ TORCH_LIBRARY(fedtgan, m) {
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
-      "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0) -> ()");
+      "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0, Tensor? oh_w=None, Tensor? oh_col=None, "
+      "Tensor? oh_opt=None, Tensor? oh_off=None) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

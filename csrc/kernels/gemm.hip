@@ -29,6 +29,9 @@
 //   EPI_MASK            out = v * ms
 //   EPI_RELU            out = max(v, 0)
 //   EPI_BN_EVAL_RELU    out = relu((v - rm) * rsqrt(rv + eps) * gamma + beta)   (eval BatchNorm)
+// One-hot conditional block (GemmArgs::oh_w): before the epilogue, v += the weight column of the
+// row's active condition -- the generator layers multiply only the dense part of [... | z | c]
+// and gather the c block's single non-zero product (c is 303 of G0's 431 input columns on Intrusion).
 #include <algorithm>
 #include <type_traits>
 
@@ -56,6 +59,11 @@ __device__ __forceinline__ void st_out(float* base, size_t idx, float v, int wt)
   } else {
     base[idx] = v;
   }
+}
+
+// the one-hot block's contribution to output (m, n): one gathered weight (see GemmArgs::oh_w)
+__device__ __forceinline__ float onehot_term(const GemmArgs& g, int m, int n) {
+  return g.oh_w[(size_t)n * g.oh_ld + g.oh_off[g.oh_col[m]] + g.oh_opt[m]];
 }
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
@@ -398,6 +406,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       float* cp = g.c + (size_t)m * g.ldc + n;
       if (g.beta != 0.f) v += g.beta * (*cp);
       if (g.bias) v += g.bias[n];
+      if (g.oh_w) v += onehot_term(g, m, n);
       st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
     }
     return;
@@ -420,6 +429,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
         if (g.bias) v += g.bias[n];
+      if (g.oh_w) v += onehot_term(g, m, n);
         st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
 }
@@ -485,6 +495,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
     float* cp = g.c + (size_t)m * g.ldc + n;
     if (g.beta != 0.f) v += g.beta * (*cp);
     if (g.bias) v += g.bias[n];
+    if (g.oh_w) v += onehot_term(g, m, n);
     st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, idx), g.wt);
   }
 }

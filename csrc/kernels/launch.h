@@ -44,6 +44,15 @@ struct GemmArgs {
   int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
   int xcd_remap;   // 1: XCD-contiguous tile order (set by launch_gemm)
   int wt;          // 1: write-through (sc1) output stores (set by launch_gemm)
+  // One-hot conditional block (nullable): the K columns of op(A) are only the DENSE part of the
+  // input; its trailing one-hot block (the conditional vector c, exactly one 1 per row at
+  // oh_off[oh_col[m]] + oh_opt[m]) is applied as a gather of one weight column per row in the
+  // epilogue: v += oh_w[n * oh_ld + oh_off[oh_col[m]] + oh_opt[m]]   (op(B) = B^T row-major weight)
+  const float* oh_w;
+  int oh_ld;
+  const int* oh_col;
+  const int* oh_opt;
+  const int* oh_off;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);

@@ -89,6 +89,9 @@ class EngineConfig:
     graph_unroll: int = 8       # GPU: training steps captured per hipGraph (fewer graph launches)
     streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
     paired: bool = True         # draw + generate the D- and G-phase batches of a step in one pass
+    # generator GEMMs multiply only the dense part of their input [... | z | c]; the one-hot
+    # conditional block c (exactly one 1 per row) is a gathered weight column in the epilogue
+    onehot: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -135,6 +138,8 @@ class CTGANEngine:
         self.c_cols = (off[0] + self.E, self.Hw)
         self.spans = [(int(s), int(w), int(k)) for s, w, k in zip(layout.start, layout.width, layout.kind)]
         self.cond_spans = [(int(s), int(w)) for s, w in zip(layout.cond_start, layout.cond_width)]
+        self.use_onehot = bool(cfg.onehot) and self.C > 0
+        self._cond_off = torch.as_tensor(np.asarray(layout.cond_offset, dtype=np.int32), device=self.device)
         self._build_params()
         self._build_buffers()
         # side streams ("lanes") for independent work inside a step; the captured graph keeps the
@@ -406,27 +411,41 @@ class CTGANEngine:
             return _ext(x, kp), _ext(W, kp)
         return x, W
 
-    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None, paired=False):
+    def _g_in(self, H, a: int, W: torch.Tensor, cond):
+        """GEMM operands of a generator layer reading H[:, a:]: (x, W, onehot).  With the row
+        conditions ``cond`` = (col, opt), x / W are only the DENSE columns (up to the conditional
+        block) and the one-hot block becomes the gather ``onehot`` (ops.gemm); else the full K."""
+        if cond is None or not self.use_onehot:
+            x, Wk = self._kpad(H, a, W)
+            return x, Wk, None
+        c0 = self.c_cols[0]
+        kd = c0 - a
+        return H[:, a:c0], W[:, :kd], (W[:, kd:], cond[0], cond[1], self._cond_off)
+
+    def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None, paired=False,
+                   cond=None):
         """Residual stack + output layer; with ``act_out`` the activation is fused onto the
         output GEMM (tanh / Gumbel-softmax into act_out, Philox stream ``stream_id``).
-        paired: H / logits hold both batches of a step (2B rows, BN statistics per batch)."""
+        paired: H / logits hold both batches of a step (2B rows, BN statistics per batch).
+        cond: the rows' (col, opt) int32 condition indices -- the conditional block of H is then
+        applied as a one-hot gather instead of a dense K range (``EngineConfig.onehot``)."""
         o = self.ops
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
-            x, W = self._kpad(H, a, self.p[f"G.{i}.W"])
+            x, W, oh = self._g_in(H, a, self.p[f"G.{i}.W"], cond)
             abuf, nh = (self.abuf2[i], self.nhat2[i]) if paired else (self.abuf[i], self.nhat[i])
             mean, istd = (self.bn_mean2[i], self.bn_invstd2[i]) if paired else (self.bn_mean[i], self.bn_invstd[i])
             o.linear_bn_relu(x, W, self.p[f"G.{i}.b"], self.p[f"G.{i}.gamma"],
                              self.p[f"G.{i}.beta"], H[:, b_:a],
                              abuf if nhat else None, nh if nhat else None,
                              mean, istd, self.p[f"G.{i}.rm"], self.p[f"G.{i}.rv"],
-                             training, self.cfg.bn_momentum, self.cfg.bn_eps, groups=2 if paired else 1)
-        x, W = self._kpad(H, 0, self.p["G.out.W"])
+                             training, self.cfg.bn_momentum, self.cfg.bn_eps, groups=2 if paired else 1, onehot=oh)
+        x, W, oh = self._g_in(H, 0, self.p["G.out.W"], cond)
         if act_out is None:
-            o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"])
+            o.gemm(x, W, logits, tb=True, bias=self.p["G.out.b"], onehot=oh)
         else:
             o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
-                              slerp=slerp)
+                              slerp=slerp, onehot=oh)
 
     def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None):
         """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
@@ -497,7 +516,7 @@ class CTGANEngine:
                        stream_id=1)
         # activation of the fake rows + slerp(real, fake) for the gradient penalty in one launch
         self._g_forward(self.H, self.logits, training=True, act_out=self.X_fake[:, :self.Dd], stream_id=2,
-                        slerp=(self.X_real, self.X_fake, self.X_interp, 3))
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), cond=(self.col, self.opt))
 
     def _prepare_paired(self):
         """Both phases' batches in one pass: one sampler launch draws the D-phase batch (with real
@@ -512,7 +531,7 @@ class CTGANEngine:
                        self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
                        zero_metrics=True, stream_id=1)
         self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
-                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True)
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True, cond=(self.col2, self.opt2))
 
     def _d_update(self):
         """D forward on the stacked rows, WGAN + GP backward, D Adam step."""
@@ -572,7 +591,8 @@ class CTGANEngine:
         o, B = self.ops, self.B
         o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xg, None, self.Dd,
                        self.col, self.opt, step_counter=self.stepG, stream_id=11)
-        self._g_forward(self.H, self.logits, training=True, act_out=self.Xg[:, :self.Dd], stream_id=12)
+        self._g_forward(self.H, self.logits, training=True, act_out=self.Xg[:, :self.Dd], stream_id=12,
+                        cond=(self.col, self.opt))
 
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
@@ -752,9 +772,9 @@ class CTGANEngine:
         out = torch.empty(n, self.Dd, device=self.device)
         for a in range(0, n, self.cfg.gen_chunk):
             b = min(n, a + self.cfg.gen_chunk)
-            H, logits = self._gen_buffers(b - a)
-            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, stream_id=21)
-            self._g_forward(H, logits, training=False, nhat=False)
+            H, logits, col, opt = self._gen_buffers(b - a)
+            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
+            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt))
             self.ops.activate(logits, out[a:b], self.spans, self.cfg.tau, stream_id=22)
         return out
 
@@ -780,9 +800,9 @@ class CTGANEngine:
     def _gen_pass(self, n: int, out: torch.Tensor, bufs):
         for a in range(0, n, self.cfg.gen_chunk):
             b = min(n, a + self.cfg.gen_chunk)
-            H, logits = bufs(b - a)
-            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, stream_id=21)
-            self._g_forward(H, logits, training=False, nhat=False)
+            H, logits, col, opt = bufs(b - a)
+            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
+            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt))
             self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23)
 
     def _capture_gen(self, n: int):
@@ -790,8 +810,9 @@ class CTGANEngine:
         from ..utils.devsync import CAPTURE_LOCK
         m = min(n, self.cfg.gen_chunk)
         H, lg = _padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device)
+        col, opt = (torch.zeros(m, dtype=torch.int32, device=self.device) for _ in range(2))
         out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
-        bufs = lambda k: (H[:k], lg[:k])  # noqa: E731
+        bufs = lambda k: (H[:k], lg[:k], col[:k], opt[:k])  # noqa: E731
         with CAPTURE_LOCK:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -802,12 +823,14 @@ class CTGANEngine:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
                 self._gen_pass(n, out, bufs)
-        self._gen_graphs[n] = (g, H, lg, out)
+        self._gen_graphs[n] = (g, H, lg, out, col, opt)
         return self._gen_graphs[n]
 
     def _gen_buffers(self, n: int):
         if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n:
             m = max(n, min(self.cfg.gen_chunk, n))
-            self._gen_bufs = (_padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device))
-        H, lg = self._gen_bufs
-        return H[:n], lg[:n]
+            self._gen_bufs = (_padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device),
+                              torch.zeros(m, dtype=torch.int32, device=self.device),
+                              torch.zeros(m, dtype=torch.int32, device=self.device))
+        H, lg, col, opt = self._gen_bufs
+        return H[:n], lg[:n], col[:n], opt[:n]

@@ -125,9 +125,11 @@ class HipOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0):
-        """C = epi(alpha op(A) op(B) + beta C + bias).  head = (coef [M], v [N], A_out [M, N]):
+             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None):
+        """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
+        onehot = (W_c [N, C], col [M], opt [M], cond_offset): A holds only the dense input columns; the
+        trailing one-hot block contributes W_c[n, cond_offset[col[m]] + opt[m]] (a gather, no MFMA).
         group 1 holds this GEMM, group 2 launches it together with the held one in ONE kernel (the
         two must be independent); 0 launches now."""
         M = a.shape[1] if ta else a.shape[0]
@@ -143,20 +145,22 @@ class HipOps:
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
-                    float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group))
+                    float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group),
+                    *(onehot or (None, None, None, None)))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
-                       momentum=0.1, eps=1e-5, groups=1):
+                       momentum=0.1, eps=1e-5, groups=1, onehot=None):
         """groups = 2: the rows are two batches (BN statistics per batch, running stats updated
-        batch after batch); mean / invstd are then [2, cols]."""
+        batch after batch); mean / invstd are then [2, cols].  onehot: see gemm."""
         if training:
             # (fusing the split-K reduction into this BN launch was measured slower: the BN grid
             # has only cols/16 workgroups to pull the slabs -- profiles/README.md)
-            self.gemm(x, W, abuf, tb=True, bias=b)
+            self.gemm(x, W, abuf, tb=True, bias=b, onehot=onehot)
             self.L.bn_relu_train(abuf, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps),
                                  int(groups))
         else:
-            self.gemm(x, W, out, tb=True, bias=b, epi=EPI_BN_EVAL_RELU, bn=(gamma, beta, rmean, rvar), bn_eps=eps)
+            self.gemm(x, W, out, tb=True, bias=b, epi=EPI_BN_EVAL_RELU, bn=(gamma, beta, rmean, rvar), bn_eps=eps,
+                      onehot=onehot)
 
     def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
                     eps=1e-5, groups=1):
@@ -205,9 +209,9 @@ class HipOps:
         self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16, sr, so,
                         cols, ss)
 
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None):
         """logits = x W^T + b; out = activate(logits) (optionally + the fused slerp)."""
-        self.gemm(x, W, logits, tb=True, bias=b)
+        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot)
         self.activate(logits, out, spans, tau, stream_id, slerp=slerp)
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):

@@ -29,8 +29,11 @@ class TorchOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0):
-        """c = epi(alpha * op(a) @ op(b) + beta * c + bias)."""
+             slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0, onehot=None):
+        """c = epi(alpha * op(a) @ op(b) + beta * c + bias [+ onehot]).
+
+        onehot = (W_c [N, C], col [M], opt [M], cond_offset): a holds only the dense input columns and
+        the one-hot conditional block adds W_c[:, cond_offset[col[m]] + opt[m]] to row m."""
         A = a.t() if ta else a
         B = b.t() if tb else b
         acc = torch.matmul(A, B)
@@ -40,6 +43,11 @@ class TorchOps:
             acc = acc + beta * c
         if bias is not None:
             acc = acc + bias
+        if onehot is not None:
+            w_c, col, opt, off = onehot
+            m = acc.shape[0]
+            idx = (off.long()[col[:m].long()] + opt[:m].long())
+            acc = acc + w_c[:, idx].t()
         if epi == EPI_LRELU_DROPOUT:
             keep = (torch.rand(acc.shape, device=acc.device) >= p_drop).to(acc.dtype) / (1.0 - p_drop)
             s = torch.where(acc > 0, torch.ones_like(acc), torch.full_like(acc, slope))
@@ -117,6 +125,9 @@ class TorchOps:
         opt = (t["cdf_emp"][col] > u).to(torch.int32).argmax(1)
         opt = torch.minimum(opt, t["cond_width"][col].long() - 1)
         c.scatter_(1, (t["cond_offset"][col].long() + opt).view(-1, 1), 1.0)
+        if col_out is not None:
+            col_out[:B].copy_(col.to(col_out.dtype))
+            opt_out[:B].copy_(opt.to(opt_out.dtype))
 
     # ------------------------------------------------------------------ batch norm + relu
     def bn_relu_fwd(self, a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training=True, momentum=0.1,
@@ -149,9 +160,12 @@ class TorchOps:
         out.copy_(torch.relu(nh * gamma + beta))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
-                       momentum=0.1, eps=1e-5, groups=1):
+                       momentum=0.1, eps=1e-5, groups=1, onehot=None):
         """out = relu(BN(x @ W^T + b)); training mode uses batch statistics and updates running ones."""
         a = torch.addmm(b, x, W.t())
+        if onehot is not None:
+            w_c, col, opt, off = onehot
+            a = a + w_c[:, off.long()[col[:a.shape[0]].long()] + opt[:a.shape[0]].long()].t()
         self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps, groups)
 
     def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
@@ -166,8 +180,8 @@ class TorchOps:
             dbias.copy_(da.sum(0))
 
     # ------------------------------------------------------------------ activations
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
-        self.gemm(x, W, logits, tb=True, bias=b)
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None):
+        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot)
         self.activate(logits, out, spans, tau, stream_id=stream_id)
         if slerp is not None:
             real, fake_full, interp, sid = slerp

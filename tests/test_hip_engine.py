@@ -175,3 +175,27 @@ def test_large_batches_train(batch):
     torch.cuda.synchronize()
     assert np.isfinite(eng.losses()).all() and bool(torch.isfinite(eng.flat).all())
     assert g0 == out.shape[1]
+
+
+def test_onehot_generator_matches_dense():
+    """EngineConfig.onehot: the generator's conditional block applied as a gather gives the same
+    paired forward (logits, BN statistics) and the same generation tables as the dense K range."""
+    from fed_tgan_amd.models.samplers import CondTables
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    outs = []
+    for oh in (True, False):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32", onehot=oh), DEV, backend="hip",
+                          seed=9)
+        eng.set_training_data(X)
+        eng._prepare_paired()
+        eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+        enc = eng.generate_encoded(3000)
+        torch.cuda.synchronize()
+        outs.append((eng.logits2.clone(), eng.bn_mean2[0].clone(), eng.p["G.1.rv"].clone(), enc))
+    (la, ma, va, ea), (lb, mb, vb, eb) = outs
+    assert torch.allclose(la, lb, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(ma, mb, atol=1e-5, rtol=1e-5) and torch.allclose(va, vb, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(ea, eb, atol=1e-3)     # same Philox draws: identical up to GEMM rounding

@@ -714,3 +714,35 @@ def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
         torch.cuda.synchronize()
         res.append(out)
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("tile", [32, 64, 128])
+@pytest.mark.parametrize("bn", [False, True])
+def test_gemm_onehot_gather_matches_dense(hip32, tile, bn):
+    """The one-hot conditional block as an epilogue gather (GemmArgs::oh_w) equals the dense product
+    over [dense | one-hot] columns, incl. the eval-BN epilogue and the 128-tile LDS epilogue."""
+    M, Kd, N = 700, 200, 96
+    widths = [3, 7, 1, 12, 5]
+    C = sum(widths)
+    off = torch.tensor(np.cumsum([0] + widths[:-1]), dtype=torch.int32, device=DEV)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    col = torch.randint(0, len(widths), (M,), generator=g)
+    opt = torch.tensor([int(torch.randint(0, widths[c], (1,), generator=g)) for c in col], dtype=torch.int32)
+    H = torch.zeros(M, Kd + C, device=DEV)
+    H[:, :Kd] = mat(M, Kd, seed=60)
+    H[torch.arange(M), Kd + off.cpu()[col].long() + opt.long()] = 1.0
+    W = mat(N, Kd + C, seed=61)
+    bias = mat(N, seed=62)
+    col, opt = col.to(torch.int32).to(DEV), opt.to(DEV)
+    hip32.tile_override = tile
+    kw = {}
+    if bn:
+        kw = dict(epi=4, bn=(torch.rand(N, device=DEV) + 0.5, mat(N, seed=63), mat(N, seed=64),
+                             torch.rand(N, device=DEV) + 0.5))
+    dense = torch.zeros(M, N, device=DEV)
+    hip32.gemm(H, W, dense, tb=True, bias=bias, **kw)
+    gath = torch.zeros(M, N, device=DEV)
+    hip32.gemm(H[:, :Kd], W[:, :Kd], gath, tb=True, bias=bias, onehot=(W[:, Kd:], col, opt, off), **kw)
+    torch.cuda.synchronize()
+    hip32.tile_override = None
+    assert torch.allclose(gath, dense, atol=2e-4, rtol=1e-5)

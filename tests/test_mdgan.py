@@ -49,8 +49,10 @@ class QueueP2P:
 def _engine(tr, X=None):
     torch.manual_seed(0)
     # per-phase step order: the split mode draws each phase's batch when it runs, and the fused
-    # reference must consume torch's global RNG in that same order
-    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=100, paired=False), "cpu", backend="torch", seed=3)
+    # reference must consume torch's global RNG in that same order.  The split server receives only
+    # [z | c] (no row conditions), so its generator multiplies c densely: the fused reference does too
+    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=100, paired=False, onehot=False), "cpu", backend="torch",
+                      seed=3)
     if X is not None:
         eng.set_training_data(X)
     return eng

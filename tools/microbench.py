@@ -42,6 +42,25 @@ def step_only(eng, dev):
         print(f"full step: side lanes {a:8.2f} us   one stream {b:8.2f} us")
 
 
+def onehot_ab(eng, tr, X, dev):
+    """EngineConfig.onehot A/B: full captured step and generate_decoded(40000), dense K vs gathered c."""
+    from fed_tgan_amd.models.samplers import CondTables
+    eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+    for rep in range(2):
+        for oh in (False, True):
+            eng.use_onehot = oh
+            eng._gen_graphs = {}
+            t_step = per_call(eng._one_step, dev, n=5, reps=20)
+            eng.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for _ in range(20):
+                eng.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            t_gen = (time.perf_counter() - t) / 20 * 1e6
+            print(f"onehot={int(oh)}: full step {t_step:8.2f} us   generate_decoded(40000) {t_gen:8.1f} us", flush=True)
+
+
 def gen_only(eng, tr, X, dev):
     """generate_decoded(40000): eager vs hipGraph, chunk 8192 vs one chunk (wall time per call)."""
     from fed_tgan_amd.models.samplers import CondTables
@@ -119,6 +138,7 @@ def main():
     ap.add_argument("--store-sweep", action="store_true", help="GEMM output stores: plain / write-through")
     ap.add_argument("--fold-sweep", action="store_true", help="column sums: own launch / folded into Adam")
     ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
+    ap.add_argument("--onehot-ab", action="store_true", help="step + generation: dense c block vs one-hot gather")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -133,6 +153,8 @@ def main():
         return step_only(eng, dev)
     if args.gen:
         return gen_only(eng, tr, X, dev)
+    if args.onehot_ab:
+        return onehot_ab(eng, tr, X, dev)
     if args.unroll:
         return unroll_sweep(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
