@@ -58,7 +58,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
           const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group,
           const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
-          const optional<Tensor>& oh_off) {
+          const optional<Tensor>& oh_off, bool oh_trans) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -121,7 +121,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   if (oh_w.has_value() && oh_w->defined()) {
     TORCH_CHECK(tb && !ta, "gemm: the one-hot block needs C = A B^T");
     check_f32_2d(*oh_w, "oh_w");
-    TORCH_CHECK(oh_w->size(0) == N, "gemm: oh_w must be [N, C]");
+    TORCH_CHECK(oh_trans ? oh_w->size(1) == N : oh_w->size(0) == N, "gemm: oh_w must be [N, C] (or [C, N] transposed)");
+    g.oh_trans = oh_trans ? 1 : 0;
     TORCH_CHECK(oh_col.has_value() && oh_opt.has_value() && oh_off.has_value(), "gemm: one-hot needs col / opt / off");
     for (const auto* t : {&*oh_col, &*oh_opt, &*oh_off})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(), "gemm: one-hot int32 tables");
@@ -690,7 +691,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
       "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0, Tensor? oh_w=None, Tensor? oh_col=None, "
-      "Tensor? oh_opt=None, Tensor? oh_off=None) -> ()");
+      "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

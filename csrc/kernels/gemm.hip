@@ -63,7 +63,8 @@ __device__ __forceinline__ void st_out(float* base, size_t idx, float v, int wt)
 
 // the one-hot block's contribution to output (m, n): one gathered weight (see GemmArgs::oh_w)
 __device__ __forceinline__ float onehot_term(const GemmArgs& g, int m, int n) {
-  return g.oh_w[(size_t)n * g.oh_ld + g.oh_off[g.oh_col[m]] + g.oh_opt[m]];
+  const int idx = g.oh_off[g.oh_col[m]] + g.oh_opt[m];
+  return g.oh_trans ? g.oh_w[(size_t)idx * g.oh_ld + n] : g.oh_w[(size_t)n * g.oh_ld + idx];
 }
 
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {

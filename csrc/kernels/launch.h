@@ -50,6 +50,8 @@ struct GemmArgs {
   // epilogue: v += oh_w[n * oh_ld + oh_off[oh_col[m]] + oh_opt[m]]   (op(B) = B^T row-major weight)
   const float* oh_w;
   int oh_ld;
+  int oh_trans;   // 1: oh_w is the transposed block [C, N] (coalesced gathers: lanes of a row read
+                  //    consecutive n) -- v += oh_w[(oh_off[oh_col[m]] + oh_opt[m]) * oh_ld + n]
   const int* oh_col;
   const int* oh_opt;
   const int* oh_off;

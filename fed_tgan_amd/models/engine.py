@@ -92,6 +92,7 @@ class EngineConfig:
     # generator GEMMs multiply only the dense part of their input [... | z | c]; the one-hot
     # conditional block c (exactly one 1 per row) is a gathered weight column in the epilogue
     onehot: bool = True
+    onehot_trans: bool = False   # training: gather from per-step [C, N] copies (A/B knob; generation always does)
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -413,13 +414,17 @@ class CTGANEngine:
 
     def _g_in(self, H, a: int, W: torch.Tensor, cond):
         """GEMM operands of a generator layer reading H[:, a:]: (x, W, onehot).  With the row
-        conditions ``cond`` = (col, opt), x / W are only the DENSE columns (up to the conditional
-        block) and the one-hot block becomes the gather ``onehot`` (ops.gemm); else the full K."""
+        conditions ``cond`` = (col, opt[, transposed]), x / W are only the DENSE columns (up to the
+        conditional block) and the one-hot block becomes the gather ``onehot`` (ops.gemm); else the
+        full K.  transposed: gather from a [C, N] copy of the block made here (generation: 40k rows,
+        where strided gathers from the [N, C] weight cost more than the K they save)."""
         if cond is None or not self.use_onehot:
             x, Wk = self._kpad(H, a, W)
             return x, Wk, None
         c0 = self.c_cols[0]
         kd = c0 - a
+        if len(cond) > 2 and cond[2]:
+            return H[:, a:c0], W[:, :kd], (W[:, kd:].t().contiguous(), cond[0], cond[1], self._cond_off, True)
         return H[:, a:c0], W[:, :kd], (W[:, kd:], cond[0], cond[1], self._cond_off)
 
     def _g_forward(self, H, logits, training: bool, nhat=True, act_out=None, stream_id=0, slerp=None, paired=False,
@@ -516,7 +521,8 @@ class CTGANEngine:
                        stream_id=1)
         # activation of the fake rows + slerp(real, fake) for the gradient penalty in one launch
         self._g_forward(self.H, self.logits, training=True, act_out=self.X_fake[:, :self.Dd], stream_id=2,
-                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), cond=(self.col, self.opt))
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3),
+                        cond=(self.col, self.opt, self.cfg.onehot_trans))
 
     def _prepare_paired(self):
         """Both phases' batches in one pass: one sampler launch draws the D-phase batch (with real
@@ -531,7 +537,8 @@ class CTGANEngine:
                        self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
                        zero_metrics=True, stream_id=1)
         self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
-                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True, cond=(self.col2, self.opt2))
+                        slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True,
+                        cond=(self.col2, self.opt2, self.cfg.onehot_trans))
 
     def _d_update(self):
         """D forward on the stacked rows, WGAN + GP backward, D Adam step."""
@@ -592,7 +599,7 @@ class CTGANEngine:
         o.sample_train(self.tables, self.H, self.z_cols, self.c_cols, self.Xg, None, self.Dd,
                        self.col, self.opt, step_counter=self.stepG, stream_id=11)
         self._g_forward(self.H, self.logits, training=True, act_out=self.Xg[:, :self.Dd], stream_id=12,
-                        cond=(self.col, self.opt))
+                        cond=(self.col, self.opt, self.cfg.onehot_trans))
 
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
@@ -774,7 +781,7 @@ class CTGANEngine:
             b = min(n, a + self.cfg.gen_chunk)
             H, logits, col, opt = self._gen_buffers(b - a)
             self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
-            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt))
+            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt, True))
             self.ops.activate(logits, out[a:b], self.spans, self.cfg.tau, stream_id=22)
         return out
 
@@ -802,7 +809,7 @@ class CTGANEngine:
             b = min(n, a + self.cfg.gen_chunk)
             H, logits, col, opt = bufs(b - a)
             self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
-            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt))
+            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt, True))
             self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23)
 
     def _capture_gen(self, n: int):

@@ -128,8 +128,9 @@ class HipOps:
              slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None):
         """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
-        onehot = (W_c [N, C], col [M], opt [M], cond_offset): A holds only the dense input columns; the
-        trailing one-hot block contributes W_c[n, cond_offset[col[m]] + opt[m]] (a gather, no MFMA).
+        onehot = (W_c [N, C], col [M], opt [M], cond_offset[, transposed]): A holds only the dense input
+        columns; the trailing one-hot block contributes W_c[n, cond_offset[col[m]] + opt[m]] (a gather, no
+        MFMA).  transposed: W_c is given as [C, N] (contiguous rows: coalesced gathers).
         group 1 holds this GEMM, group 2 launches it together with the held one in ONE kernel (the
         two must be independent); 0 launches now."""
         M = a.shape[1] if ta else a.shape[0]
@@ -146,7 +147,8 @@ class HipOps:
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
                     float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group),
-                    *(onehot or (None, None, None, None)))
+                    *(onehot[:4] if onehot else (None, None, None, None)),
+                    bool(onehot is not None and len(onehot) > 4 and onehot[4]))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):

@@ -44,7 +44,9 @@ class TorchOps:
         if bias is not None:
             acc = acc + bias
         if onehot is not None:
-            w_c, col, opt, off = onehot
+            w_c, col, opt, off = onehot[:4]
+            if len(onehot) > 4 and onehot[4]:
+                w_c = w_c.t()
             m = acc.shape[0]
             idx = (off.long()[col[:m].long()] + opt[:m].long())
             acc = acc + w_c[:, idx].t()
@@ -164,7 +166,9 @@ class TorchOps:
         """out = relu(BN(x @ W^T + b)); training mode uses batch statistics and updates running ones."""
         a = torch.addmm(b, x, W.t())
         if onehot is not None:
-            w_c, col, opt, off = onehot
+            w_c, col, opt, off = onehot[:4]
+            if len(onehot) > 4 and onehot[4]:
+                w_c = w_c.t()
             a = a + w_c[:, off.long()[col[:a.shape[0]].long()] + opt[:a.shape[0]].long()].t()
         self.bn_relu_fwd(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, training, momentum, eps, groups)
 

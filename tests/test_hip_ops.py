@@ -716,9 +716,10 @@ def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
     assert torch.equal(res[0], res[1])
 
 
+@pytest.mark.parametrize("trans", [False, True])
 @pytest.mark.parametrize("tile", [32, 64, 128])
 @pytest.mark.parametrize("bn", [False, True])
-def test_gemm_onehot_gather_matches_dense(hip32, tile, bn):
+def test_gemm_onehot_gather_matches_dense(hip32, tile, bn, trans):
     """The one-hot conditional block as an epilogue gather (GemmArgs::oh_w) equals the dense product
     over [dense | one-hot] columns, incl. the eval-BN epilogue and the 128-tile LDS epilogue."""
     M, Kd, N = 700, 200, 96
@@ -742,7 +743,8 @@ def test_gemm_onehot_gather_matches_dense(hip32, tile, bn):
     dense = torch.zeros(M, N, device=DEV)
     hip32.gemm(H, W, dense, tb=True, bias=bias, **kw)
     gath = torch.zeros(M, N, device=DEV)
-    hip32.gemm(H[:, :Kd], W[:, :Kd], gath, tb=True, bias=bias, onehot=(W[:, Kd:], col, opt, off), **kw)
+    oh = (W[:, Kd:].t().contiguous(), col, opt, off, True) if trans else (W[:, Kd:], col, opt, off)
+    hip32.gemm(H[:, :Kd], W[:, :Kd], gath, tb=True, bias=bias, onehot=oh, **kw)
     torch.cuda.synchronize()
     hip32.tile_override = None
     assert torch.allclose(gath, dense, atol=2e-4, rtol=1e-5)

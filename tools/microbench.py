@@ -47,8 +47,9 @@ def onehot_ab(eng, tr, X, dev):
     from fed_tgan_amd.models.samplers import CondTables
     eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
     for rep in range(2):
-        for oh in (False, True):
+        for oh, tr_ in ((False, False), (True, False), (True, True)):
             eng.use_onehot = oh
+            eng.cfg.onehot_trans = tr_
             eng._gen_graphs = {}
             t_step = per_call(eng._one_step, dev, n=5, reps=20)
             eng.generate_decoded(40000)
@@ -58,7 +59,8 @@ def onehot_ab(eng, tr, X, dev):
                 eng.generate_decoded(40000)
             torch.cuda.synchronize(dev)
             t_gen = (time.perf_counter() - t) / 20 * 1e6
-            print(f"onehot={int(oh)}: full step {t_step:8.2f} us   generate_decoded(40000) {t_gen:8.1f} us", flush=True)
+            print(f"onehot={int(oh)} train_transposed={int(tr_)}: full step {t_step:8.2f} us   "
+                  f"generate_decoded(40000) {t_gen:8.1f} us", flush=True)
 
 
 def gen_only(eng, tr, X, dev):
