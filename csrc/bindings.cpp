@@ -120,6 +120,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   }
   if (oh_w.has_value() && oh_w->defined()) {
     TORCH_CHECK(tb && !ta, "gemm: the one-hot block needs C = A B^T");
+    TORCH_CHECK(alpha == 1.0, "gemm: the one-hot block needs alpha = 1 (it is folded into the accumulators)");
     check_f32_2d(*oh_w, "oh_w");
     TORCH_CHECK(oh_trans ? oh_w->size(1) == N : oh_w->size(0) == N, "gemm: oh_w must be [N, C] (or [C, N] transposed)");
     g.oh_trans = oh_trans ? 1 : 0;

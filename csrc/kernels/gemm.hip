@@ -378,6 +378,29 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
   }
 
+  // one-hot block (alpha == 1, checked on the host): every gathered weight of this lane's outputs is
+  // loaded in one unrolled loop with no global store in between (all loads in flight together, one
+  // memory round trip) and folded into the accumulators before the epilogue.  Split-K slabs leave it
+  // to gemm_splitk_epilogue.
+  if (g.oh_w && gz == 1) {
+    int rows[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = min(m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r, g.M - 1);
+        rows[i][r] = g.oh_off[g.oh_col[m]] + g.oh_opt[m];
+      }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = min(n0 + wn * WN + j * 16 + (lane & 15), g.N - 1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[i][j][r] += g.oh_trans ? g.oh_w[(size_t)rows[i][r] * g.oh_ld + n] : g.oh_w[(size_t)n * g.oh_ld + rows[i][r]];
+      }
+  }
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   if constexpr (TM >= 128) {
     // 64 accumulators per lane: a fully unrolled epilogue (Philox, loads, stores per element) is
@@ -407,7 +430,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       float* cp = g.c + (size_t)m * g.ldc + n;
       if (g.beta != 0.f) v += g.beta * (*cp);
       if (g.bias) v += g.bias[n];
-      if (g.oh_w) v += onehot_term(g, m, n);
       st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
     }
     return;
@@ -430,7 +452,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
         if (g.bias) v += g.bias[n];
-      if (g.oh_w) v += onehot_term(g, m, n);
         st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
 }
