@@ -58,7 +58,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
           const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group,
           const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
-          const optional<Tensor>& oh_off, bool oh_trans) {
+          const optional<Tensor>& oh_off, bool oh_trans, const optional<Tensor>& bn_part, int64_t bn_rpg) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -133,6 +133,17 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.oh_col = oh_col->data_ptr<int>();
     g.oh_opt = oh_opt->data_ptr<int>();
     g.oh_off = oh_off->data_ptr<int>();
+  }
+  if (bn_part.has_value() && bn_part->defined()) {
+    TORCH_CHECK(tb && !ta && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && g.splitk == 1 &&
+                    (tile == 32 || tile == 64) && group == 0,
+                "gemm: BN partials need a plain unsplit C = A B^T + bias on 32/64 tiles");
+    const int64_t tiles = (M + tile - 1) / tile;
+    TORCH_CHECK(bn_part->is_cuda() && bn_part->scalar_type() == at::kFloat && bn_part->is_contiguous() &&
+                    bn_part->numel() >= tiles * 6 * N, "gemm: bn_part must hold [m_tiles, 2, 3, N] floats");
+    TORCH_CHECK(bn_rpg >= 1 && bn_rpg <= M, "gemm: bn_rpg");
+    g.bn_part = fp(*bn_part);
+    g.bn_rpg = (int)bn_rpg;
   }
   // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
   // must be independent -- neither reads what the other writes); group 0: launch now
@@ -381,6 +392,26 @@ void bn_relu_train(const Tensor& a, const Tensor& gamma, const Tensor& beta, con
   fedtgan::launch_bn_relu_train(cfp(a), ld_of(a), cfp(gamma), cfp(beta), fp(out), ld_of(out), fp(nhat), ld_of(nhat),
                                 fp(mean), fp(invstd), fp(rm), fp(rv), (int)a.size(0), (int)a.size(1), (int)groups,
                                 (float)momentum, (float)eps, cur_stream());
+}
+
+void bn_relu_apply(const Tensor& a, const Tensor& part, int64_t n_tiles, const Tensor& gamma, const Tensor& beta,
+                   const Tensor& out, const Tensor& nhat, const Tensor& mean, const Tensor& invstd, const Tensor& rm,
+                   const Tensor& rv, double momentum, double eps, int64_t groups) {
+  check_f32_2d(a, "a");
+  check_f32_2d(out, "out");
+  check_f32_2d(nhat, "nhat");
+  const int64_t rows = a.size(0), cols = a.size(1);
+  TORCH_CHECK(groups == 1 || groups == 2, "bn_relu_apply: 1 or 2 batches");
+  TORCH_CHECK(rows >= 1 && rows % groups == 0, "bn_relu_apply: rows must split evenly");
+  TORCH_CHECK(out.sizes() == a.sizes() && nhat.sizes() == a.sizes() && gamma.numel() == cols && beta.numel() == cols &&
+                  rm.numel() == cols && rv.numel() == cols, "bn_relu_apply: shapes");
+  TORCH_CHECK(mean.is_contiguous() && invstd.is_contiguous() && mean.numel() == groups * cols &&
+                  invstd.numel() == groups * cols, "bn_relu_apply: mean/invstd must be contiguous [groups, cols]");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() >= n_tiles * 6 * cols && n_tiles >= 1, "bn_relu_apply: partials [n_tiles, 2, 3, cols]");
+  fedtgan::launch_bn_relu_apply(cfp(a), ld_of(a), cfp(part), (int)n_tiles, cfp(gamma), cfp(beta), fp(out), ld_of(out),
+                                fp(nhat), ld_of(nhat), fp(mean), fp(invstd), fp(rm), fp(rv), (int)rows, (int)cols,
+                                (int)groups, (float)momentum, (float)eps, cur_stream());
 }
 
 void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Tensor& gamma, const Tensor& invstd,
@@ -692,7 +723,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
       "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0, Tensor? oh_w=None, Tensor? oh_col=None, "
-      "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False) -> ()");
+      "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False, Tensor(f!)? bn_part=None, int bn_rpg=0) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
@@ -717,6 +748,9 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
       "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
+  m.def(
+      "bn_relu_apply(Tensor a, Tensor part, int n_tiles, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, "
+      "Tensor(c!) mean, Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
   m.def(
       "bn_relu_bwd(Tensor dr, Tensor r, Tensor nhat, Tensor gamma, Tensor invstd, Tensor(a!) da, Tensor(b!) dgamma, "
       "Tensor(c!) dbeta, Tensor(d!)? dbias) -> ()");
@@ -762,6 +796,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("colsum_ex", &colsum_ex);
   m.impl("bn_relu_train", &bn_relu_train);
   m.impl("bn_relu_bwd", &bn_relu_bwd);
+  m.impl("bn_relu_apply", &bn_relu_apply);
   m.impl("adam", &adam);
   m.impl("adam_cs", &adam_cs);
   m.impl("sample_decode", &sample_decode);

@@ -1188,6 +1188,104 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
   }
 }
 
+// BatchNorm(train) + ReLU from the producing GEMM's per-tile partial statistics (GemmArgs::bn_part):
+// no reduction over the batch's rows here, so the rows split over many workgroups -- a workgroup
+// owns 16 columns x 128 rows (one float4 per thread) instead of 8 columns x every row.
+//   1. wave w merges the tile triples (count, mean, M2) of columns 2w, 2w+1 for both batches with
+//      Chan's formula, lanes over tiles then a butterfly; lane 0's result is the statistic;
+//   2. row block 0 updates the running statistics (batch after batch, like the reference's two
+//      forward passes) and writes mean / invstd;
+//   3. every thread normalises one float4 of its row and writes nhat and relu(gamma nhat + beta).
+constexpr int BNA_THREADS = 512, BNA_COLS = 16, BNA_ROWS = 128;
+
+__device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
+  const float nt = n + nb;
+  if (nt > 0.f) {
+    const float d = mub - mu;
+    mu += d * (nb / nt);
+    m2 += m2b + d * d * (n * nb / nt);
+    n = nt;
+  }
+}
+
+__global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
+    const float* __restrict__ a, int lda, const float* __restrict__ part, int n_tiles, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn,
+    float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows,
+    int cols, int groups, float momentum, float eps) {
+  __shared__ float st[BNA_COLS][2][2];   // [col][batch] = (mean, invstd)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int c0 = blockIdx.x * BNA_COLS;
+  const int rpg = rows / groups;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int cl = 2 * w + q, c = c0 + cl;
+    float res[2][2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float n = 0.f, mu = 0.f, m2 = 0.f;
+      if (c < cols) {
+        for (int tile = lane; tile < n_tiles; tile += 64) {
+          const float* p = part + ((size_t)(tile * 2 + b) * 3) * cols + c;
+          chan_merge(n, mu, m2, p[0], p[cols], p[2 * (size_t)cols]);
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float nb = __shfl_xor(n, o, 64), mub = __shfl_xor(mu, o, 64), m2b = __shfl_xor(m2, o, 64);
+        chan_merge(n, mu, m2, nb, mub, m2b);
+      }
+      const float var = n > 0.f ? fmaxf(m2 / n, 0.f) : 0.f;
+      res[b][0] = mu;
+      res[b][1] = rsqrtf(var + eps);
+      if (lane == 0 && c < cols) {
+        st[cl][b][0] = mu;
+        st[cl][b][1] = res[b][1];
+        if (blockIdx.y == 0 && b < groups) {
+          mean[(size_t)b * cols + c] = mu;
+          invstd[(size_t)b * cols + c] = res[b][1];
+        }
+      }
+      res[b][0] = var;   // reuse: biased variance for the running update
+    }
+    if (lane == 0 && c < cols && blockIdx.y == 0) {
+      const float unb = (float)rpg / (float)max(rpg - 1, 1);
+      float m = rm[c], v = rv[c];
+      m = (1.f - momentum) * m + momentum * st[cl][0][0];
+      v = (1.f - momentum) * v + momentum * res[0][0] * unb;
+      if (groups > 1) {
+        m = (1.f - momentum) * m + momentum * st[cl][1][0];
+        v = (1.f - momentum) * v + momentum * res[1][0] * unb;
+      }
+      rm[c] = m;
+      rv[c] = v;
+    }
+  }
+  __syncthreads();
+  const int r = blockIdx.y * BNA_ROWS + (t >> 2);
+  const int cq = (t & 3) * 4;
+  if (r >= rows) return;
+  const int b = (groups > 1 && r >= rpg) ? 1 : 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int cl = cq + e, c = c0 + cl;
+    if (c >= cols) break;
+    const float nv = (a[(size_t)r * lda + c] - st[cl][b][0]) * st[cl][b][1];
+    nhat[(size_t)r * ldn + c] = nv;
+    const float y = nv * gamma[c] + beta[c];
+    out[(size_t)r * ldo + c] = y > 0.f ? y : 0.f;
+  }
+}
+
+void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tiles, const float* gamma,
+                          const float* beta, float* out, int ldo, float* nhat, int ldn, float* mean, float* invstd,
+                          float* rm, float* rv, int rows, int cols, int groups, float momentum, float eps,
+                          hipStream_t stream) {
+  const dim3 grid((cols + BNA_COLS - 1) / BNA_COLS, (rows + BNA_ROWS - 1) / BNA_ROWS);
+  hipLaunchKernelGGL(bn_relu_apply_kernel, grid, dim3(BNA_THREADS), 0, stream, a, lda, part, n_tiles, gamma, beta,
+                     out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps);
+}
+
 template <int COLS>
 static void bn_train_cols(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,

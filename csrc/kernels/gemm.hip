@@ -223,6 +223,113 @@ struct Chunk {
   }
 };
 
+// Per-tile BatchNorm partials (GemmArgs::bn_part) of the stored values v = acc + bias: for each column
+// and batch, the tile's row count, mean and sum of squared deviations (two passes over the
+// accumulators: the mean, then the centred squares -- no cancellation), reduced over the 4 lane
+// groups of a wave with shuffles and over the 2 row-waves through LDS.  The BN kernel merges the
+// tiles' triples (Chan) instead of re-reducing every row of the batch.
+template <int MI, int NJ, int TN>
+__device__ __forceinline__ void bn_tile_partials(const GemmArgs& g, const f32x4 (&acc)[MI][NJ], int m0, int n0, int by,
+                                                 int lane, int wm, int wn, unsigned char* smem) {
+  constexpr int WM = 16 * MI, WN = 16 * NJ;
+  float* red = reinterpret_cast<float*>(smem);   // [2 wm][TN][2 batch][2] (sum|count), then M2
+  float bias[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = min(n0 + wn * WN + j * 16 + (lane & 15), g.N - 1);
+    bias[j] = g.bias ? g.bias[n] : 0.f;
+  }
+  float sum[NJ][2], cnt[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    sum[j][0] = sum[j][1] = cnt[j][0] = cnt[j][1] = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const float v = acc[i][j][r] + bias[j];
+        const bool in = m < g.M, g1 = m >= g.bn_rpg;
+        sum[j][0] += (in && !g1) ? v : 0.f;
+        sum[j][1] += (in && g1) ? v : 0.f;
+        cnt[j][0] += (in && !g1) ? 1.f : 0.f;
+        cnt[j][1] += (in && g1) ? 1.f : 0.f;
+      }
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        sum[j][b] += __shfl_xor(sum[j][b], o, 64);
+        cnt[j][b] += __shfl_xor(cnt[j][b], o, 64);
+      }
+  }
+  __syncthreads();   // the stage buffers are free
+  if ((lane >> 4) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* e = red + (((wm * TN) + wn * WN + j * 16 + lane) * 2 + b) * 2;
+        e[0] = sum[j][b];
+        e[1] = cnt[j][b];
+      }
+  }
+  __syncthreads();
+  float mean[NJ][2], tot[NJ][2], m2[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int col = wn * WN + j * 16 + (lane & 15);
+      const float* e0 = red + ((col) * 2 + b) * 2;
+      const float* e1 = red + ((TN + col) * 2 + b) * 2;
+      tot[j][b] = e0[1] + e1[1];
+      mean[j][b] = tot[j][b] > 0.f ? (e0[0] + e1[0]) / tot[j][b] : 0.f;
+      m2[j][b] = 0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const float v = acc[i][j][r] + bias[j];
+        const bool in = m < g.M, g1 = m >= g.bn_rpg;
+        const float d0 = v - mean[j][0], d1 = v - mean[j][1];
+        m2[j][0] += (in && !g1) ? d0 * d0 : 0.f;
+        m2[j][1] += (in && g1) ? d1 * d1 : 0.f;
+      }
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) m2[j][b] += __shfl_xor(m2[j][b], o, 64);
+  }
+  __syncthreads();
+  if ((lane >> 4) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) red[((wm * TN) + wn * WN + j * 16 + lane) * 2 + b] = m2[j][b];
+  }
+  __syncthreads();
+  if (wm == 0 && (lane >> 4) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = wn * WN + j * 16 + lane;
+      const int n = n0 + col;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        float* o = g.bn_part + ((size_t)(by * 2 + b) * 3) * g.N + n;
+        o[0] = tot[j][b];
+        o[g.N] = mean[j][b];
+        o[2 * (size_t)g.N] = red[col * 2 + b] + red[(TN + col) * 2 + b];
+      }
+    }
+  }
+}
+
 template <bool F32, int TM, int TN>
 struct Cfg {
   // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
@@ -454,6 +561,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         if (g.bias) v += g.bias[n];
         st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
+  if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
 }
 
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits

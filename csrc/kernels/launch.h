@@ -55,6 +55,11 @@ struct GemmArgs {
   const int* oh_col;
   const int* oh_opt;
   const int* oh_off;
+  // BatchNorm partial statistics (nullable; 32/64 tiles, no split-K, plain C = A B^T + bias): every
+  // tile writes, per output column and batch (rows [0, bn_rpg) / [bn_rpg, M)), its row count, mean
+  // and sum of squared deviations: bn_part[((m_tile * 2 + batch) * 3 + {0,1,2}) * N + n]
+  float* bn_part;
+  int bn_rpg;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -175,6 +180,11 @@ void launch_bn_relu_train(const float* a, int lda, const float* gamma, const flo
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream);
 
+// BatchNorm(train) + ReLU from the GEMM's per-tile partial statistics (kernels/ctgan_ops.hip)
+void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tiles, const float* gamma,
+                          const float* beta, float* out, int ldo, float* nhat, int ldn, float* mean, float* invstd,
+                          float* rm, float* rv, int rows, int cols, int groups, float momentum, float eps,
+                          hipStream_t stream);
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream);

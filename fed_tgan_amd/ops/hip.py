@@ -86,6 +86,10 @@ class HipOps:
         self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
         self._dec: Dict[int, Tuple] = {}
         self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
+        # BatchNorm(train) from the GEMM's per-tile partial statistics (gemm epilogue + bn_relu_apply)
+        # instead of a separate full reduction over the batch (bn_relu_train); A/B knob
+        self.bn_fused = True
+        self._bnp: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ helpers
     def _workspace(self, n: int) -> torch.Tensor:
@@ -97,6 +101,16 @@ class HipOps:
             ws = torch.zeros(max(1 << 20, int(n * 1.25)), dtype=torch.float32, device=self.device)
             self._ws[self.lane] = ws
         return ws
+
+    def _bn_partials(self, n: int) -> torch.Tensor:
+        """Per-tile BN partial-statistics buffer of the current lane (sized before graph capture)."""
+        t = self._bnp.get(self.lane)
+        if t is None or t.numel() < n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("BN partials buffer must be sized before graph capture")
+            t = torch.zeros(max(n, 1 << 16), dtype=torch.float32, device=self.device)
+            self._bnp[self.lane] = t
+        return t
 
     def _span_tables(self, spans, cond_spans=None):
         key = (tuple(spans), tuple(cond_spans or ()))
@@ -125,7 +139,8 @@ class HipOps:
 
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None):
+             slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None,
+             bn_part=None, bn_rpg=0):
         """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
         onehot = (W_c [N, C], col [M], opt [M], cond_offset[, transposed]): A holds only the dense input
@@ -148,13 +163,27 @@ class HipOps:
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
                     float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group),
                     *(onehot[:4] if onehot else (None, None, None, None)),
-                    bool(onehot is not None and len(onehot) > 4 and onehot[4]))
+                    bool(onehot is not None and len(onehot) > 4 and onehot[4]), bn_part, int(bn_rpg))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):
         """groups = 2: the rows are two batches (BN statistics per batch, running stats updated
         batch after batch); mean / invstd are then [2, cols].  onehot: see gemm."""
         if training:
+            M, N, K = x.shape[0], W.shape[0], x.shape[1]
+            kc = 64 if self.f32 else 128
+            tile, sk = _plan(M, N, K, kc)
+            tile = self.tile_override or tile
+            sk = _effective_splits(K, self.split_override or sk, kc)
+            if self.bn_fused and tile in (32, 64) and sk == 1:
+                # the GEMM epilogue writes per-tile (count, mean, M2) per column and batch; the BN
+                # kernel merges them (no reduction over the rows) and normalises many row blocks
+                nt = -(-M // tile)
+                part = self._bn_partials(nt * 6 * N)
+                self.gemm(x, W, abuf, tb=True, bias=b, onehot=onehot, bn_part=part, bn_rpg=M // groups)
+                self.L.bn_relu_apply(abuf, part, nt, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum),
+                                     float(eps), int(groups))
+                return
             # (fusing the split-K reduction into this BN launch was measured slower: the BN grid
             # has only cols/16 workgroups to pull the slabs -- profiles/README.md)
             self.gemm(x, W, abuf, tb=True, bias=b, onehot=onehot)

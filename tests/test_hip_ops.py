@@ -748,3 +748,27 @@ def test_gemm_onehot_gather_matches_dense(hip32, tile, bn, trans):
     torch.cuda.synchronize()
     hip32.tile_override = None
     assert torch.allclose(gath, dense, atol=2e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("rows,groups,tile", [(1000, 2, 32), (500, 1, 32), (1000, 2, 64), (37, 1, 32), (1200, 2, 32)])
+def test_linear_bn_relu_from_gemm_partials(hip32, rows, groups, tile):
+    """BatchNorm(train) from the GEMM epilogue's per-tile (count, mean, M2) partials merged by
+    bn_relu_apply equals the separate full-reduction BN kernel (both batches, running stats)."""
+    K, N = 200, 256
+    x = mat(rows, K, seed=70) * 2 + 3
+    W = mat(N, K, seed=71) * 0.1
+    bvec = mat(N, seed=72)
+    gamma, beta = torch.rand(N, device=DEV) + 0.5, mat(N, seed=73)
+    res = {}
+    for fused in (True, False):
+        hip32.bn_fused = fused
+        hip32.tile_override = tile
+        ab, out, nh = (torch.zeros(rows, N, device=DEV) for _ in range(3))
+        mean, inv = torch.zeros(groups, N, device=DEV), torch.zeros(groups, N, device=DEV)
+        rm, rv = torch.full((N,), 0.3, device=DEV), torch.full((N,), 1.7, device=DEV)
+        hip32.linear_bn_relu(x, W, bvec, gamma, beta, out, ab, nh, mean, inv, rm, rv, True, 0.1, 1e-5, groups=groups)
+        torch.cuda.synchronize()
+        res[fused] = (out, nh, mean, inv, rm, rv)
+    hip32.bn_fused, hip32.tile_override = True, None
+    for name, a, b in zip(("out", "nhat", "mean", "invstd", "rm", "rv"), res[True], res[False]):
+        assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), name

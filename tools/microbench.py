@@ -63,6 +63,14 @@ def onehot_ab(eng, tr, X, dev):
                   f"generate_decoded(40000) {t_gen:8.1f} us", flush=True)
 
 
+def bn_ab(eng, dev):
+    """BN(train) from GEMM partials (bn_relu_apply) vs the separate full-reduction BN kernel."""
+    for rep in range(3):
+        for fused in (False, True):
+            eng.ops.bn_fused = fused
+            print(f"bn_fused={int(fused)}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
+
+
 def gen_only(eng, tr, X, dev):
     """generate_decoded(40000): eager vs hipGraph, chunk 8192 vs one chunk (wall time per call)."""
     from fed_tgan_amd.models.samplers import CondTables
@@ -141,6 +149,7 @@ def main():
     ap.add_argument("--fold-sweep", action="store_true", help="column sums: own launch / folded into Adam")
     ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
     ap.add_argument("--onehot-ab", action="store_true", help="step + generation: dense c block vs one-hot gather")
+    ap.add_argument("--bn-ab", action="store_true", help="step: BN from GEMM partials vs full-reduction BN kernel")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -157,6 +166,8 @@ def main():
         return gen_only(eng, tr, X, dev)
     if args.onehot_ab:
         return onehot_ab(eng, tr, X, dev)
+    if args.bn_ab:
+        return bn_ab(eng, dev)
     if args.unroll:
         return unroll_sweep(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
