@@ -408,7 +408,8 @@ void bn_relu_apply(const Tensor& a, const Tensor& part, int64_t n_tiles, const T
   TORCH_CHECK(mean.is_contiguous() && invstd.is_contiguous() && mean.numel() == groups * cols &&
                   invstd.numel() == groups * cols, "bn_relu_apply: mean/invstd must be contiguous [groups, cols]");
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
-                  part.numel() >= n_tiles * 6 * cols && n_tiles >= 1, "bn_relu_apply: partials [n_tiles, 2, 3, cols]");
+                  part.numel() >= n_tiles * 6 * cols && n_tiles >= 1 && n_tiles <= 64,
+              "bn_relu_apply: partials [n_tiles <= 64, 2, 3, cols]");
   fedtgan::launch_bn_relu_apply(cfp(a), ld_of(a), cfp(part), (int)n_tiles, cfp(gamma), cfp(beta), fp(out), ld_of(out),
                                 fp(nhat), ld_of(nhat), fp(mean), fp(invstd), fp(rm), fp(rv), (int)rows, (int)cols,
                                 (int)groups, (float)momentum, (float)eps, cur_stream());

@@ -1213,64 +1213,68 @@ __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
     const float* __restrict__ beta, float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn,
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows,
     int cols, int groups, float momentum, float eps) {
-  __shared__ float st[BNA_COLS][2][2];   // [col][batch] = (mean, invstd)
+  __shared__ float st[BNA_COLS][2][3];   // [col][batch] = (mean, invstd, biased var)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c0 = blockIdx.x * BNA_COLS;
   const int rpg = rows / groups;
+  // this thread's float4 of the GEMM output: requested first, in flight during the merge
+  const int r = blockIdx.y * BNA_ROWS + (t >> 2);
+  const int cq = (t & 3) * 4;
+  float x[4];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int cl = 2 * w + q, c = c0 + cl;
-    float res[2][2];
+  for (int e = 0; e < 4; ++e) x[e] = a[(size_t)min(r, rows - 1) * lda + min(c0 + cq + e, cols - 1)];
+  // every tile triple this lane merges, all loads issued before the first merge (lane = tile,
+  // n_tiles <= 64: the 32/64-tile GEMMs of a <= 4096-row batch pair)
+  float pv[2][2][3];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-      float n = 0.f, mu = 0.f, m2 = 0.f;
-      if (c < cols) {
-        for (int tile = lane; tile < n_tiles; tile += 64) {
-          const float* p = part + ((size_t)(tile * 2 + b) * 3) * cols + c;
-          chan_merge(n, mu, m2, p[0], p[cols], p[2 * (size_t)cols]);
-        }
-      }
+      const int c = min(c0 + 2 * w + q, cols - 1);
+      const float* p = part + ((size_t)(min(lane, n_tiles - 1) * 2 + b) * 3) * cols + c;
+      const bool ok = lane < n_tiles;
+      pv[q][b][0] = ok ? p[0] : 0.f;
+      pv[q][b][1] = ok ? p[cols] : 0.f;
+      pv[q][b][2] = ok ? p[2 * (size_t)cols] : 0.f;
+    }
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float n = pv[q][b][0], mu = pv[q][b][1], m2 = pv[q][b][2];
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const float nb = __shfl_xor(n, o, 64), mub = __shfl_xor(mu, o, 64), m2b = __shfl_xor(m2, o, 64);
         chan_merge(n, mu, m2, nb, mub, m2b);
       }
-      const float var = n > 0.f ? fmaxf(m2 / n, 0.f) : 0.f;
-      res[b][0] = mu;
-      res[b][1] = rsqrtf(var + eps);
-      if (lane == 0 && c < cols) {
-        st[cl][b][0] = mu;
-        st[cl][b][1] = res[b][1];
-        if (blockIdx.y == 0 && b < groups) {
-          mean[(size_t)b * cols + c] = mu;
-          invstd[(size_t)b * cols + c] = res[b][1];
-        }
+      if (lane == 0) {
+        const float var = n > 0.f ? fmaxf(m2 / n, 0.f) : 0.f;
+        st[2 * w + q][b][0] = mu;
+        st[2 * w + q][b][1] = rsqrtf(var + eps);
+        st[2 * w + q][b][2] = var;
       }
-      res[b][0] = var;   // reuse: biased variance for the running update
     }
-    if (lane == 0 && c < cols && blockIdx.y == 0) {
-      const float unb = (float)rpg / (float)max(rpg - 1, 1);
-      float m = rm[c], v = rv[c];
-      m = (1.f - momentum) * m + momentum * st[cl][0][0];
-      v = (1.f - momentum) * v + momentum * res[0][0] * unb;
-      if (groups > 1) {
-        m = (1.f - momentum) * m + momentum * st[cl][1][0];
-        v = (1.f - momentum) * v + momentum * res[1][0] * unb;
-      }
-      rm[c] = m;
-      rv[c] = v;
-    }
-  }
   __syncthreads();
-  const int r = blockIdx.y * BNA_ROWS + (t >> 2);
-  const int cq = (t & 3) * 4;
+  if (blockIdx.y == 0 && t < BNA_COLS && c0 + t < cols) {
+    const int c = c0 + t;
+    const float unb = (float)rpg / (float)max(rpg - 1, 1);
+    float m = rm[c], v = rv[c];
+    for (int b = 0; b < groups; ++b) {
+      mean[(size_t)b * cols + c] = st[t][b][0];
+      invstd[(size_t)b * cols + c] = st[t][b][1];
+      m = (1.f - momentum) * m + momentum * st[t][b][0];      // batch after batch, in row order
+      v = (1.f - momentum) * v + momentum * st[t][b][2] * unb;
+    }
+    rm[c] = m;
+    rv[c] = v;
+  }
   if (r >= rows) return;
-  const int b = (groups > 1 && r >= rpg) ? 1 : 0;
+  const int bb = (groups > 1 && r >= rpg) ? 1 : 0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int cl = cq + e, c = c0 + cl;
     if (c >= cols) break;
-    const float nv = (a[(size_t)r * lda + c] - st[cl][b][0]) * st[cl][b][1];
+    const float nv = (x[e] - st[cl][bb][0]) * st[cl][bb][1];
     nhat[(size_t)r * ldn + c] = nv;
     const float y = nv * gamma[c] + beta[c];
     out[(size_t)r * ldo + c] = y > 0.f ? y : 0.f;

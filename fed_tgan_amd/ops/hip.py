@@ -175,7 +175,7 @@ class HipOps:
             tile, sk = _plan(M, N, K, kc)
             tile = self.tile_override or tile
             sk = _effective_splits(K, self.split_override or sk, kc)
-            if self.bn_fused and tile in (32, 64) and sk == 1:
+            if self.bn_fused and tile in (32, 64) and sk == 1 and -(-M // tile) <= 64:
                 # the GEMM epilogue writes per-tile (count, mean, M2) per column and batch; the BN
                 # kernel merges them (no reduction over the rows) and normalises many row blocks
                 nt = -(-M // tile)
