@@ -87,8 +87,10 @@ class HipOps:
         self._dec: Dict[int, Tuple] = {}
         self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
         # BatchNorm(train) from the GEMM's per-tile partial statistics (gemm epilogue + bn_relu_apply)
-        # instead of a separate full reduction over the batch (bn_relu_train); A/B knob
-        self.bn_fused = True
+        # instead of a separate full reduction over the batch (bn_relu_train).  A/B knob, default off:
+        # measured slower in the step (224.6 -> 231.4 us; bn_relu_apply 11.3 us vs bn_relu_train 7.8 us,
+        # profiles/README.md "negative results")
+        self.bn_fused = False
         self._bnp: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ helpers

@@ -508,10 +508,14 @@ def test_wide_activation_and_backward(hip):
             assert torch.allclose(o1[:, s:s + w].sum(1), torch.ones(rows, device=DEV), atol=1e-4)
     # identical rows: Gumbel-softmax means agree with the torch reference.  Each column mean is
     # over 3000 draws (difference std <= sqrt(2 * 0.25 / 3000) ~ 0.013); the max over the wide
-    # table's columns needs ~4.5 sigma, and the seed keeps the draw independent of test order
+    # table's columns needs ~4.5 sigma.  Both draws are pinned: the torch reference by the seed, the
+    # HIP Philox stream by a fresh counter (earlier tests in this module advance the fixture's)
     torch.manual_seed(1234)
     base = logits[:1].repeat(rows, 1)
+    saved_ctr = hip.ctr.clone()
+    hip.ctr.zero_()
     hip.activate(base, o1, spans, 0.2)
+    hip.ctr.copy_(saved_ctr)
     REF.activate(base, o2, spans, 0.2)
     torch.cuda.synchronize()
     assert (o1.mean(0) - o2.mean(0)).abs().max().item() < 0.06
@@ -769,6 +773,6 @@ def test_linear_bn_relu_from_gemm_partials(hip32, rows, groups, tile):
         hip32.linear_bn_relu(x, W, bvec, gamma, beta, out, ab, nh, mean, inv, rm, rv, True, 0.1, 1e-5, groups=groups)
         torch.cuda.synchronize()
         res[fused] = (out, nh, mean, inv, rm, rv)
-    hip32.bn_fused, hip32.tile_override = True, None
+    hip32.bn_fused, hip32.tile_override = False, None
     for name, a, b in zip(("out", "nhat", "mean", "invstd", "rm", "rv"), res[True], res[False]):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), name
