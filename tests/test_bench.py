@@ -78,3 +78,15 @@ def test_bench_world_size_mismatch_fails():
                         "--rows", "1000", "--quiet"], capture_output=True, text=True, timeout=120, env=env,
                        cwd="/tmp")
     assert r.returncode != 0 and "WORLD_SIZE" in (r.stderr + r.stdout)
+
+
+def test_bench_engine_override_and_force_dist():
+    """--engine KEY=VALUE reaches EngineConfig (reported back); --force-dist builds real process groups
+    for one rank (gloo here; RCCL on a GPU box)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0", "--rows",
+                        "1000", "--n-sample", "600", "--quiet", "--no-eval", "--engine", "onehot=0", "--force-dist",
+                        "--check"], capture_output=True, text=True, timeout=300, env=_env(), cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["engine_overrides"] == ["onehot=0"] and rec["config"]["data_plane"] == "gloo"
+    assert rec["consistency"]["csv_rows"] == 600
