@@ -124,6 +124,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     check_f32_2d(*oh_w, "oh_w");
     TORCH_CHECK(oh_trans ? oh_w->size(1) == N : oh_w->size(0) == N, "gemm: oh_w must be [N, C] (or [C, N] transposed)");
     g.oh_trans = oh_trans ? 1 : 0;
+    g.oh_c = (int)(oh_trans ? oh_w->size(0) : oh_w->size(1));
     TORCH_CHECK(oh_col.has_value() && oh_opt.has_value() && oh_off.has_value(), "gemm: one-hot needs col / opt / off");
     for (const auto* t : {&*oh_col, &*oh_opt, &*oh_off})
       TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous(), "gemm: one-hot int32 tables");
@@ -203,6 +204,7 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
     if (a.ldx == 0) a.ldx = ld_of(*xr);
     TORCH_CHECK(ld_of(*xr) == a.ldx, "sample: xf/xr strides differ");
     a.row_off = optp<int64_t>(row_off); a.row_cnt = optp<int64_t>(row_cnt); a.rows = optp<int64_t>(rows);
+    a.n_entries = rows->numel();
     a.data = data->data_ptr<float>();
     a.n_rows = (int)data->size(0);
   }
@@ -510,6 +512,7 @@ void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, 
   a.cont = cont.data_ptr<int>();
   a.code_off = code_off.data_ptr<int>();
   a.codes = codes.data_ptr<double>();
+  a.n_codes = (int)codes.numel();
   a.mu = mu.data_ptr<double>();
   a.sd = sd.data_ptr<double>();
   a.K = mu.dim() == 2 ? (int)mu.size(1) : 1;
@@ -663,6 +666,18 @@ void vgm_fit(const Tensor& x, const Tensor& n_rows, const c10::optional<Tensor>&
   fedtgan::launch_vgm_fit(a, cur_stream());
 }
 
+// checked build: the check bits raised by every kernel since the last call (cleared); synchronises
+int64_t check_status() {
+  (void)hipDeviceSynchronize();
+  return (int64_t)(fedtgan::check_status_gemm() | fedtgan::check_status_ctgan_ops() | fedtgan::check_status_vgm());
+}
+
+#ifdef FEDTGAN_CHECKED
+bool is_checked() { return true; }
+#else
+bool is_checked() { return false; }
+#endif
+
 std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
 // kernel variant knobs for measured sweeps (tools/microbench.py); returns the previous value
@@ -783,6 +798,8 @@ TORCH_LIBRARY(fedtgan, m) {
       "int threads) -> ()");
   m.def("py_float(float x) -> str", &py_float);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
+  m.def("check_status() -> int", &check_status);
+  m.def("is_checked() -> bool", &is_checked);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {

@@ -6,7 +6,11 @@ source or header is newer than its object.  The library links against the HIP ru
 ships inside the torch wheel (same soname as /opt/rocm's), so one HIP runtime is loaded per
 process.
 
-    python csrc/build.py [--force] [-j N] [--debug]
+    python csrc/build.py [--force] [-j N] [--debug] [--checked]
+
+``--checked`` builds ``fed_tgan_amd/_C_checked.so`` (objects under ``build/native_checked``):
+the same kernels with -DFEDTGAN_CHECKED=1, which verify every table-derived index on the device
+(see ``kernels/common.h`` FT_CHECK).  ``FEDTGAN_CHECKED=1`` at run time loads it instead of _C.so.
 """
 from __future__ import annotations
 
@@ -64,35 +68,40 @@ def main():
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--save-temps", action="store_true")
+    ap.add_argument("--checked", action="store_true", help="device bounds-checked build -> _C_checked.so")
     args = ap.parse_args()
-    os.makedirs(BUILD, exist_ok=True)
+    build_dir = BUILD + ("_checked" if args.checked else "")
+    out = OUT.replace("_C.so", "_C_checked.so") if args.checked else OUT
+    os.makedirs(build_dir, exist_ok=True)
     inc, tlib, abi = torch_paths()
     headers = glob.glob(os.path.join(HERE, "**", "*.h"), recursive=True)
     opt = ["-O0", "-g"] if args.debug else ["-O3"]
     common = ["-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-I" + HERE] + opt
+    if args.checked:
+        common.append("-DFEDTGAN_CHECKED=1")
     jobs = []
     for src in sorted(glob.glob(os.path.join(HERE, "kernels", "*.hip"))):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         cmd = [hipcc(), "-c", src, "-o", obj, f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + common
         if args.save_temps:
             cmd += ["-save-temps=obj"]
         jobs.append((src, obj, cmd))
     for src in sorted(glob.glob(os.path.join(HERE, "host", "*.cpp"))):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         jobs.append((src, obj, ["g++", "-c", src, "-o", obj, "-pthread"] + common))
     bsrc = os.path.join(HERE, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.cpp.o")
+    bobj = os.path.join(build_dir, "bindings.cpp.o")
     jobs.append((bsrc, bobj, [hipcc(), "-c", bsrc, "-o", bobj, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                               "-I" + os.path.join(rocm(), "include")] + ["-I" + p for p in inc] + common))
     todo = [(s, o, c) for s, o, c in jobs if args.force or newer([s] + headers, o)]
     with cf.ThreadPoolExecutor(max_workers=max(1, args.j)) as ex:
         list(ex.map(lambda j: run(j[2]), todo))
     objs = [o for _, o, _ in jobs]
-    if args.force or todo or newer(objs, OUT):
-        run([hipcc(), "-shared", "-o", OUT] + objs + [f"--offload-arch={ARCH}", "-L" + tlib, "-lc10", "-lc10_hip",
+    if args.force or todo or newer(objs, out):
+        run([hipcc(), "-shared", "-o", out] + objs + [f"--offload-arch={ARCH}", "-L" + tlib, "-lc10", "-lc10_hip",
                                                        "-ltorch", "-ltorch_cpu", "-l:libamdhip64.so", "-pthread",
                                                        "-Wl,-rpath," + tlib])
-    print(f"built {OUT} ({len(todo)} objects recompiled)")
+    print(f"built {out} ({len(todo)} objects recompiled)")
 
 
 if __name__ == "__main__":

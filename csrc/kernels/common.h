@@ -14,6 +14,32 @@ namespace fedtgan {
 
 constexpr int WAVE = 64;
 
+// ---- checked build (csrc/build.py --checked -> _C_checked.so, FEDTGAN_CHECKED=1 at run time): every
+// data-dependent index a kernel derives from its tables (CSR row picks, condition options, decode
+// codes, one-hot gathers, encode lookups) is verified; a violation sets a bit in the translation
+// unit's flag word with a vector atomic (no trap: the access itself is clamped so the kernel never
+// faults) and the host raises after the launch sequence (`fedtgan_check_status`).  Release builds
+// compile the checks away.
+enum CheckCode : unsigned {
+  CHK_CSR_PICK = 0,      // sampler: CSR entry outside the row-list array
+  CHK_DATA_ROW = 1,      // sampler: data row outside the training matrix
+  CHK_COND = 2,          // sampler: drawn column / option outside the span tables
+  CHK_DECODE_CODE = 3,   // decode: categorical code index outside the code table
+  CHK_DECODE_MODE = 4,   // decode: mode index >= K
+  CHK_ONEHOT = 5,        // GEMM one-hot gather: condition index outside the block
+  CHK_ENCODE_LUT = 6,    // encode: label lookup outside the table
+};
+#ifdef FEDTGAN_CHECKED
+#define FT_CHECK(flag, cond, code)                                  \
+  do {                                                              \
+    if (!(cond)) atomicOr((flag), 1u << (unsigned)(code));          \
+  } while (0)
+#define FT_CHECKED 1
+#else
+#define FT_CHECK(flag, cond, code) ((void)0)
+#define FT_CHECKED 0
+#endif
+
 struct RngArgs {
   uint64_t seed;
   const uint64_t* ctr;  // device-resident step counter

@@ -22,6 +22,18 @@
 
 namespace fedtgan {
 
+#if FT_CHECKED
+__device__ unsigned g_check_ops = 0u;
+unsigned check_status_ctgan_ops() {
+  unsigned v = 0u, z = 0u;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_check_ops), sizeof(v));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_check_ops), &z, sizeof(z));
+  return v;
+}
+#else
+unsigned check_status_ctgan_ops() { return 0u; }
+#endif
+
 // ============================================================================ sampling
 // One wave per batch row.  The option of the sampled conditional column is found with a
 // lane-parallel inverse-CDF search (each lane tests one CDF entry, a ballot picks the first
@@ -143,6 +155,9 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   if (!real) return;
   // (4) real row for the permuted condition: count -> CSR entry -> row copy
   const int pc = per.col, po = cond_draw_finish(a, per, cv_per, lane);
+#if FT_CHECKED
+  FT_CHECK(&g_check_ops, pc >= 0 && pc < a.n_col && po >= 0 && po < a.maxw, CHK_COND);
+#endif
   const size_t cell = (size_t)pc * a.maxw + po;
   const int64_t cnt = a.row_cnt[cell];
   const int64_t off = a.row_off[cell];
@@ -150,7 +165,14 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const uint4 r4 = rng4(rp, step, (uint64_t)b);
   int64_t pick = (int64_t)(u01d(r4.x, r4.y) * (double)(cnt > 0 ? cnt : 1));
   if (pick >= cnt) pick = cnt > 0 ? cnt - 1 : 0;
+#if FT_CHECKED
+  FT_CHECK(&g_check_ops, off >= 0 && off + pick < a.n_entries, CHK_CSR_PICK);
+  int64_t row = a.rows[min(max(off + pick, (int64_t)0), a.n_entries - 1)];
+  FT_CHECK(&g_check_ops, row >= 0 && row < a.n_rows, CHK_DATA_ROW);
+  row = min(max(row, (int64_t)0), (int64_t)a.n_rows - 1);
+#else
   const int64_t row = a.rows[off + pick];
+#endif
   const float* src = a.data + (size_t)row * a.Dd;
   float* dst = a.xr + (size_t)b * a.ldx;
   const int phot = a.cond_off[pc] + po;
@@ -1725,8 +1747,14 @@ __global__ __launch_bounds__(256) void sample_decode_kernel(DecodeArgs a) {
     double al = (double)tanhf(x[st]);
     al = al < -1.0 ? -1.0 : (al > 1.0 ? 1.0 : al);
     const int c = a.cont[j];
+#if FT_CHECKED
+    FT_CHECK(&g_check_ops, best >= 0 && best < a.K, CHK_DECODE_MODE);
+#endif
     val = al * 4.0 * a.sd[(size_t)c * a.K + best] + a.mu[(size_t)c * a.K + best];
   } else {
+#if FT_CHECKED
+    FT_CHECK(&g_check_ops, a.code_off[j] + best >= 0 && a.code_off[j] + best < a.n_codes, CHK_DECODE_CODE);
+#endif
     val = a.codes[a.code_off[j] + best];
   }
   a.out[(size_t)r * a.n_cols + j] = val;
@@ -1784,8 +1812,14 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void sample_decode_row_kernel(Decod
       double al = (double)tanhf(x[a.start[j]]);
       al = al < -1.0 ? -1.0 : (al > 1.0 ? 1.0 : al);
       const int c = a.cont[j];
+#if FT_CHECKED
+      FT_CHECK(&g_check_ops, bi >= 0 && bi < a.K, CHK_DECODE_MODE);
+#endif
       val = al * 4.0 * a.sd[(size_t)c * a.K + bi] + a.mu[(size_t)c * a.K + bi];
     } else {
+#if FT_CHECKED
+      FT_CHECK(&g_check_ops, a.code_off[j] + bi >= 0 && a.code_off[j] + bi < a.n_codes, CHK_DECODE_CODE);
+#endif
       val = a.codes[a.code_off[j] + bi];
     }
     a.out[(size_t)r * a.n_cols + j] = val;

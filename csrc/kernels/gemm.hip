@@ -40,6 +40,18 @@
 
 namespace fedtgan {
 
+#if FT_CHECKED
+__device__ unsigned g_check_gemm = 0u;
+unsigned check_status_gemm() {
+  unsigned v = 0u, z = 0u;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_check_gemm), sizeof(v));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_check_gemm), &z, sizeof(z));
+  return v;
+}
+#else
+unsigned check_status_gemm() { return 0u; }
+#endif
+
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
@@ -497,6 +509,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       for (int r = 0; r < 4; ++r) {
         const int m = min(m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r, g.M - 1);
         rows[i][r] = g.oh_off[g.oh_col[m]] + g.oh_opt[m];
+#if FT_CHECKED
+        FT_CHECK(&g_check_gemm, rows[i][r] >= 0 && rows[i][r] < g.oh_c, CHK_ONEHOT);
+        rows[i][r] = min(max(rows[i][r], 0), g.oh_c - 1);
+#endif
       }
 #pragma unroll
     for (int i = 0; i < MI; ++i)

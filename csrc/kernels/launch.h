@@ -60,9 +60,14 @@ struct GemmArgs {
   // and sum of squared deviations: bn_part[((m_tile * 2 + batch) * 3 + {0,1,2}) * N + n]
   float* bn_part;
   int bn_rpg;
+  int oh_c;       // width of the one-hot block (checked build: gather index bound)
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
+// checked build: the OR of the check bits raised since the last call in each kernel TU (cleared)
+unsigned check_status_gemm();
+unsigned check_status_ctgan_ops();
+unsigned check_status_vgm();
 // two independent GEMMs in one launch where the pair is instantiated, else two launches
 void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream);
 extern int g_gemm_pairs;
@@ -80,6 +85,7 @@ struct SampleArgs {
   const int64_t* row_off;   // [n_col, maxw]
   const int64_t* row_cnt;   // [n_col, maxw]
   const int64_t* rows;      // CSR row lists
+  int64_t n_entries;        // length of `rows` (checked build: CSR pick bound)
   const float* data;        // encoded training matrix [n_rows, Dd]
   int* col;
   int* opt;
@@ -201,6 +207,7 @@ struct DecodeArgs {
   const int* cont;      // continuous column index into mu/sd
   const int* code_off;  // categorical: offset into codes
   const double* codes;
+  int n_codes;          // length of `codes` (checked build)
   const double* mu;     // [n_cont, K]
   const double* sd;
   int K;

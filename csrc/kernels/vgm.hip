@@ -20,6 +20,18 @@
 
 namespace fedtgan {
 
+#if FT_CHECKED
+__device__ unsigned g_check_vgm = 0u;
+unsigned check_status_vgm() {
+  unsigned v = 0u, z = 0u;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_check_vgm), sizeof(v));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_check_vgm), &z, sizeof(z));
+  return v;
+}
+#else
+unsigned check_status_vgm() { return 0u; }
+#endif
+
 constexpr int VGM_K = 10;   // components per continuous column (N_CLUSTERS)
 
 __global__ __launch_bounds__(256) void vgm_encode_kernel(VgmEncodeArgs a) {
@@ -75,6 +87,9 @@ __global__ __launch_bounds__(256) void vgm_encode_kernel(VgmEncodeArgs a) {
       row[pos + 1 + opt] = 1.f;
     } else {
       // codes were range-checked on the host; the clamp keeps a stray value inside the LUT row
+#if FT_CHECKED
+      FT_CHECK(&g_check_vgm, (int)xv >= 0 && (int)xv < a.col_lut_n[j], CHK_ENCODE_LUT);
+#endif
       opt = a.lut[aux + min(max((int)xv, 0), a.col_lut_n[j] - 1)];
       row[pos + opt] = 1.f;
     }

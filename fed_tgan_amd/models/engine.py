@@ -734,6 +734,8 @@ class CTGANEngine:
             for _ in range(n):
                 self._one_step()
         self.bn_batches += 2 * n
+        if hasattr(self.ops, "check"):
+            self.ops.check()
 
     def train_epoch(self, use_graph: bool | None = None):
         self.train_steps(self.steps_per_epoch, use_graph)
@@ -799,9 +801,12 @@ class CTGANEngine:
         if use_graph:
             ent = self._gen_graphs.get(n) or self._capture_gen(n)
             ent[0].replay()
-            return ent[3].clone()
-        out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
-        self._gen_pass(n, out, self._gen_buffers)
+            out = ent[3].clone()
+        else:
+            out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
+            self._gen_pass(n, out, self._gen_buffers)
+        if hasattr(self.ops, "check"):
+            self.ops.check()
         return out
 
     def _gen_pass(self, n: int, out: torch.Tensor, bufs):

@@ -94,6 +94,12 @@ class HipOps:
         self._bnp: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ helpers
+    def check(self) -> None:
+        """Checked native build (FEDTGAN_CHECKED=1): raise if a kernel flagged an out-of-range table
+        index since the last check (synchronises).  Release build: nothing."""
+        if native.CHECKED:
+            native.check()
+
     def _workspace(self, n: int) -> torch.Tensor:
         """Split-K slab of the current lane (concurrent lanes never share one)."""
         ws = self._ws.get(self.lane)

@@ -14,7 +14,14 @@ import numpy as np
 import torch
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "_C.so")
+# FEDTGAN_CHECKED=1: the device bounds-checked build (csrc/build.py --checked)
+CHECKED = os.environ.get("FEDTGAN_CHECKED", "0") not in ("", "0")
+LIB_PATH = os.path.join(PKG_DIR, "_C_checked.so" if CHECKED else "_C.so")
+
+CHECK_NAMES = {0: "sampler CSR pick outside the row lists", 1: "sampler data row outside the training matrix",
+               2: "sampler condition outside the span tables", 3: "decode code index outside the code table",
+               4: "decode mode index >= K", 5: "one-hot gather index outside the conditional block",
+               6: "encode label outside the lookup table"}
 
 _lock = threading.Lock()
 _loaded = None
@@ -51,6 +58,18 @@ def require():
     if _loaded is None:
         raise RuntimeError(_error or "native library unavailable")
     return _loaded
+
+
+def check() -> None:
+    """Checked build: raise if any kernel since the last call flagged an out-of-range index (the
+    access itself was clamped).  A no-op with the release library."""
+    L = require()
+    if not CHECKED:
+        return
+    bits = int(L.check_status())
+    if bits:
+        raise RuntimeError("device bounds check failed: " +
+                           "; ".join(n for b, n in CHECK_NAMES.items() if bits >> b & 1))
 
 
 def write_csv(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
