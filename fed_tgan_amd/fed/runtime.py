@@ -29,6 +29,7 @@ last round ``timestamp_experiment.csv`` is written (`:827-829`).
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import json
 import os
@@ -102,6 +103,10 @@ class FedConfig:
     # sample + write the epoch CSV every N rounds (and after the last); 1 = every round (reference)
     csv_every: int = 1
     csv_epochs: Optional[List[int]] = None  # if set: sample + write only these epochs (and the last)
+    # per-collective sub-phase timers (allreduce / share / generate / gather / d2h), each a stream
+    # sync: None = on when real process groups exist (multi-rank runs, --force-dist), off otherwise
+    # (one plain GPU rank, in-process emulation: the extra syncs cost ~2-10 % of a round there)
+    phase_detail: Optional[bool] = None
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -329,15 +334,22 @@ class FedRuntime:
             pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
 
     # ================================================================= rounds
+    def _sub(self, name: str):
+        """Sub-phase timer (see FedConfig.phase_detail), or nothing."""
+        on = self.cfg.phase_detail
+        if on is None:
+            on = bool(getattr(self.comm, "dist_active", False))
+        return self.timer.phase(name, self.device) if on else contextlib.nullcontext()
+
     def aggregate(self, alive: np.ndarray | None = None):
         """Weighted FedAvg of every G/D parameter and BN statistic (`Server/dtds/distributed.py:86-106`)
         as one all-reduce of the pre-scaled flat buffer; clients that missed the round get weight 0."""
         c = self.comm
         wts = self.weights if alive is None else effective_weights(self.weights, alive)
         w = float(wts[c.client_index]) if self.is_client else 0.0
-        with self.timer.phase("allreduce", self.device):
+        with self._sub("allreduce"):
             c.weighted_all_reduce(self.engine.flat, w)
-        with self.timer.phase("share", self.device):
+        with self._sub("share"):
             c.share_with_federator(self.engine.flat, self.federator)
         # num_batches_tracked: weighted average of every client's counter, truncated (reference cast)
         ep = self.engine
@@ -360,21 +372,20 @@ class FedRuntime:
         # stream and the writer waits for it: round r's copy + CSV overlap round r + 1's training
         # (bench.py's timed region still ends with every table on disk)
         async_copy = self.cfg.async_csv and self.device.type == "cuda"
-        tm, dev = self.timer, self.device
         if len(samplers) == 1:
             if self.rank in samplers:
-                with tm.phase("generate", dev):
+                with self._sub("generate"):
                     vals = self.engine.generate_decoded(per[0])
-                with tm.phase("d2h", dev):
+                with self._sub("d2h"):
                     share = self._host(vals) if async_copy else vals.cpu().numpy()
         else:
             # every client decodes its share on its GPU; one gather to the federator (RCCL over
             # xGMI when the data plane is RCCL), one device-to-host copy there
-            with tm.phase("generate", dev):
+            with self._sub("generate"):
                 vals = self.engine.generate_decoded(per[samplers.index(self.rank)])
-            with tm.phase("gather", dev):
+            with self._sub("gather"):
                 rows = c.gather_rows(vals, per, samplers, dst=self.federator, to_host=not async_copy)
-            with tm.phase("d2h", dev):
+            with self._sub("d2h"):
                 if self.is_fed:
                     if rows.device.type == "cuda":
                         share = self._host(rows)
