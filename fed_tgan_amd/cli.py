@@ -130,12 +130,36 @@ def pick_device(rank: int, colocated: bool, backend: str, mode: str = "fedavg") 
     if backend == "torch" or not torch.cuda.is_available():
         return torch.device("cpu")
     n = torch.cuda.device_count()
-    local = int(os.environ.get("LOCAL_RANK", rank))
     # dedicated federator: it shares GPU 0 with client 1, except in MD-GAN mode where it runs the
     # generator for every client and gets a GPU of its own (RCCL needs one rank per device)
-    idx = local % n if (colocated or mode == "mdgan") else max(local - 1, 0) % n
+    idx = device_index(int(os.environ.get("LOCAL_RANK", rank)), n, colocated, mode)
     torch.cuda.set_device(idx)
     return torch.device("cuda", idx)
+
+
+def device_index(local: int, ngpu: int, colocated: bool, mode: str = "fedavg") -> int:
+    """The GPU of the rank with node-local index ``local`` (see pick_device): one per rank when
+    co-located (or MD-GAN), else the dedicated federator shares GPU 0 with client 1."""
+    return local % ngpu if (colocated or mode == "mdgan") else max(local - 1, 0) % ngpu
+
+
+def limit_queues_when_sharing(rank: int, world: int, colocated: bool, mode: str = "fedavg") -> None:
+    """Several ranks on one GPU (a dedicated federator next to client 1, or more clients than GPUs):
+    cap every process at 2 HIP hardware queues unless the user chose otherwise.  With HIP's default
+    of 4 per process, three processes oversubscribe the GPU's hardware queue slots and get
+    time-sliced: measured on one MI355X (world_size 3, dedicated federator), 69.9 ms per round with
+    4 queues against 26.3 ms with 1 or 2 (`tools/gpu_recipes/topologies_queues.sh`).  Must run before
+    the process first touches HIP (``torch.cuda.device_count`` does not)."""
+    try:
+        ngpu = torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return
+    if not ngpu:
+        return
+    mine = device_index(int(os.environ.get("LOCAL_RANK", rank)), ngpu, colocated, mode)
+    sharers = sum(1 for r in range(world) if device_index(r, ngpu, colocated, mode) == mine)
+    if sharers > 1:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
 
 
 def run_rank(rank: int, args) -> None:
@@ -145,6 +169,7 @@ def run_rank(rank: int, args) -> None:
     from .parallel.comm import Comm
     world = args.world_size
     colocated = args.colocated
+    limit_queues_when_sharing(rank, world, colocated, args.mode)
     device = pick_device(rank, colocated, args.backend, args.mode)
     if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
         torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
