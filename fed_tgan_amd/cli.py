@@ -143,23 +143,26 @@ def device_index(local: int, ngpu: int, colocated: bool, mode: str = "fedavg") -
     return local % ngpu if (colocated or mode == "mdgan") else max(local - 1, 0) % ngpu
 
 
-def limit_queues_when_sharing(rank: int, world: int, colocated: bool, mode: str = "fedavg") -> None:
-    """Several ranks on one GPU (a dedicated federator next to client 1, or more clients than GPUs):
-    cap every process at 2 HIP hardware queues unless the user chose otherwise.  With HIP's default
-    of 4 per process, three processes oversubscribe the GPU's hardware queue slots and get
-    time-sliced: measured on one MI355X (world_size 3, dedicated federator), 69.9 ms per round with
-    4 queues against 26.3 ms with 1 or 2 (`tools/gpu_recipes/topologies_queues.sh`).  Must run before
-    the process first touches HIP (``torch.cuda.device_count`` does not)."""
+def gpus_shared(world: int, colocated: bool, mode: str = "fedavg") -> bool:
+    """Will several ranks of this node run on one GPU (a dedicated federator next to client 1, or
+    more clients than GPUs)?"""
     try:
         ngpu = torch.cuda.device_count()
     except Exception:  # pragma: no cover
-        return
+        return False
     if not ngpu:
-        return
-    mine = device_index(int(os.environ.get("LOCAL_RANK", rank)), ngpu, colocated, mode)
-    sharers = sum(1 for r in range(world) if device_index(r, ngpu, colocated, mode) == mine)
-    if sharers > 1:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+        return False
+    idx = [device_index(r, ngpu, colocated, mode) for r in range(world)]
+    return len(set(idx)) < len(idx)
+
+
+# Ranks sharing a GPU run with at most 2 HIP hardware queues each.  With HIP's default of 4 per
+# process, three processes oversubscribe the GPU's hardware queue slots and are time-sliced:
+# measured on one MI355X (world_size 3, dedicated federator) 69.9 ms per round with 4 queues against
+# 26.3 ms with 1 or 2 (`tools/gpu_recipes/topologies_queues.sh`).  HIP reads the variable when the
+# library loads, so the launcher sets it for its children; ranks started by hand need it in their
+# environment (run_rank prints a hint).
+SHARED_GPU_QUEUES = "2"
 
 
 def run_rank(rank: int, args) -> None:
@@ -169,7 +172,9 @@ def run_rank(rank: int, args) -> None:
     from .parallel.comm import Comm
     world = args.world_size
     colocated = args.colocated
-    limit_queues_when_sharing(rank, world, colocated, args.mode)
+    if "GPU_MAX_HW_QUEUES" not in os.environ and args.backend != "torch" and gpus_shared(world, colocated, args.mode):
+        print(f"[rank {rank}] several ranks share a GPU: export GPU_MAX_HW_QUEUES={SHARED_GPU_QUEUES} before "
+              "starting each rank (HIP's default 4 queues per process get time-sliced)", flush=True)
     device = pick_device(rank, colocated, args.backend, args.mode)
     if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
         torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
@@ -215,6 +220,8 @@ def main(argv: Optional[List[str]] = None) -> None:
         args.colocated = True
     if args.port == 7788:
         args.port = free_port()
+    if args.backend != "torch" and gpus_shared(args.world_size, args.colocated, args.mode):
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", SHARED_GPU_QUEUES)   # inherited by the spawned ranks
     import torch.multiprocessing as mp
     mp.spawn(_spawn_entry, args=(args,), nprocs=args.world_size, join=True)
 
