@@ -70,10 +70,10 @@ def _free_port() -> int:
 
 
 def _visible_gpus() -> int:
-    # device_count() does not initialise HIP on this image (is_available() would): safe in a
-    # parent that later starts the GPU ranks
-    import torch
-    return torch.cuda.device_count()
+    # from the kernel driver's topology, without loading HIP: the parent stays alive for the whole
+    # run and must not hold a GPU context (or queues) of its own
+    from fed_tgan_amd.utils.gpus import visible_gpu_count
+    return visible_gpu_count()
 
 
 def launch(n: int, argv) -> int:

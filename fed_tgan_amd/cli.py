@@ -146,10 +146,8 @@ def device_index(local: int, ngpu: int, colocated: bool, mode: str = "fedavg") -
 def gpus_shared(world: int, colocated: bool, mode: str = "fedavg") -> bool:
     """Will several ranks of this node run on one GPU (a dedicated federator next to client 1, or
     more clients than GPUs)?"""
-    try:
-        ngpu = torch.cuda.device_count()
-    except Exception:  # pragma: no cover
-        return False
+    from .utils.gpus import visible_gpu_count
+    ngpu = visible_gpu_count()      # (no HIP here: a launcher parent must not hold a GPU context)
     if not ngpu:
         return False
     idx = [device_index(r, ngpu, colocated, mode) for r in range(world)]
