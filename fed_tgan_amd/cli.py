@@ -174,6 +174,9 @@ def run_rank(rank: int, args) -> None:
         print(f"[rank {rank}] several ranks share a GPU: export GPU_MAX_HW_QUEUES={SHARED_GPU_QUEUES} before "
               "starting each rank (HIP's default 4 queues per process get time-sliced)", flush=True)
     device = pick_device(rank, colocated, args.backend, args.mode)
+    if not args.quiet:
+        print(f"[rank {rank}] device {device}, GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES', 'default')}",
+              flush=True)
     if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
         torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
     client_ranks = list(range(world)) if colocated else list(range(1, world))
@@ -218,8 +221,11 @@ def main(argv: Optional[List[str]] = None) -> None:
         args.colocated = True
     if args.port == 7788:
         args.port = free_port()
-    if args.backend != "torch" and gpus_shared(args.world_size, args.colocated, args.mode):
+    shared = args.backend != "torch" and gpus_shared(args.world_size, args.colocated, args.mode)
+    if shared:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", SHARED_GPU_QUEUES)   # inherited by the spawned ranks
+    if not args.quiet:
+        print(f"[launch] {args.world_size} ranks, GPUs shared: {shared}", flush=True)
     import torch.multiprocessing as mp
     mp.spawn(_spawn_entry, args=(args,), nprocs=args.world_size, join=True)
 
