@@ -163,6 +163,19 @@ def gpus_shared(world: int, colocated: bool, mode: str = "fedavg") -> bool:
 SHARED_GPU_QUEUES = "2"
 
 
+def cap_shared_queues() -> None:
+    """Lower GPU_MAX_HW_QUEUES to FEDTGAN_SHARED_HW_QUEUES (default 2) for ranks that share a GPU; a
+    lower value already in the environment is kept (boxes often export HIP's default, 4)."""
+    target = int(os.environ.get("FEDTGAN_SHARED_HW_QUEUES", SHARED_GPU_QUEUES))
+    cur = os.environ.get("GPU_MAX_HW_QUEUES")
+    try:
+        keep = cur is not None and int(cur) <= target
+    except ValueError:
+        keep = False
+    if not keep:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(target)
+
+
 def run_rank(rank: int, args) -> None:
     """One process of the federation (the reference ``run()``, `Server/dtds/distributed.py:838-891`)."""
     from .fed.runtime import FedRuntime
@@ -170,7 +183,8 @@ def run_rank(rank: int, args) -> None:
     from .parallel.comm import Comm
     world = args.world_size
     colocated = args.colocated
-    if "GPU_MAX_HW_QUEUES" not in os.environ and args.backend != "torch" and gpus_shared(world, colocated, args.mode):
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) > int(SHARED_GPU_QUEUES) and args.backend != "torch" \
+            and gpus_shared(world, colocated, args.mode):
         print(f"[rank {rank}] several ranks share a GPU: export GPU_MAX_HW_QUEUES={SHARED_GPU_QUEUES} before "
               "starting each rank (HIP's default 4 queues per process get time-sliced)", flush=True)
     device = pick_device(rank, colocated, args.backend, args.mode)
@@ -223,7 +237,7 @@ def main(argv: Optional[List[str]] = None) -> None:
         args.port = free_port()
     shared = args.backend != "torch" and gpus_shared(args.world_size, args.colocated, args.mode)
     if shared:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", SHARED_GPU_QUEUES)   # inherited by the spawned ranks
+        cap_shared_queues()       # inherited by the spawned ranks
     if not args.quiet:
         print(f"[launch] {args.world_size} ranks, GPUs shared: {shared}", flush=True)
     import torch.multiprocessing as mp
