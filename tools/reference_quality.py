@@ -58,7 +58,8 @@ class FakeRRefAsync(FakeRRef):
         return _Async(self.obj)
 
 
-def run_seed(ref_dir: str, work: str, seed: int, epochs: int, bootstrap: int) -> dict:
+def run_seed(ref_dir: str, work: str, seed: int, epochs: int, bootstrap: int, csv_epochs=None,
+             utility: bool = False) -> dict:
     import pandas as pd
     import torch
     os.makedirs(work)
@@ -82,16 +83,31 @@ def run_seed(ref_dir: str, work: str, seed: int, epochs: int, bootstrap: int) ->
     np.savez(os.path.join("models", "Intrusion_train.npz"), train=np.concatenate([c.train for c in clients]))
     server.server_local_synthesizer_initialization()
     t_init = time.time() - t0
+    if csv_epochs is not None:      # long runs: the reference's sample_data only on the scored epochs
+        keep = set(csv_epochs) | {epochs - 1}
+        orig = server.sample_data
+        server.sample_data = lambda i: orig(i) if i in keep else None
     server.fit()
     times = pd.read_csv("timestamp_experiment.csv", header=None).iloc[:, 0].tolist()
     res = []
-    for ep in range(epochs):
+    scored = sorted(set(csv_epochs) | {epochs - 1}) if csv_epochs is not None else list(range(epochs))
+    for ep in scored:
         jsd, wd = rsim.stat_sim_normalize(train_path, f"Intrusion_result/Intrusion_synthesis_epoch_{ep}.csv",
                                           list(CATEGORICAL))
         res.append((float(jsd), float(wd)))
-    return {"seed": seed, "init_s": t_init, "round_s": times, "avg_jsd": [r[0] for r in res],
-            "avg_wd": [r[1] for r in res], "weights": np.asarray(server.weights_con_cat_combination).tolist(),
-            "steps_per_epoch": [int(c.steps_per_epoch) for c in clients]}
+    out = {"seed": seed, "init_s": t_init, "round_s": times, "epochs": scored, "avg_jsd": [r[0] for r in res],
+           "avg_wd": [r[1] for r in res], "weights": np.asarray(server.weights_con_cat_combination).tolist(),
+           "steps_per_epoch": [int(c.steps_per_epoch) for c in clients]}
+    if utility:     # the reference's utility_analysis protocol on the last epoch (real vs synthetic rows)
+        import utility_analysis as rutil    # (reference)
+        real, hold = pd.read_csv(train_path), pd.read_csv(os.path.join(os.path.dirname(train_path), "holdout.csv"))
+        fake = pd.read_csv(f"Intrusion_result/Intrusion_synthesis_epoch_{epochs - 1}.csv")
+        orig_real = pd.concat([real, hold])
+        ru = rutil.real_res(orig_real, real, hold, TARGET, list(CATEGORICAL))
+        fu = rutil.real_res(orig_real, fake, hold, TARGET, list(CATEGORICAL))
+        diff = np.asarray(ru) - np.asarray(fu)
+        out["utility_final"] = {"diff": diff.tolist(), "f1_gap": float(diff.mean(axis=0)[1])}
+    return out
 
 
 def main():
@@ -102,6 +118,9 @@ def main():
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2, 3])
     ap.add_argument("--bootstrap-rows", type=int, default=20000)
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "reference_quality_r2.json"))
+    ap.add_argument("--csv-epochs", type=int, nargs="*", default=None, help="only these epochs' CSVs (+ the last)")
+    ap.add_argument("--utility", action="store_true", help="ML-utility gap of the last epoch")
+    ap.add_argument("--threads", type=int, default=0)
     args = ap.parse_args()
     shutil.rmtree(args.work, ignore_errors=True)
     shim = os.path.join(args.work, "shim")
@@ -111,15 +130,19 @@ def main():
     sys.dont_write_bytecode = True
     sys.path[:0] = [shim, args.reference]      # ahead of this repo's own `dtds` shim
     import torch
-    torch.set_num_threads(os.cpu_count() or 8)
+    torch.set_num_threads(args.threads or os.cpu_count() or 8)
     runs = []
     for seed in args.seeds:
-        r = run_seed(args.reference, os.path.join(args.work, f"s{seed}"), seed, args.epochs, args.bootstrap_rows)
+        r = run_seed(args.reference, os.path.join(args.work, f"s{seed}"), seed, args.epochs, args.bootstrap_rows,
+                     args.csv_epochs, args.utility)
         runs.append(r)
         print(json.dumps(r), flush=True)
-    summary = {"avg_jsd_mean": np.mean([r["avg_jsd"] for r in runs], axis=0).round(4).tolist(),
+    summary = {"epochs": runs[0]["epochs"],
+               "avg_jsd_mean": np.mean([r["avg_jsd"] for r in runs], axis=0).round(4).tolist(),
                "avg_wd_mean": np.mean([r["avg_wd"] for r in runs], axis=0).round(4).tolist(),
                "round_s_mean": float(np.mean([np.mean(r["round_s"]) for r in runs]))}
+    if args.utility:
+        summary["f1_gap_mean"] = float(np.mean([r["utility_final"]["f1_gap"] for r in runs]))
     with open(args.out, "w") as f:
         json.dump({"protocol": __doc__, "bootstrap_rows": args.bootstrap_rows, "runs": runs, "summary": summary}, f,
                   indent=1)
