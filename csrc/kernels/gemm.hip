@@ -737,6 +737,8 @@ static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3
     if (g2.tb) FEDTGAN_PAIR(64, false, true); else FEDTGAN_PAIR(64, false, false);
   } else if (g1.tile == 32) {
     if (g2.tb) FEDTGAN_PAIR(32, false, true); else FEDTGAN_PAIR(32, false, false);
+  } else if (g1.tile == 128) {
+    if (g2.tb) FEDTGAN_PAIR(128, false, true); else FEDTGAN_PAIR(128, false, false);
   } else {
     return false;
   }

@@ -93,6 +93,7 @@ class EngineConfig:
     # conditional block c (exactly one 1 per row) is a gathered weight column in the epilogue
     onehot: bool = True
     onehot_trans: bool = False   # training: gather from per-step [C, N] copies (A/B knob; generation always does)
+    dw0_tile: int = 0            # HIP: output tile of D0's weight-gradient GEMM (0 = planner's choice)
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -558,7 +559,8 @@ class CTGANEngine:
         pair = self.lanes is None     # weight gradient + R product of a layer: one launch
         for i in range(L):
             with self._lane(1 + i % 2):
-                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=1 if pair else 0)
+                kw = {"tile": self.cfg.dw0_tile} if (i == 0 and self.cfg.dw0_tile and self.ops.name == "hip") else {}
+                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=1 if pair else 0, **kw)
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
                    group=2 if pair else 0)
             inp = self.dl[i][I]

@@ -148,7 +148,7 @@ class HipOps:
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
              slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None,
-             bn_part=None, bn_rpg=0):
+             bn_part=None, bn_rpg=0, tile=None):
         """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
         onehot = (W_c [N, C], col [M], opt [M], cond_offset[, transposed]): A holds only the dense input
@@ -160,8 +160,8 @@ class HipOps:
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
         kc = 64 if self.f32 else 128
-        tile, sk = _plan(M, N, K, kc)
-        tile = self.tile_override or tile
+        tile_p, sk = _plan(M, N, K, kc)
+        tile = self.tile_override or tile or tile_p
         sk = _effective_splits(K, self.split_override or sk, kc)
         ws = None
         if sk > 1:

@@ -71,6 +71,14 @@ def bn_ab(eng, dev):
             print(f"bn_fused={int(fused)}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
 
 
+def dw0_tile_ab(eng, dev):
+    """D0 weight-gradient GEMM (paired with R0): planner tile vs 128x128 (fewer, fatter workgroups)."""
+    for rep in range(3):
+        for t in (0, 128):
+            eng.cfg.dw0_tile = t
+            print(f"dw0_tile={t}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
+
+
 def gen_only(eng, tr, X, dev):
     """generate_decoded(40000): eager vs hipGraph, chunk 8192 vs one chunk (wall time per call)."""
     from fed_tgan_amd.models.samplers import CondTables
@@ -150,6 +158,7 @@ def main():
     ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
     ap.add_argument("--onehot-ab", action="store_true", help="step + generation: dense c block vs one-hot gather")
     ap.add_argument("--bn-ab", action="store_true", help="step: BN from GEMM partials vs full-reduction BN kernel")
+    ap.add_argument("--dw0-ab", action="store_true", help="step: D0 weight-gradient tile 64 vs 128")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -168,6 +177,8 @@ def main():
         return onehot_ab(eng, tr, X, dev)
     if args.bn_ab:
         return bn_ab(eng, dev)
+    if args.dw0_ab:
+        return dw0_tile_ab(eng, dev)
     if args.unroll:
         return unroll_sweep(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
