@@ -30,13 +30,13 @@ def _kfd_gpu_nodes(root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
     return n
 
 
-def visible_gpu_count() -> int:
-    """GPUs this process would see, without initialising HIP."""
-    total = _kfd_gpu_nodes()
+def visible_gpu_count(root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this process would see, without initialising HIP: the driver's GPU nodes, capped by the
+    length of every *_VISIBLE_DEVICES list that is set (an empty list hides every GPU)."""
+    total = _kfd_gpu_nodes(root)
     for var in _VIS_VARS:
         v = os.environ.get(var)
-        if v is not None:
-            v = v.strip()
-            ids = [x for x in v.split(",") if x.strip() != ""] if v else []
-            total = min(total, len(ids)) if total else len(ids) if _kfd_gpu_nodes() else 0
+        if v is None:
+            continue
+        total = min(total, len([x for x in v.split(",") if x.strip()]))
     return total
