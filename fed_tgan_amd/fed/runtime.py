@@ -292,6 +292,8 @@ class FedRuntime:
         if cfg.resume:
             self.load_checkpoint()
         self.csv_cols = csv_columns(merged, self.vocabs) if not spec.date_dic else None
+        # RCCL's lazy communicator / P2P setup happens here, not in round 0
+        c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
 
