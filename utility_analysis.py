@@ -15,8 +15,7 @@ import pandas as pd
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from fed_tgan_amd.data.schema import get_spec  # noqa: E402
-from fed_tgan_amd.eval.utility import real_res  # noqa: E402,F401
-from fed_tgan_amd.eval.utility import utility_difference  # noqa: E402
+from fed_tgan_amd.eval.utility import real_res  # noqa: E402
 
 
 def main(argv=None):
@@ -31,9 +30,13 @@ def main(argv=None):
     real = pd.read_csv(args.train_path)
     test = pd.read_csv(args.test_path)
     fake = pd.read_csv(args.synthetic_path)
+    original_real = pd.concat([real, test])
     print("=========== evaluation for real data===============")
+    real_utility = real_res(original_real, real, test, spec.target_column, spec.categorical_list)
     print("=========== evaluation for synthetic data===============")
-    diff, f1 = utility_difference(real, test, fake, spec.target_column, spec.categorical_list)
+    fake_utility = real_res(original_real, fake, test, spec.target_column, spec.categorical_list)
+    diff = np.array(real_utility) - np.array(fake_utility)
+    f1 = float(diff.mean(axis=0)[1])
     print("difference in accuracy and f1-score for all AL algorithms: ", diff)
     print("difference in f1-score: ", f1)
     return diff, f1
