@@ -8,11 +8,16 @@ writes ``{name}_statistical_similarity_analysis.csv`` with columns
 import argparse
 import os
 import sys
+import warnings
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from fed_tgan_amd.data.schema import get_spec  # noqa: E402
 from fed_tgan_amd.eval.similarity import similarity_table, stat_sim_normalize  # noqa: E402,F401
+
+
+if not sys.warnoptions:          # as the reference scripts do
+    warnings.simplefilter("ignore")
 
 
 def main(argv=None):

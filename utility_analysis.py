@@ -8,6 +8,7 @@ mean F1 difference.
 import argparse
 import os
 import sys
+import warnings
 
 import numpy as np
 import pandas as pd
@@ -16,6 +17,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from fed_tgan_amd.data.schema import get_spec  # noqa: E402
 from fed_tgan_amd.eval.utility import real_res  # noqa: E402
+
+
+if not sys.warnoptions:          # as the reference scripts do
+    warnings.simplefilter("ignore")
 
 
 def main(argv=None):
