@@ -107,6 +107,8 @@ class FedConfig:
     # sync: None = on when real process groups exist (multi-rank runs, --force-dist), off otherwise
     # (one plain GPU rank, in-process emulation: the extra syncs cost ~2-10 % of a round there)
     phase_detail: Optional[bool] = None
+    # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
+    save_generator: bool = True
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -530,6 +532,8 @@ class FedRuntime:
             self.write_timestamps()
             if cfg.dump_real:
                 self.merge_real_shards()
+            if cfg.save_generator:
+                self.save_generator()
 
     def epoch_stamps(self) -> List[float]:
         """Per-round entries of ``timestamp_experiment.csv``, each INCLUDING that round's CSV dump.
@@ -551,6 +555,18 @@ class FedRuntime:
             out.append(done - prev)
             prev = done
         return prior + out
+
+    def save_generator(self, path: Optional[str] = None) -> str:
+        """The aggregated generator + transformer + sampler tables + decode metadata in one
+        weights-only file (`fed_tgan_amd.models.generator_io`); the reference's unused
+        ``save_model`` (`Server/dtds/distributed.py:560-563`) made usable."""
+        from ..models.generator_io import export_generator
+        if path is None:
+            d = os.path.join(self.cfg.out_dir, "models")
+            os.makedirs(d, exist_ok=True)
+            path = os.path.join(d, f"{self.name}_generator.pt")
+        return export_generator(path, self.engine, self.transformer, self.gen_cond, self.global_meta, self.vocabs,
+                                self.name)
 
     def write_timestamps(self):
         """One per-round wall time per line, no header (`Server/dtds/distributed.py:827-829`)."""

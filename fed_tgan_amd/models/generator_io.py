@@ -1,0 +1,93 @@
+"""Export the trained (aggregated) generator and sample from it later, without the federation.
+
+The reference's federator has a ``save_model`` that pickles ``[generator, cond, transformer,
+batch_size, embedding_dim]`` (`Server/dtds/distributed.py:560-563`), but nothing calls it and the
+pickle needs the reference classes to load.  Here the federator writes ONE self-contained file after
+the last round (``models/{name}_generator.pt``):
+
+* the flat G / D / BN buffer and the engine configuration,
+* the fitted VGM transformer (plain dict: meta, VGM posteriors, valid modes),
+* the global span counts of the generation-time conditional sampler,
+* the merged table meta and the label vocabularies (for the CSV decode).
+
+Everything is tensors, lists, strings and numbers, so it loads with
+``torch.load(..., weights_only=True)`` (no unpickling of code).  ``python -m dtds.sample`` then
+regenerates any number of rows on the GPU (HIP engine, eval-mode BN, Gumbel-argmax decode) or the
+CPU, and writes the same CSV as the per-epoch dumps.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..data.decode import csv_columns, decode_frame
+from ..data.vocab import CategoryVocab
+from ..features.transformer import VGMTransformer
+from .engine import CTGANEngine, EngineConfig
+from .samplers import CondTables
+
+FORMAT = "fed_tgan_amd.generator/1"
+
+
+def export_generator(path: str, engine: CTGANEngine, transformer: VGMTransformer, gen_cond: CondTables,
+                     meta: dict, vocabs, name: str) -> str:
+    cfg = dataclasses.asdict(engine.cfg)
+    state = {
+        "format": FORMAT,
+        "name": name,
+        "engine_cfg": json.dumps(cfg),
+        "flat": engine.flat.detach().cpu().clone(),
+        "bn_batches": int(engine.bn_batches),
+        "transformer": json.dumps(transformer.to_dict()),
+        "span_counts": torch.as_tensor(np.asarray(gen_cond.counts, dtype=np.float64)),
+        "meta": json.dumps(meta, default=lambda o: o.item() if hasattr(o, "item") else str(o)),
+        "vocabs": [[v.column_name, list(v.tolist())] for v in vocabs],
+    }
+    torch.save(state, path)
+    return path
+
+
+@dataclasses.dataclass
+class LoadedGenerator:
+    name: str
+    engine: CTGANEngine
+    transformer: VGMTransformer
+    meta: dict
+    vocabs: list
+
+    def sample(self, n: int) -> np.ndarray:
+        """[n, n_columns] decoded values (label codes for categoricals), float64."""
+        return self.engine.generate_decoded(int(n)).cpu().numpy()
+
+    def write_csv(self, path: str, n: int, threads: int = 0) -> str:
+        vals = self.sample(n)
+        if not self.meta.get("date_info"):
+            from ..utils import csvio
+            if csvio.available():
+                names, kinds, vocab_lists = csv_columns(self.meta, self.vocabs)
+                csvio.write_table(path, vals, names, kinds, vocab_lists, threads=threads)
+                return path
+        decode_frame(vals, self.meta, self.vocabs).to_csv(path, index=False)
+        return path
+
+
+def load_generator(path: str, device: Optional[torch.device] = None, backend: str = "auto",
+                   seed: int = 0) -> LoadedGenerator:
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    if st.get("format") != FORMAT:
+        raise ValueError(f"{path}: not a {FORMAT} file")
+    device = device or (torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
+    cfg = json.loads(st["engine_cfg"])
+    cfg = {k: tuple(v) if isinstance(v, list) else v for k, v in cfg.items()}
+    ecfg = EngineConfig(**cfg)
+    tr = VGMTransformer.from_dict(json.loads(st["transformer"]))
+    eng = CTGANEngine(tr.layout, ecfg, device, backend=backend, seed=seed)
+    eng.flat.copy_(st["flat"].to(device))
+    eng.bn_batches = int(st["bn_batches"])
+    eng.set_generation_tables(CondTables(tr.layout, st["span_counts"].numpy()), tr)
+    vocabs = [CategoryVocab(lst, name) for name, lst in st["vocabs"]]
+    return LoadedGenerator(st["name"], eng, tr, json.loads(st["meta"]), vocabs)

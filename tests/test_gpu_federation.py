@@ -118,3 +118,20 @@ def test_bench_one_gpu_rccl_data_plane():
     assert rec["config"]["data_plane"] == "nccl" and rec["n_gpus"] == 1
     assert rec["consistency"]["flat_identical"] and rec["consistency"]["csv_rows"] == 3000
     assert "allreduce" in rec["phase_s"]
+
+
+def test_saved_generator_on_gpu(tmp_path):
+    """models/{name}_generator.pt from a HIP run reloads into a fresh HIP engine (weights-only load)
+    whose generation pass matches the runtime's engine bit for bit (same seed, same Philox draws)."""
+    from fed_tgan_amd.models.generator_io import load_generator
+    from fed_tgan_amd.ops import native
+    native.require()
+    rt = FedRuntime(_cfg(tmp_path, epochs=1), Comm(0, 1, [0], "gloo", device=DEV), DEV)
+    rt.initialize()
+    rt.fit()
+    gen = load_generator(str(tmp_path / "models" / "Intrusion_generator.pt"), DEV, backend="hip", seed=5)
+    assert gen.engine.ops.name == "hip" and torch.equal(gen.engine.flat, rt.engine.flat)
+    a = gen.sample(3000)
+    assert a.shape == (3000, 42) and np.isfinite(a).all()
+    gen.write_csv(str(tmp_path / "g.csv"), 2500)
+    assert pd.read_csv(tmp_path / "g.csv").shape == (2500, 42)
