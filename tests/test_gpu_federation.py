@@ -122,7 +122,7 @@ def test_bench_one_gpu_rccl_data_plane():
 
 def test_saved_generator_on_gpu(tmp_path):
     """models/{name}_generator.pt from a HIP run reloads into a fresh HIP engine (weights-only load)
-    whose generation pass matches the runtime's engine bit for bit (same seed, same Philox draws)."""
+    holding exactly the run's final weights, and generates / writes a full-width table."""
     from fed_tgan_amd.models.generator_io import load_generator
     from fed_tgan_amd.ops import native
     native.require()
