@@ -20,8 +20,8 @@ layout: one process per GPU, RCCL data plane).
 New flags: -config (dataset spec JSON or builtin name), -backend {auto,hip,torch},
 -precision {bf16,fp32}, -data_backend {auto,gloo,nccl}, -synthetic_rows, -shard
 {independent,iid,dirichlet,skew}, -alpha, -n_sample, -aggregation {weighted,uniform}, -gmm
-{torch,sklearn}, -seed, -out_dir, -ckpt_every, -resume, -local_clients (single-process
-multi-client emulation), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan},
+{torch,sklearn}, -seed, -out_dir, -ckpt_every, -resume, -local_clients K (K clients per process,
+as threads sharing its GPU; with -world_size N: N*K clients over N ranks), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan},
 -init {independent,broadcast} (initial weights; independent = the reference's per-client init).
 """
 from __future__ import annotations
@@ -52,7 +52,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-datapath", type=str, default="data/raw/Intrusion_train.csv")
     p.add_argument("-epochs", type=int, default=10)
     p.add_argument("-E_interval", type=int, default=1)
-    p.add_argument("-world_size", type=int, default=2)
+    p.add_argument("-world_size", type=int, default=None, help="processes (default 2; 1 with -local_clients)")
     p.add_argument("-report", action="store_true")
     p.add_argument("-problem_type", type=str, default=None)
     p.add_argument("-target_column", type=str, default=None)
@@ -192,7 +192,7 @@ def run_rank(rank: int, args) -> None:
         print(f"[rank {rank}] device {device}, GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES', 'default')}",
               flush=True)
     if device.type == "cpu":   # several ranks on one host: do not oversubscribe the cores
-        torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world, 1)))
+        torch.set_num_threads(max(1, (os.cpu_count() or 4) // max(world * max(args.local_clients, 1), 1)))
     client_ranks = list(range(world)) if colocated else list(range(1, world))
     data_backend = args.data_backend
     if data_backend == "auto":
@@ -202,6 +202,12 @@ def run_rank(rank: int, args) -> None:
             data_backend = "nccl" if (device.type == "cuda" and colocated) else "gloo"
     comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
     try:
+        if args.local_clients:      # K clients as threads of this rank: clients rank*K .. rank*K+K-1
+            from .fed.local import run_local_emulation
+            run_local_emulation(fed_config_from_args(args), args.local_clients, backend=args.backend, device=device,
+                                outer=comm)
+            comm.barrier()
+            return
         cls = MDGANRuntime if args.mode == "mdgan" else FedRuntime
         rt = cls(fed_config_from_args(args), comm, device, federator=0)
         rt.initialize()
@@ -223,10 +229,17 @@ def free_port() -> int:
 
 def main(argv: Optional[List[str]] = None) -> None:
     args = build_parser().parse_args(argv)
+    if args.world_size is None:
+        args.world_size = 1 if args.local_clients else 2
     if args.local_clients:
-        from .fed.local import run_local_emulation
-        run_local_emulation(fed_config_from_args(args), args.local_clients, backend=args.backend)
-        return
+        if args.mode == "mdgan":
+            raise SystemExit("-local_clients: the MD-GAN split mode runs one client per process")
+        if args.rank is None and args.world_size <= 1:
+            from .fed.local import run_local_emulation
+            run_local_emulation(fed_config_from_args(args), args.local_clients, backend=args.backend)
+            return
+        # N processes x K clients each: every process runs clients, rank 0 hosts the federator
+        args.colocated = True
     if args.rank is not None:
         run_rank(args.rank, args)
         return

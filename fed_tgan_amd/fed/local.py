@@ -1,11 +1,18 @@
-"""Single-process multi-client emulation (``-local_clients K``).
+"""Several clients per process (``-local_clients K``).
 
-A ``gpurun`` box exposes one MI355X and RCCL forbids two ranks on one device, so the
-federation logic (init protocol, weighted aggregation, fault injection, sampling) is also run
-with K clients as K threads of one process sharing one GPU.  ``ThreadComm`` implements the
-:class:`~fed_tgan_amd.parallel.comm.Comm` collectives with a barrier and shared slots; the
-aggregation sums the clients' pre-scaled device buffers on the GPU.  Graph capture uses the
-thread-local capture mode so every client captures and replays its own step graph.
+RCCL allows one rank per device, so more clients than GPUs run as threads: K clients are K
+threads of one process sharing its GPU, each with its own HIP stream and its own captured step
+graph (thread-local capture mode).
+
+* ``ThreadComm`` -- one process, K clients: the :class:`~fed_tgan_amd.parallel.comm.Comm`
+  collectives over a thread barrier and shared slots; the aggregation sums the clients'
+  pre-scaled device buffers on the GPU.
+* ``HierComm`` -- N processes (one per GPU, ``-world_size N -local_clients K``), K clients each:
+  N*K clients in all, client ``r*K + t`` being thread ``t`` of rank ``r``.  Every collective is
+  two-level: the threads of a process combine on their shared GPU, thread 0 runs the process-level
+  collective (RCCL all-reduce / gather over xGMI, gloo for the control plane) on the combined
+  value, and the threads pick the result up.  One RCCL all-reduce per process per round instead of
+  one per client.
 """
 from __future__ import annotations
 
@@ -121,8 +128,156 @@ class ThreadComm(Comm):
         return flat
 
 
-def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[torch.device] = None):
-    """Run a K-client federation in one process; returns the federator's runtime (rank 0)."""
+class HierComm(Comm):
+    """Client ``outer.rank * K + t`` of ``outer.world_size * K``: thread ``t`` of this process.
+
+    Needs a co-located federation (every process runs clients; the federator is client 0, thread 0
+    of rank 0).  Only thread 0 touches the process-level ``outer`` communicator."""
+
+    def __init__(self, group: LocalGroup, thread: int, device: torch.device, outer: Comm):
+        k = group.k
+        n = outer.world_size
+        if outer.client_ranks != list(range(n)):
+            raise ValueError("several clients per process need every process to run clients (-colocated)")
+        super().__init__(outer.rank * k + thread, n * k, list(range(n * k)), outer.data_backend, device=device,
+                         init=False)
+        self.g, self.t, self.k, self.outer = group, thread, k, outer
+        self.dist_active = outer.dist_active
+
+    def data_world_size(self) -> int:
+        return self.outer.data_world_size() * self.k
+
+    # ---- thread-level building blocks
+    def _tgather(self, obj) -> list:
+        self.g.slots[self.t] = obj
+        self.g.wait()
+        out = list(self.g.slots)
+        self.g.wait()
+        return out
+
+    def _lead(self, fn):
+        """Thread 0 computes fn() (a process-level collective); every thread returns its result."""
+        if self.t == 0:
+            self.g.result = fn()
+        self.g.wait()
+        out = self.g.result
+        self.g.wait()
+        return out
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            device_sync(self.device)
+
+    # ---- control plane
+    def all_gather_object(self, obj):
+        local = self._tgather(obj)
+        return self._lead(lambda: [x for part in self.outer.all_gather_object(local) for x in part])
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.t == src % self.k:
+            self.g.result = obj
+        self.g.wait()
+        return self._lead(lambda: self.outer.broadcast_object(self.g.result, src=src // self.k))
+
+    def barrier(self):
+        self.g.wait()
+        self._lead(lambda: self.outer.barrier())
+
+    def heartbeat(self, timeout_s: float):
+        self.g.wait()
+        self._lead(lambda: self.outer.heartbeat(timeout_s))
+
+    def broadcast_tensor(self, t, src: int = 0):
+        self._sync()
+        if self.t == src % self.k:
+            self.g.result = t.detach().clone()
+        self.g.wait()
+
+        def bcast():
+            v = self.outer.broadcast_tensor(self.g.result, src=src // self.k)
+            self._sync()
+            return v
+        t.copy_(self._lead(bcast))
+        self._sync()
+        self.g.wait()
+        return t
+
+    def all_reduce_cpu(self, t, op=None):
+        parts = self._tgather(t.detach().clone())
+
+        def reduce():
+            total = parts[0].clone()
+            for x in parts[1:]:
+                total += x
+            return self.outer.all_reduce_cpu(total)
+        t.copy_(self._lead(reduce))
+        return t
+
+    def max_float(self, x: float) -> float:
+        m = max(self._tgather(float(x)))
+        return self._lead(lambda: self.outer.max_float(m))
+
+    def gather_bytes(self, payload, dst: int = 0):
+        out = self.all_gather_object(payload)
+        return out if self.rank == dst else None
+
+    # ---- data plane
+    def weighted_all_reduce(self, flat, weight: float):
+        """sum_i w_i * flat_i: the process' clients are summed on its GPU by thread 0, which then
+        runs ONE process-level all-reduce (weight 1: the terms are already scaled)."""
+        self._sync()
+        parts = self._tgather((flat, float(weight)))
+
+        def reduce():
+            acc = torch.zeros_like(flat)
+            for buf, w in parts:
+                if w != 0.0:
+                    acc.add_(buf, alpha=w)
+            self.outer.weighted_all_reduce(acc, 1.0)
+            self._sync()
+            return acc
+        flat.copy_(self._lead(reduce))
+        self._sync()
+        self.g.wait()
+        return flat
+
+    def share_with_federator(self, flat, federator: int = 0):
+        return flat         # co-located: the federator is a client and already holds the aggregate
+
+    def gather_rows(self, t, counts, ranks, dst: int = 0, to_host: bool = True):
+        """The process' client shares are concatenated on its GPU, then one process-level gather."""
+        if list(ranks) != self.client_ranks:
+            raise ValueError("HierComm.gather_rows gathers from every client, in client order")
+        self._sync()
+        parts = self._tgather(t)
+        k, n = self.k, self.outer.world_size
+
+        def gather():
+            me = self.outer.rank
+            local = torch.cat([p[:counts[me * k + i]] for i, p in enumerate(parts)])
+            per = [sum(counts[q * k:(q + 1) * k]) for q in range(n)]
+            out = self.outer.gather_rows(local, per, list(range(n)), dst=dst // k, to_host=to_host)
+            self._sync()
+            return out
+        out = self._lead(gather)
+        return out if self.rank == dst else None
+
+    def init_p2p(self):
+        raise NotImplementedError("MD-GAN split mode runs one client per process")
+
+    def warmup(self, width: int = 4, dst: int = 0, gather: bool = True):
+        self.g.wait()
+        self._lead(lambda: self.outer.warmup(width, dst=dst // self.k, gather=gather))
+
+    def destroy(self):
+        pass        # the process-level communicator belongs to the caller
+
+
+def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[torch.device] = None,
+                        outer: Optional[Comm] = None):
+    """Run K clients as threads of this process; returns the runtime of the process' first client
+    (the federator on rank 0).  With ``outer`` (a process-level Comm over N ranks) the threads are
+    clients ``outer.rank*K .. outer.rank*K + K-1`` of an N*K-client federation (``HierComm``)."""
     from .runtime import FedRuntime
     if device is None:
         device = torch.device("cuda", 0) if (torch.cuda.is_available() and backend != "torch") else torch.device("cpu")
@@ -141,7 +296,7 @@ def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[tor
                 if getattr(cfg, "client_streams", True):
                     stream_ctx = torch.cuda.stream(torch.cuda.Stream(device))
             with stream_ctx:
-                comm = ThreadComm(group, rank, device)
+                comm = ThreadComm(group, rank, device) if outer is None else HierComm(group, rank, device, outer)
                 rt = FedRuntime(cfg, comm, device, federator=0)
                 rt.thread_local_capture = True
                 runtimes[rank] = rt
@@ -153,11 +308,19 @@ def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[tor
             group.failed.set()
             group.barrier.abort()
 
+    # CPU clients: K threads each running intra-op parallel torch ops would oversubscribe the cores
+    # (measured: a 2-rank x 2-client CPU round 38 s with 4 intra-op threads per client, 1.3 s with 2)
+    n_threads = torch.get_num_threads()
+    if device.type == "cpu" and outer is None:
+        torch.set_num_threads(max(1, n_threads // k))
     threads = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(k)]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    finally:
+        torch.set_num_threads(n_threads)
     if errors:
         raise RuntimeError(f"local emulation failed: {errors[0]!r}")
     return runtimes[0]

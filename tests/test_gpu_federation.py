@@ -1,6 +1,7 @@
 """Federation on the GPU: the HIP engine inside FedRuntime (single client, and the in-process
-multi-client emulation with one HIP stream per client), and the asynchronous table path
-(pinned side-stream copy awaited by the background CSV writer)."""
+multi-client emulation with one HIP stream per client), several clients per process over several
+processes (HierComm), and the asynchronous table path (pinned side-stream copy awaited by the
+background CSV writer)."""
 import os
 
 import numpy as np
@@ -135,3 +136,31 @@ def test_saved_generator_on_gpu(tmp_path):
     assert a.shape == (3000, 42) and np.isfinite(a).all()
     gen.write_csv(str(tmp_path / "g.csv"), 2500)
     assert pd.read_csv(tmp_path / "g.csv").shape == (2500, 42)
+
+
+def test_hier_one_rank_rccl_two_clients(tmp_path):
+    """Two clients as threads over a one-rank RCCL process group (HierComm): the thread-level sum
+    on the GPU, then the process-level RCCL all-reduce and gather."""
+    from fed_tgan_amd.cli import free_port
+    from fed_tgan_amd.ops import native
+    native.require()
+    comm = Comm(0, 1, [0], "nccl", port=free_port(), device=DEV, force_dist=True)
+    try:
+        rt = run_local_emulation(_cfg(tmp_path, shard_mode="iid"), 2, backend="hip", device=DEV, outer=comm)
+        rt.flush_writes()
+        assert comm.data_world_size() == 1 and rt.comm.data_world_size() == 2
+    finally:
+        comm.destroy()
+    _check_outputs(tmp_path, 2, 3000)
+    assert len(rt.weights) == 2 and bool(torch.isfinite(rt.engine.flat).all())
+
+
+def test_hier_two_processes_two_clients_each(tmp_path):
+    """-world_size 2 -local_clients 2: four HIP clients, two per process, on the box's one GPU (gloo
+    data plane between the processes, as RCCL needs a GPU per rank)."""
+    r = _run(["-m", "dtds.distributed", "-world_size", "2", "-local_clients", "2", "-data_backend", "gloo", "-backend",
+              "hip", "-epochs", "2", "-synthetic_rows", "4000", "-n_sample", "3001", "-out_dir", str(tmp_path),
+              "-dump_real", "-quiet"], timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check_outputs(tmp_path, 2, 3001)
+    assert len(list((tmp_path / "data" / "raw").glob("Intrusion_train_client*.csv"))) == 4
