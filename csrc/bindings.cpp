@@ -58,7 +58,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& bn_rv, double bn_eps, bool f32, const optional<Tensor>& head_coef,
           const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group,
           const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
-          const optional<Tensor>& oh_off, bool oh_trans, const optional<Tensor>& bn_part, int64_t bn_rpg) {
+          const optional<Tensor>& oh_off, bool oh_trans, const optional<Tensor>& bn_part, int64_t bn_rpg,
+          const optional<Tensor>& tile_cnt) {
   check_f32_2d(a, "a");
   check_f32_2d(b, "b");
   check_f32_2d(c, "c");
@@ -146,6 +147,13 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.bn_part = fp(*bn_part);
     g.bn_rpg = (int)bn_rpg;
   }
+  if (tile_cnt.has_value() && tile_cnt->defined() && g.splitk > 1) {
+    // one arrival counter per output tile, all zero (the reducing workgroup re-zeroes its tile's)
+    const int64_t tiles = ((M + tile - 1) / tile) * ((N + tile - 1) / tile);
+    TORCH_CHECK(tile_cnt->is_cuda() && tile_cnt->scalar_type() == at::kInt && tile_cnt->is_contiguous() &&
+                    tile_cnt->numel() >= tiles, "gemm: tile_cnt must hold one int32 per output tile");
+    g.tile_cnt = reinterpret_cast<unsigned*>(tile_cnt->data_ptr<int>());
+  }
   // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
   // must be independent -- neither reads what the other writes); group 0: launch now
   thread_local fedtgan::GemmArgs held{};
@@ -161,6 +169,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   }
   if (group == 2) {
     TORCH_CHECK(has_held && held_stream == hs, "gemm: group 2 needs a held GEMM on the same stream");
+    TORCH_CHECK(!(held.splitk > 1 && g.splitk > 1 && held.ws == g.ws), "gemm: paired split-K GEMMs share a workspace");
+    TORCH_CHECK(!(held.tile_cnt && g.tile_cnt && held.tile_cnt == g.tile_cnt), "gemm: paired GEMMs share tile counters");
     has_held = false;
     fedtgan::launch_gemm_pair(held, g, hs);
     return;
@@ -717,6 +727,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gemm_store_wt = value ? 1 : 0;
     return prev;
   }
+  if (key == "gemm_splitk_inlaunch") {
+    const int64_t prev = fedtgan::g_gemm_splitk_inlaunch;
+    fedtgan::g_gemm_splitk_inlaunch = value ? 1 : 0;
+    return prev;
+  }
   if (key == "gemm_pairs") {
     const int64_t prev = fedtgan::g_gemm_pairs;
     fedtgan::g_gemm_pairs = value ? 1 : 0;
@@ -739,7 +754,8 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
       "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0, Tensor? oh_w=None, Tensor? oh_col=None, "
-      "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False, Tensor(f!)? bn_part=None, int bn_rpg=0) -> ()");
+      "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False, Tensor(f!)? bn_part=None, int bn_rpg=0, "
+      "Tensor(g!)? tile_cnt=None) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

@@ -54,6 +54,7 @@ unsigned check_status_gemm() { return 0u; }
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 constexpr int NT = 256;
 
@@ -357,6 +358,87 @@ struct Cfg {
   static constexpr int DEPTH = (!F32 && TM <= FEDTGAN_GEMM_DEPTH2_MAX_TM) ? 2 : 1;
 };
 
+// In-launch split-K reduction (GemmArgs::tile_cnt, 32/64 tiles, N % 4 == 0): the hand-off of
+// cdna_hip_programming.md's "projection GEMM" recipe in its write-through form --
+//   every K-slice workgroup stages its accumulators through LDS and stores its slab row-contiguously
+//   with 16-B write-through (sc1) stores; every wave waits for its stores; after a workgroup barrier
+//   one lane takes a ticket (relaxed agent-scope fetch_add on the tile's counter);
+//   the workgroup that draws the last ticket resets the counter for the next launch, reads every
+//   slab of the tile with sc1 loads (no acquire fence needed: all stores and loads of the slabs are
+//   sc1) and applies the epilogue, summing the slabs in the same order as gemm_splitk_epilogue (so
+//   both paths give bit-identical outputs).
+// Nothing waits on another workgroup (no spinning): every workgroup ends.
+template <int TM, int TN, int MI, int NJ>
+__device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (&acc)[MI][NJ], int m0, int n0, int tile,
+                                                int bz, int gz, int lane, int wm, int wn, unsigned char* smem,
+                                                uint64_t step) {
+  constexpr int WM = TM / 2, WN = TN / 2;
+  constexpr int LDT = TN + 4;   // LDS row stride (floats): float4 rows stay 16-B aligned
+  constexpr int Q = TN / 4;     // float4 per tile row
+  float* cs = reinterpret_cast<float*>(smem);
+  unsigned* last = reinterpret_cast<unsigned*>(smem + TM * LDT * 4);
+  __syncthreads();   // the stage buffers are free
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(g.ws, 0, 0x7FFFFFFF, 0x00020000);
+  const size_t slab = (size_t)g.M * g.N;
+  for (int e = threadIdx.x; e < TM * Q; e += NT) {
+    const int ml = e / Q, nl = 4 * (e % Q);
+    const int m = m0 + ml, n = n0 + nl;
+    if (m < g.M && n < g.N) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(&cs[ml * LDT + nl]);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ws,
+                                             (int)(((size_t)bz * slab + (size_t)m * g.N + n) * 4), 0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(&g.tile_cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned is_last = t == (unsigned)(gz - 1) ? 1u : 0u;
+    if (is_last) __hip_atomic_store(&g.tile_cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = is_last;
+  }
+  __syncthreads();
+  if (*last == 0u) return;
+  for (int e = threadIdx.x; e < TM * Q; e += NT) {
+    const int ml = e / Q, nl = 4 * (e % Q);
+    const int m = m0 + ml, n = n0 + nl;
+    if (m >= g.M || n >= g.N) continue;
+    const int base = (int)(((size_t)m * g.N + n) * 4);
+    f32x4 a4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z0 = 0; z0 < gz; z0 += 8) {     // 8 slab loads in flight per pass
+      f32x4 part[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int z = min(z0 + q, gz - 1);
+        part[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ws, base + (int)((size_t)z * slab * 4), 0, 16));
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (z0 + q < gz) a4[q & 3] += part[q];   // slab z adds into a4[z & 3] (z0 % 4 == 0)
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float v = g.alpha * ((a4[0][c] + a4[1][c]) + (a4[2][c] + a4[3][c]));
+      const int nn = n + c;
+      float* cp = g.c + (size_t)m * g.ldc + nn;
+      if (g.beta != 0.f) v += g.beta * (*cp);
+      if (g.bias) v += g.bias[nn];
+      if (g.oh_w) v += onehot_term(g, m, nn);
+      st_out(g.c, (size_t)m * g.ldc + nn, apply_epi(g, v, m, nn, step, (uint64_t)m * g.N + nn), g.wt);
+    }
+  }
+}
+
 // TM x TN output tile (64x64; 32x32 for short-K GEMMs that would otherwise need split-K; 128x128
 // for large-M x N GEMMs -- generation at M = 40k, wide tables -- where the operand re-reads of
 // small tiles make the GEMM L2-bandwidth-bound):
@@ -525,6 +607,12 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       }
   }
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  if constexpr (TM <= 64) {
+    if (gz > 1 && g.red_inl) {
+      splitk_inlaunch<TM, TN, MI, NJ>(g, acc, m0, n0, by * gx + bx, bz, gz, lane, wm, wn, smem, step);
+      return;
+    }
+  }
   if constexpr (TM >= 128) {
     // 64 accumulators per lane: a fully unrolled epilogue (Philox, loads, stores per element) is
     // past the unroller's budget and the accumulator array would land in scratch, so the tile goes
@@ -621,7 +709,8 @@ struct GemmShape {
 constexpr int GEMM_MAX_SPLITS = 64;
 int g_gemm_xcd_remap = 1;
 int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
-int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)   // 0 off, 1 long-K tiles only, 2 always
+int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)
+int g_gemm_splitk_inlaunch = 1;   // 1: split-K reduced by the last-arriving slice (GemmArgs::tile_cnt)
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
@@ -667,6 +756,8 @@ static dim3 gemm_prepare(GemmArgs& g) {
   // 13.1 -> 10.9 us, split D0 11.9 -> 11.5 us) and costs ~0.2 us of index math on short-K ones;
   // on 128x128-tile GEMMs over >= 8192 rows (generation) the N tiles of one A row block then share
   // an L2 whatever K is (generate_decoded(40000): 375 -> 360 us)
+  g.red_inl = g.tile_cnt != nullptr && g_gemm_splitk_inlaunch && g.splitk > 1 && T <= 64 && g.N % 4 == 0 &&
+              (int64_t)g.splitk * g.M * g.N * 4 < (int64_t)INT32_MAX;
   g.xcd_remap = g_gemm_xcd_remap == 2 ||
                 (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768) ||
                                            (T == 128 && tm >= 64)));
@@ -707,7 +798,7 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
 }
 
 static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
-  if (g.splitk <= 1) return;
+  if (g.splitk <= 1 || g.red_inl) return;
   const size_t total = (size_t)g.M * g.N;
   int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
   if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, dim3(blocks), dim3(256), 0, stream, g);

@@ -61,6 +61,12 @@ struct GemmArgs {
   float* bn_part;
   int bn_rpg;
   int oh_c;       // width of the one-hot block (checked build: gather index bound)
+  // Split-K reduced inside the GEMM launch (nullable): one arrival counter per output tile, zero
+  // between launches.  Every K-slice workgroup publishes its slab write-through and takes a ticket;
+  // the one that completes a tile sums the tile's slabs and applies the epilogue (no
+  // gemm_splitk_epilogue launch).  red_inl is set by the launcher where the shape allows it.
+  unsigned* tile_cnt;
+  int red_inl;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -179,6 +185,7 @@ extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
+extern int g_gemm_splitk_inlaunch;   // split-K reduced inside the GEMM launch where a tile counter is given (1)
 extern int g_act_row_mode;   // activation kernels on rows wider than 512: one workgroup per row (1) or per 1-4 rows
 extern int g_decode_rows;   // generation decode: one wave per row (1) or one thread per (row, column) (0)
 extern int g_bn_cols;   // BatchNorm kernels: columns per workgroup (4 / 8 / 16); set_tuning("bn_cols")

@@ -82,7 +82,13 @@ class HipOps:
         self.split_override = None   # int: force the split-K factor (tuning / microbenchmarks)
         self.tile_override = None    # 32 | 64: force the output tile (tuning / microbenchmarks)
         self.lane = 0          # set by the engine while it issues work on a side stream
-        self._ws: Dict[int, torch.Tensor] = {}
+        self._ws: Dict[Tuple[int, bool], torch.Tensor] = {}
+        self._cnt: Dict[Tuple[int, bool], torch.Tensor] = {}
+        # split-K partial slabs reduced by the last-arriving K-slice workgroup inside the GEMM launch
+        # (no gemm_splitk_epilogue launch).  A/B knob, default off: bit-identical but measured slower
+        # (the G-phase D0 forward 9.4 -> 11.7 us, full step 228 -> 230 us: the reducer reads its tile's
+        # 13-25 write-through slabs serially; profiles/splitk_inlaunch_ab_r2.txt)
+        self.splitk_inlaunch = False
         self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
         self._dec: Dict[int, Tuple] = {}
         self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
@@ -100,15 +106,29 @@ class HipOps:
         if native.CHECKED:
             native.check()
 
-    def _workspace(self, n: int) -> torch.Tensor:
-        """Split-K slab of the current lane (concurrent lanes never share one)."""
-        ws = self._ws.get(self.lane)
+    def _workspace(self, n: int, held: bool = False) -> torch.Tensor:
+        """Split-K slab of the current lane (concurrent lanes never share one; nor do the two GEMMs
+        of a pair: ``held`` = the first of the pair)."""
+        key = (self.lane, held)
+        ws = self._ws.get(key)
         if ws is None or ws.numel() < n:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")
             ws = torch.zeros(max(1 << 20, int(n * 1.25)), dtype=torch.float32, device=self.device)
-            self._ws[self.lane] = ws
+            self._ws[key] = ws
         return ws
+
+    def _tile_counters(self, n: int, held: bool = False) -> torch.Tensor:
+        """Arrival counters of the in-launch split-K reduction (per lane / pair slot like the
+        workspace; zero between launches: the reducing workgroup re-zeroes its tile's counter)."""
+        key = (self.lane, held)
+        t = self._cnt.get(key)
+        if t is None or t.numel() < n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("split-K tile counters must be sized before graph capture")
+            t = torch.zeros(max(n, 4096), dtype=torch.int32, device=self.device)
+            self._cnt[key] = t
+        return t
 
     def _bn_partials(self, n: int) -> torch.Tensor:
         """Per-tile BN partial-statistics buffer of the current lane (sized before graph capture)."""
@@ -163,15 +183,17 @@ class HipOps:
         tile_p, sk = _plan(M, N, K, kc)
         tile = self.tile_override or tile or tile_p
         sk = _effective_splits(K, self.split_override or sk, kc)
-        ws = None
+        ws = cnt = None
         if sk > 1:
-            ws = self._workspace(sk * M * N)
+            ws = self._workspace(sk * M * N, held=group == 1)
+            if self.splitk_inlaunch:
+                cnt = self._tile_counters(-(-M // tile) * -(-N // tile), held=group == 1)
         g = bn or (None, None, None, None)
         self.L.gemm(a, b, c, bool(ta), bool(tb), float(alpha), float(beta), bias, int(epi), ms, float(slope),
                     float(p_drop), ws, int(sk), self.seed, self.ctr, int(stream_id), g[0], g[1], g[2], g[3],
                     float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group),
                     *(onehot[:4] if onehot else (None, None, None, None)),
-                    bool(onehot is not None and len(onehot) > 4 and onehot[4]), bn_part, int(bn_rpg))
+                    bool(onehot is not None and len(onehot) > 4 and onehot[4]), bn_part, int(bn_rpg), cnt)
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):

@@ -776,3 +776,78 @@ def test_linear_bn_relu_from_gemm_partials(hip32, rows, groups, tile):
     hip32.bn_fused, hip32.tile_override = False, None
     for name, a, b in zip(("out", "nhat", "mean", "invstd", "rm", "rv"), res[True], res[False]):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), name
+
+
+@pytest.mark.parametrize("case", ["relu", "lrelu_head", "mask_beta", "onehot", "tile64", "pair"])
+def test_gemm_splitk_inlaunch_matches_epilogue_kernel(hip, hip32, case):
+    """Split-K reduced by the last-arriving K-slice workgroup (tile counters) gives bit-identical
+    outputs to the separate gemm_splitk_epilogue launch -- same slab sum order, same epilogue --
+    over repeated launches (the reducer re-zeroes the counters) and inside a replayed hipGraph."""
+    ops = hip32 if case == "onehot" else hip
+
+    def jobs():
+        if case == "relu":
+            return [dict(a=mat(50, 9000, seed=90) * 0.1, b=mat(256, 9000, seed=91) * 0.1, tb=True, bias=mat(256, seed=92),
+                         epi=3, out=(50, 256))]
+        if case == "lrelu_head":
+            return [dict(a=mat(150, 6280, seed=93), b=mat(256, 6280, seed=94), tb=True, bias=mat(256, seed=95), epi=1,
+                         ms=torch.zeros(150, 256, device=DEV), head=(mat(150, seed=96), mat(256, seed=97),
+                                                                      torch.zeros(150, 256, device=DEV)),
+                         out=(150, 256))]
+        if case == "mask_beta":
+            ms = (mat(50, 256, seed=98) > 0).float() * 2
+            return [dict(a=mat(50, 6280, seed=99), b=mat(256, 6280, seed=100), tb=True, beta=1.0, epi=2, ms=ms,
+                         c0=mat(50, 256, seed=101), out=(50, 256))]
+        if case == "onehot":
+            Wc = mat(256, 300, seed=102)
+            col = torch.randint(0, 3, (60,), device=DEV, dtype=torch.int32)
+            opt = torch.randint(0, 100, (60,), device=DEV, dtype=torch.int32)
+            off = torch.tensor([0, 100, 200], device=DEV, dtype=torch.int32)
+            return [dict(a=mat(60, 5000, seed=103), b=mat(256, 5000, seed=104), tb=True, bias=mat(256, seed=105),
+                         onehot=(Wc, col, opt, off), out=(60, 256))]
+        if case == "tile64":
+            return [dict(a=mat(130, 7000, seed=106), b=mat(200, 7000, seed=107), tb=True, tile=64, out=(130, 200))]
+        A, X, W = mat(150, 256, seed=108), mat(150, 6280, seed=109), mat(256, 6280, seed=110)
+        ms = (mat(50, 256, seed=111) > 0).float() * 2
+        return [dict(a=A, b=X, ta=True, out=(256, 6280), group=1),
+                dict(a=X[:50], b=W, tb=True, epi=2, ms=ms, out=(50, 256), group=2)]
+
+    def run(inlaunch, graph=False):
+        torch.manual_seed(0)
+        js = jobs()
+        outs = [j.pop("c0").clone() if "c0" in j else torch.zeros(*j["out"], device=DEV) for j in js]
+        for j in js:
+            j.pop("out")
+        ops.splitk_inlaunch = inlaunch
+        saved = ops.ctr.clone()
+        try:
+            def launch():
+                for j, c in zip(js, outs):
+                    ops.gemm(c=c, **j)
+            if case in ("relu", "mask_beta", "onehot", "tile64"):
+                ops.split_override = 13
+            launch()                              # sizes the workspace / counters
+            for _ in range(2):
+                launch()                          # counters must be back at zero
+            if graph:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    launch()
+                for _ in range(3):
+                    g.replay()
+        finally:
+            ops.split_override = None
+            ops.splitk_inlaunch = False
+            ops.ctr.copy_(saved)
+        torch.cuda.synchronize()
+        extra = [j["ms"] for j in js if j.get("epi") == 1] + [j["head"][2] for j in js if j.get("head")]
+        return outs + extra
+
+    ref = run(False)
+    got = run(True)
+    for r, o in zip(ref, got):
+        assert torch.equal(r, o)
+    got_g = run(True, graph=True)
+    ref_g = run(False, graph=True)
+    for r, o in zip(ref_g, got_g):
+        assert torch.equal(r, o)

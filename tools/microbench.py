@@ -79,6 +79,27 @@ def dw0_tile_ab(eng, dev):
             print(f"dw0_tile={t}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
 
 
+def inlaunch_ab(eng, dev):
+    """Split-K reduction: separate gemm_splitk_epilogue launch vs the last-arriving K-slice workgroup
+    (tile counters) -- the step's split GEMMs alone, then the full captured step."""
+    from fed_tgan_amd.ops.hip import EPI_LRELU_DROPOUT
+    o, nP = eng.ops, eng.nP
+    X = eng.X
+    shapes = {
+        "D0 fwd 3nP x256 xDin lrelu+drop": (X, eng.p["D.0.W"], eng.dl[0], dict(tb=True, bias=eng.p["D.0.b"],
+                                                                              epi=EPI_LRELU_DROPOUT, ms=eng.ms[0])),
+        "D0 fwd nP x256 xDin (G phase)": (X[:nP], eng.p["D.0.W"], eng.dl[0][:nP], dict(tb=True)),
+    }
+    for rep in range(2):
+        for inl in (False, True):
+            o.splitk_inlaunch = inl
+            row = [per_call(lambda: o.gemm(a, b, c, **kw), dev) for a, b, c, kw in shapes.values()]
+            t_step = per_call(eng._one_step, dev, n=5, reps=20)
+            print(f"splitk_inlaunch={int(inl)}: " + "  ".join(f"{k} {v:6.2f} us" for k, v in zip(shapes, row)) +
+                  f"   full step {t_step:8.2f} us", flush=True)
+    o.splitk_inlaunch = False
+
+
 def gen_only(eng, tr, X, dev):
     """generate_decoded(40000): eager vs hipGraph, chunk 8192 vs one chunk (wall time per call)."""
     from fed_tgan_amd.models.samplers import CondTables
@@ -159,6 +180,7 @@ def main():
     ap.add_argument("--onehot-ab", action="store_true", help="step + generation: dense c block vs one-hot gather")
     ap.add_argument("--bn-ab", action="store_true", help="step: BN from GEMM partials vs full-reduction BN kernel")
     ap.add_argument("--dw0-ab", action="store_true", help="step: D0 weight-gradient tile 64 vs 128")
+    ap.add_argument("--inlaunch-ab", action="store_true", help="split-K: epilogue launch vs in-launch reduction")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -179,6 +201,8 @@ def main():
         return bn_ab(eng, dev)
     if args.dw0_ab:
         return dw0_tile_ab(eng, dev)
+    if args.inlaunch_ab:
+        return inlaunch_ab(eng, dev)
     if args.unroll:
         return unroll_sweep(eng, dev)
     res["rng_bump (1 thread)"] = per_call(lambda: o.L.rng_bump(o.ctr), dev)
