@@ -39,6 +39,21 @@ bool vec_ok(const Tensor& t) {
   return t.storage_offset() + (t.size(0) - 1) * ld + ext4 <= storage;
 }
 
+// bf16 GEMM operand (GemmArgs::bin): k-contiguous rows, 16-B aligned base, ld % 8 == 0, and every
+// row's extent rounded up to 8 inside the storage (the kernel's 16-B loads are clamped to that).
+void check_bf16_operand(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2, name, " must be a 2-D bf16 GPU tensor");
+  TORCH_CHECK(t.size(1) <= 1 || t.stride(1) == 1, name, " must have unit column stride");
+  const int64_t ld = ld_of(t);
+  const int64_t ext8 = (t.size(1) + 7) / 8 * 8;
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && ld % 8 == 0 && ext8 <= ld, name,
+              ": bf16 operands need a 16-B aligned base and a leading dimension divisible by 8 covering the row");
+  const int64_t storage = (int64_t)(t.storage().nbytes() / 2);
+  TORCH_CHECK(t.storage_offset() + (t.size(0) - 1) * ld + ext8 <= storage, name, ": rows padded to 8 must fit the storage");
+}
+
+uint16_t* hp(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
 float* fp(const Tensor& t) { return t.data_ptr<float>(); }
 const float* cfp(const Tensor& t) { return t.data_ptr<float>(); }
 template <typename T>
@@ -60,9 +75,25 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
           const optional<Tensor>& oh_off, bool oh_trans, const optional<Tensor>& bn_part, int64_t bn_rpg,
           const optional<Tensor>& tile_cnt) {
-  check_f32_2d(a, "a");
-  check_f32_2d(b, "b");
-  check_f32_2d(c, "c");
+  const bool bin = a.scalar_type() == at::kBFloat16;
+  const bool cbf = c.scalar_type() == at::kBFloat16;
+  if (bin) {
+    TORCH_CHECK(!ta && tb && !f32, "gemm: bf16 operands need C = A B^T on the bf16 MFMA path");
+    check_bf16_operand(a, "a");
+    check_bf16_operand(b, "b");
+  } else {
+    check_f32_2d(a, "a");
+    check_f32_2d(b, "b");
+  }
+  if (cbf) {
+    TORCH_CHECK(c.is_cuda() && c.dim() == 2 && (c.size(1) <= 1 || c.stride(1) == 1), "gemm: c");
+    TORCH_CHECK(beta == 0.0 && (epi == fedtgan::EPI_NONE || epi == fedtgan::EPI_RELU || epi == fedtgan::EPI_BN_EVAL_RELU) &&
+                    !(head_a.has_value() && head_a->defined()) && !(bn_part.has_value() && bn_part->defined()) &&
+                    group == 0,
+                "gemm: a bf16 output takes beta = 0 and the NONE / RELU / BN_EVAL_RELU epilogues, unpaired");
+  } else {
+    check_f32_2d(c, "c");
+  }
   const int64_t M = ta ? a.size(1) : a.size(0);
   const int64_t K = ta ? a.size(0) : a.size(1);
   const int64_t Kb = tb ? b.size(1) : b.size(0);
@@ -71,9 +102,16 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: c is ", c.sizes(), " expected [", M, ", ", N, "]");
   if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm: bias");
   fedtgan::GemmArgs g{};
-  g.a = cfp(a);
-  g.b = cfp(b);
-  g.c = fp(c);
+  if (bin) {
+    g.a16 = hp(a);
+    g.b16 = hp(b);
+    g.bin = 1;
+  } else {
+    g.a = cfp(a);
+    g.b = cfp(b);
+  }
+  if (cbf) g.c16 = hp(c);
+  else g.c = fp(c);
   g.bias = optp<float>(bias);
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.lda = ld_of(a); g.ldb = ld_of(b); g.ldc = ld_of(c);
@@ -106,7 +144,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   g.rng_stream = (uint32_t)stream;
   g.f32 = f32 ? 1 : 0;
   TORCH_CHECK(tile == 32 || tile == 64 || tile == 128, "gemm: tile must be 32, 64 or 128");
-  g.vec = (vec_ok(a) && vec_ok(b)) ? 1 : 0;
+  g.vec = bin ? 1 : ((vec_ok(a) && vec_ok(b)) ? 1 : 0);
   g.tile = (int)tile;
   if (head_a.has_value() && head_a->defined()) {
     TORCH_CHECK(epi == fedtgan::EPI_LRELU_DROPOUT, "gemm: the head seed needs the LeakyReLU+dropout epilogue");
@@ -185,18 +223,29 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
             const optional<Tensor>& col, const optional<Tensor>& opt, const optional<Tensor>& step_bump,
             const optional<Tensor>& step_bump2, const optional<Tensor>& metrics, bool zero_metrics, int64_t seed,
             const Tensor& rng_ctr, int64_t stream) {
-  check_f32_2d(h, "h");
   fedtgan::SampleArgs a{};
+  const bool h16 = h.scalar_type() == at::kBFloat16;
   a.B = (int)h.size(0);
   a.E = (int)E;
-  a.C = (int)(h.size(1) - cc);
   a.Dd = (int)Dd;
   a.n_col = (int)cond_w.numel();
   a.maxw = cdf.dim() == 2 ? (int)cdf.size(1) : 0;
-  TORCH_CHECK(zc + E <= h.size(1) && cc <= h.size(1), "sample: column ranges");
   TORCH_CHECK(cond_off.scalar_type() == at::kInt && cond_w.scalar_type() == at::kInt, "sample: int32 tables");
   TORCH_CHECK(cdf.is_contiguous() && cdf.scalar_type() == at::kFloat, "sample: cdf");
-  a.h = fp(h); a.ldh = ld_of(h); a.zc = (int)zc; a.cc = (int)cc;
+  if (h16) {
+    // generation into a bf16 activation buffer: only z is written (the condition goes to col / opt)
+    TORCH_CHECK(h.is_cuda() && h.dim() == 2 && (h.size(1) <= 1 || h.stride(1) == 1), "sample: h");
+    TORCH_CHECK(zc >= 0 && zc + E <= h.size(1), "sample: z columns");
+    TORCH_CHECK(!(xf.has_value() && xf->defined()) && !(xr.has_value() && xr->defined()),
+                "sample: a bf16 h takes no D-input blocks");
+    TORCH_CHECK(a.n_col == 0 || (col.has_value() && opt.has_value()), "sample: a bf16 h needs col / opt outputs");
+    a.h16 = hp(h); a.ldh16 = ld_of(h); a.zc16 = (int)zc;
+  } else {
+    check_f32_2d(h, "h");
+    a.C = (int)(h.size(1) - cc);
+    TORCH_CHECK(zc + E <= h.size(1) && cc <= h.size(1), "sample: column ranges");
+    a.h = fp(h); a.ldh = ld_of(h); a.zc = (int)zc; a.cc = (int)cc;
+  }
   a.ldx = 0;
   if (xf.has_value() && xf->defined()) {
     check_f32_2d(*xf, "xf");
@@ -221,6 +270,10 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
   a.cdf = cfp(cdf);
   a.cond_off = cond_off.data_ptr<int>();
   a.cond_w = cond_w.data_ptr<int>();
+  for (const auto* t : {&col, &opt})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->is_cuda() && (*t)->scalar_type() == at::kInt && (*t)->is_contiguous() && (*t)->numel() >= a.B,
+                  "sample: col / opt must be int32 with one entry per row");
   a.col = optp<int>(col);
   a.opt = optp<int>(opt);
   a.step_bump = optp<float>(step_bump);
@@ -505,7 +558,7 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
 void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, const Tensor& start,
                    const Tensor& width, const Tensor& cont, const Tensor& code_off, const Tensor& codes,
                    const Tensor& mu, const Tensor& sd, int64_t seed, const Tensor& rng_ctr, int64_t stream,
-                   const optional<Tensor>& ecol) {
+                   const optional<Tensor>& ecol, const optional<Tensor>& quads) {
   check_f32_2d(logits, "logits");
   TORCH_CHECK(out.scalar_type() == at::kDouble && out.is_contiguous() && out.dim() == 2, "decode: out f64");
   TORCH_CHECK(out.size(0) == logits.size(0) && out.size(1) == kind.numel(), "decode: shapes");
@@ -536,6 +589,14 @@ void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, 
                 "decode: ecol must be int32 [data_dim]");
     // the row kernel keeps one 8-byte maximum per output column and wave in LDS
     if (a.n_cols * 4 * 8 <= 64 * 1024) a.ecol = ecol->data_ptr<int>();
+  }
+  if (quads.has_value() && quads->defined()) {
+    TORCH_CHECK(quads->scalar_type() == at::kInt && quads->is_contiguous() && quads->dim() == 2 && quads->size(1) == 2,
+                "decode: quads must be int32 [n, 2]");
+    TORCH_CHECK(logits.size(1) < 65536, "decode: quads address positions below 65536");
+    // every entry: a column, 1-4 logits inside the row and inside that column's span (host-built)
+    a.quads = quads->data_ptr<int>();
+    a.n_quads = (int)quads->size(0);
   }
   fedtgan::launch_sample_decode(a, cur_stream());
 }
@@ -699,7 +760,7 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     return prev;
   }
   if (key == "decode_rows") {
-    TORCH_CHECK(value == 0 || value == 1, "decode_rows: 0 or 1");
+    TORCH_CHECK(value >= 0 && value <= 2, "decode_rows: 0 per cell, 1 per row, 2 per row over Philox quads");
     const int prev = fedtgan::g_decode_rows;
     fedtgan::g_decode_rows = (int)value;
     return prev;
@@ -796,7 +857,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def(
       "sample_decode(Tensor logits, Tensor(a!) out, Tensor kind, Tensor start, Tensor width, Tensor cont, "
       "Tensor code_off, Tensor codes, Tensor mu, Tensor sd, int seed, Tensor rng_ctr, int stream, "
-      "Tensor? ecol=None) -> ()");
+      "Tensor? ecol=None, Tensor? quads=None) -> ()");
   m.def("rng_bump(Tensor(a!) ctr) -> ()");
   m.def(
       "vgm_estep(Tensor x, Tensor n_rows, Tensor consts, Tensor means, Tensor prec, Tensor(a!) partial, "

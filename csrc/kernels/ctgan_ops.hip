@@ -130,8 +130,29 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     if (real) cv_per = per.cdf[min(lane, a.maxw - 1)];
   }
   // (2) the noise while the CDF chunks are in flight
-  float* hrow = a.h + (size_t)b * a.ldh;
   RngArgs rz{a.seed, a.rng_ctr, a.rng_stream + 2u};
+  if (a.h16) {
+    // bf16 generation buffer: the same draws, rounded as the GEMM's staging would round them
+    uint16_t* hrow16 = a.h16 + (size_t)b * a.ldh16 + a.zc16;
+    for (int i = lane; i < (a.E + 1) / 2; i += 64) {
+      const uint4 r = rng4(rz, step, (uint64_t)b * a.E + i);
+      const float2 z = box_muller(r.x, r.y);
+      if (2 * i + 1 < a.E && ((a.zc16 | a.ldh16) & 1) == 0) {
+        *reinterpret_cast<uint32_t*>(hrow16 + 2 * i) = pack_bf16x2(z.x, z.y);
+      } else {
+        hrow16[2 * i] = f2bf(z.x);
+        if (2 * i + 1 < a.E) hrow16[2 * i + 1] = f2bf(z.y);
+      }
+    }
+    int col = 0, opt = 0;
+    if (a.n_col > 0) {
+      col = own.col;
+      opt = cond_draw_finish(a, own, cv_own, lane);
+    }
+    if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
+    return;
+  }
+  float* hrow = a.h + (size_t)b * a.ldh;
   for (int i = lane; i < (a.E + 1) / 2; i += 64) {
     const uint4 r = rng4(rz, step, (uint64_t)b * a.E + i);
     const float2 z = box_muller(r.x, r.y);
@@ -1826,11 +1847,82 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void sample_decode_row_kernel(Decod
   }
 }
 
-int g_decode_rows = 1;   // generation decode: one wave per row (1) or one thread per cell (0)
+// One wave per row over Philox QUADS: a lane takes a run of up to 4 logits of one column that share
+// one Philox word (the same counter and components as the kernels above), adds the 4 Gumbel draws of
+// that ONE Philox call, keeps the run's first maximum in registers and folds it into the column's
+// LDS maximum with one ds_max_u64 -- a quarter of the Philox calls and LDS atomics of the
+// element-per-lane kernel.  Same noise, same ties: bit-identical output.
+__global__ __launch_bounds__(DEC_WAVES * 64) void sample_decode_quad_kernel(DecodeArgs a) {
+  extern __shared__ unsigned long long dec_best[];   // [DEC_WAVES][n_cols]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * DEC_WAVES + wv;
+  if (r >= a.rows) return;   // (wave-uniform; only wave-level LDS syncs below)
+  unsigned long long* best = dec_best + (size_t)wv * a.n_cols;
+  for (int j = lane; j < a.n_cols; j += 64) best[j] = 0ull;
+  wave_lds_sync();
+  const float* x = a.logits + (size_t)r * a.ldl;
+  const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
+  RngArgs rng{a.seed, a.rng_ctr, a.rng_stream};
+  const uint64_t rbase = (uint64_t)r << 20;
+  for (int q = lane; q < a.n_quads; q += 64) {
+    const int q0 = a.quads[2 * q], q1 = a.quads[2 * q + 1];
+    const int j = q0 & 0xFFFFFF, cnt = q0 >> 24;
+    const int i0 = q1 >> 16, p0 = q1 & 0xFFFF;
+#if FT_CHECKED
+    FT_CHECK(&g_check_ops, j < a.n_cols && cnt >= 1 && cnt <= 4 && p0 + cnt <= a.dim, CHK_DECODE_MODE);
+    if (!(j < a.n_cols && cnt >= 1 && cnt <= 4 && p0 + cnt <= a.dim)) continue;
+#endif
+    float xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = x[p0 + min(u, cnt - 1)];
+    const uint4 rw = rng4(rng, step, rbase + (uint64_t)p0);   // counter = span offset + (i & ~3)
+    const uint32_t uu[4] = {rw.x, rw.y, rw.z, rw.w};
+    float bv = xv[0] + gumbel(uu[0]);
+    int bi = 0;
+#pragma unroll
+    for (int u = 1; u < 4; ++u) {
+      const float v = xv[u] + gumbel(uu[u]);
+      if (u < cnt && v > bv) { bv = v; bi = u; }
+    }
+    const uint32_t i = (uint32_t)(i0 + bi);
+    atomicMax(&best[j], ((unsigned long long)f2ord(bv) << 32) | (unsigned long long)(0xFFFFFFFFu - i));
+  }
+  wave_lds_sync();
+  for (int j = lane; j < a.n_cols; j += 64) {
+    const unsigned long long k = best[j];
+    const int bi = k ? (int)(0xFFFFFFFFu - (uint32_t)(k & 0xFFFFFFFFull)) : 0;
+    double val;
+    if (a.kind[j] == 0) {
+      double al = (double)tanhf(x[a.start[j]]);
+      al = al < -1.0 ? -1.0 : (al > 1.0 ? 1.0 : al);
+      const int c = a.cont[j];
+#if FT_CHECKED
+      FT_CHECK(&g_check_ops, bi >= 0 && bi < a.K, CHK_DECODE_MODE);
+#endif
+      val = al * 4.0 * a.sd[(size_t)c * a.K + bi] + a.mu[(size_t)c * a.K + bi];
+    } else {
+#if FT_CHECKED
+      FT_CHECK(&g_check_ops, a.code_off[j] + bi >= 0 && a.code_off[j] + bi < a.n_codes, CHK_DECODE_CODE);
+#endif
+      val = a.codes[a.code_off[j] + bi];
+    }
+    a.out[(size_t)r * a.n_cols + j] = val;
+  }
+}
+
+// generation decode: 2 = one wave per row over Philox quads, 1 = one wave per row, element per lane,
+// 0 = one thread per (row, column)
+int g_decode_rows = 2;
 
 void launch_sample_decode(const DecodeArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.rows * a.n_cols;
   if (n == 0) return;
+  if (g_decode_rows == 2 && a.quads && a.ecol) {
+    const size_t lds = (size_t)DEC_WAVES * a.n_cols * sizeof(unsigned long long);
+    hipLaunchKernelGGL(sample_decode_quad_kernel, dim3((unsigned)((a.rows + DEC_WAVES - 1) / DEC_WAVES)),
+                       dim3(DEC_WAVES * 64), lds, stream, a);
+    return;
+  }
   if (g_decode_rows && a.ecol) {
     const size_t lds = (size_t)DEC_WAVES * a.n_cols * sizeof(unsigned long long);
     hipLaunchKernelGGL(sample_decode_row_kernel, dim3((unsigned)((a.rows + DEC_WAVES - 1) / DEC_WAVES)),

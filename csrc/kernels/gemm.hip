@@ -80,6 +80,38 @@ __device__ __forceinline__ float onehot_term(const GemmArgs& g, int m, int n) {
   return g.oh_trans ? g.oh_w[(size_t)idx * g.oh_ld + n] : g.oh_w[(size_t)n * g.oh_ld + idx];
 }
 
+// Eval BatchNorm parameters of one output column, loaded once per column a thread owns (a store
+// to C between per-element loads would force the compiler to reload them: it cannot prove that C
+// and the BN vectors do not alias -- measured: the 40k-row G0 epilogue 20 -> 54 us)
+struct ColEpi {
+  float rm, r, gamma, beta;
+};
+
+__device__ __forceinline__ ColEpi col_epi(const GemmArgs& g, int n) {
+  ColEpi c{0.f, 0.f, 0.f, 0.f};
+  if (g.epi == EPI_BN_EVAL_RELU) {
+    c.rm = g.bn_rm[n];
+    c.r = rsqrtf(g.bn_rv[n] + g.bn_eps);
+    c.gamma = g.bn_gamma[n];
+    c.beta = g.bn_beta[n];
+  }
+  return c;
+}
+
+// the one BN-eval expression every path uses (bit-identical results across epilogues)
+__device__ __forceinline__ float bn_eval_relu(float v, const ColEpi& c) {
+  const float y = (v - c.rm) * c.r * c.gamma + c.beta;
+  return y > 0.f ? y : 0.f;
+}
+
+__device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx);
+
+// apply_epi with the column's BN parameters already in registers
+__device__ __forceinline__ float apply_epi_c(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx,
+                                             const ColEpi& c) {
+  return g.epi == EPI_BN_EVAL_RELU ? bn_eval_relu(v, c) : apply_epi(g, v, m, n, step, idx);
+}
+
 __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, int n, uint64_t step, uint64_t idx) {
   const int epi = g.epi;
   if (epi == EPI_LRELU_DROPOUT) {
@@ -96,8 +128,7 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
   } else if (epi == EPI_RELU) {
     return v > 0.f ? v : 0.f;
   } else if (epi == EPI_BN_EVAL_RELU) {
-    const float y = (v - g.bn_rm[n]) * rsqrtf(g.bn_rv[n] + g.bn_eps) * g.bn_gamma[n] + g.bn_beta[n];
-    return y > 0.f ? y : 0.f;
+    return bn_eval_relu(v, col_epi(g, n));
   }
   return v;
 }
@@ -236,6 +267,53 @@ struct Chunk {
   }
 };
 
+// A chunk of a bf16 operand (GemmArgs::bin): R rows x KC k-values, k contiguous in memory, 8 values
+// per 16-B load (half the loads and registers of an fp32 chunk); staged into the same [row][KC + 8]
+// LDS image without conversion.  The host guarantees a 16-B aligned base, ld % 8 == 0 and storage for
+// every row's extent rounded up to 8, so the clamped float4-style addressing of Chunk carries over.
+template <int KC, int R>
+struct ChunkBF {
+  static constexpr int QPR = KC / 8;             // 16-B loads per row
+  static constexpr int NV = R * KC / (8 * NT);   // loads per thread
+  u32x4 v[NV];
+  int r0, rmax, k0, kmax;
+
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ p, int ld, int r0_, int rmax_, int k0_, int kmax_) {
+    r0 = r0_;
+    rmax = rmax_;
+    k0 = k0_;
+    kmax = kmax_;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int rr = r0 + t / QPR + (NT / QPR) * i;
+      const int k = min(k0 + 8 * (t % QPR), ((kmax + 7) & ~7) - 8);
+      v[i] = *reinterpret_cast<const u32x4*>(p + (size_t)min(rr, rmax - 1) * ld + k);
+    }
+  }
+
+  __device__ __forceinline__ void store(uint16_t* s) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int r = t / QPR + (NT / QPR) * i, q = t % QPR;
+      const int kk = k0 + 8 * q;
+      u32x4 x = v[i];
+      if (r0 + r >= rmax) {
+        x = u32x4{0u, 0u, 0u, 0u};
+      } else if (kk + 8 > kmax) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned lo = kk + 2 * e < kmax ? 0x0000FFFFu : 0u;
+          const unsigned hi = kk + 2 * e + 1 < kmax ? 0xFFFF0000u : 0u;
+          x[e] &= lo | hi;
+        }
+      }
+      *reinterpret_cast<u32x4*>(&s[r * (KC + 8) + 8 * q]) = x;
+    }
+  }
+};
+
 // Per-tile BatchNorm partials (GemmArgs::bn_part) of the stored values v = acc + bias: for each column
 // and batch, the tile's row count, mean and sum of squared deviations (two passes over the
 // accumulators: the mean, then the centred squares -- no cancellation), reduced over the 4 lane
@@ -343,7 +421,7 @@ __device__ __forceinline__ void bn_tile_partials(const GemmArgs& g, const f32x4 
   }
 }
 
-template <bool F32, int TM, int TN>
+template <bool F32, int TM, int TN, bool BIN = false>
 struct Cfg {
   // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
   // with 135 KB of LDS raised the per-workgroup rate of long-K GEMMs by 1.36x but cost more on
@@ -355,7 +433,8 @@ struct Cfg {
   static constexpr int ESZ = F32 ? 4 : 2;
   static constexpr int STAGE = (TM + TN) * LD * ESZ;          // bytes per stage (A image + B image)
   // bursts in flight: 2 where the second register slot fits next to the fragments (bf16 path)
-  static constexpr int DEPTH = (!F32 && TM <= FEDTGAN_GEMM_DEPTH2_MAX_TM) ? 2 : 1;
+  // (bf16 operands: half the registers per burst, so two bursts fit at every tile size)
+  static constexpr int DEPTH = (!F32 && (BIN || TM <= FEDTGAN_GEMM_DEPTH2_MAX_TM)) ? 2 : 1;
 };
 
 // In-launch split-K reduction (GemmArgs::tile_cnt, 32/64 tiles, N % 4 == 0): the hand-off of
@@ -445,10 +524,11 @@ __device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (
 // 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
 // The body of one output tile; (bx, by, bz) index the tile within a (gx, gy, gz) tile grid.  Called by
 // gemm_kernel (one GEMM per launch) and gemm_pair_kernel (two independent GEMMs in one launch).
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int gx, int gy, int gz,
                                           unsigned char* __restrict__ smem) {
-  using C = Cfg<F32, TM, TN>;
+  static_assert(!BIN || (!TA && TB && !F32), "bf16 operands: C = A B^T, both k-contiguous, bf16 MFMA");
+  using C = Cfg<F32, TM, TN, BIN>;
   constexpr int KC = C::KC;
   constexpr int MI = TM / 32, NJ = TN / 32, WM = TM / 2, WN = TN / 2;
 
@@ -481,22 +561,34 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   // A(m,k): TA ? a[k*lda+m] : a[m*lda+k]   -> staged [m][k]; k-contiguous in memory iff !TA
   // B(k,n): TB ? b[n*ldb+k] : b[k*ldb+n]   -> staged [n][k]; k-contiguous in memory iff TB
   // one register slot: burst i+1's loads are issued before burst i is multiplied out of LDS
-  Chunk<KC, !TA, TM> ca;
-  Chunk<KC, TB, TN> cb;
-  auto issue = [&](int k0) {
-    ca.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
-    cb.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
-  };
-  auto stage = [&](int st) {
-    unsigned char* base = smem + st * C::STAGE;
-    if constexpr (F32) {
-      ca.store_f32(reinterpret_cast<float*>(base));
-      cb.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
+  using CA = std::conditional_t<BIN, ChunkBF<KC, TM>, Chunk<KC, !TA, TM>>;
+  using CB = std::conditional_t<BIN, ChunkBF<KC, TN>, Chunk<KC, TB, TN>>;
+  auto load_ab = [&](CA& a_, CB& b_, int k0) {
+    if constexpr (BIN) {
+      a_.load(g.a16, g.lda, m0, g.M, k0, ke);
+      b_.load(g.b16, g.ldb, n0, g.N, k0, ke);
     } else {
-      ca.store_bf16(reinterpret_cast<uint16_t*>(base));
-      cb.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
+      a_.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
+      b_.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
     }
   };
+  auto stage_ab = [&](const CA& a_, const CB& b_, int st) {
+    unsigned char* base = smem + st * C::STAGE;
+    if constexpr (F32) {
+      a_.store_f32(reinterpret_cast<float*>(base));
+      b_.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
+    } else if constexpr (BIN) {
+      a_.store(reinterpret_cast<uint16_t*>(base));
+      b_.store(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
+    } else {
+      a_.store_bf16(reinterpret_cast<uint16_t*>(base));
+      b_.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
+    }
+  };
+  CA ca;
+  CB cb;
+  auto issue = [&](int k0) { load_ab(ca, cb, k0); };
+  auto stage = [&](int st) { stage_ab(ca, cb, st); };
   auto compute = [&](int st, int kvalid) {
     if constexpr (F32) {
       const float* A = reinterpret_cast<const float*>(smem + st * C::STAGE);
@@ -541,17 +633,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     // slot stays a static register set; a burst's loads are issued two bursts ahead of its use,
     // so a B-burst GEMM costs ~B/2 memory round trips instead of ~B (the compiler's counted
     // vmcnt waits only for the older slot when staging it)
-    Chunk<KC, !TA, TM> ca2;
-    Chunk<KC, TB, TN> cb2;
-    auto issue2 = [&](int k0) {
-      ca2.template load<VEC>(g.a, g.lda, m0, g.M, k0, ke);
-      cb2.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
-    };
-    auto stage2 = [&](int s) {
-      unsigned char* base = smem + s * C::STAGE;
-      ca2.store_bf16(reinterpret_cast<uint16_t*>(base));
-      cb2.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
-    };
+    CA ca2;
+    CB cb2;
+    auto issue2 = [&](int k0) { load_ab(ca2, cb2, k0); };
+    auto stage2 = [&](int s) { stage_ab(ca2, cb2, s); };
     issue(kb);
     if (kb + KC < ke) issue2(kb + KC);
     for (int k0 = kb; k0 < ke; k0 += 2 * KC) {
@@ -607,6 +692,66 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       }
   }
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  if constexpr (BIN && TM <= 64) if (g.c16) {
+    // bf16 output (host: unsplit, beta = 0, epilogue NONE / RELU / BN_EVAL_RELU): the tile goes
+    // through LDS and each thread writes 8 consecutive columns of a row as one 16-B store (128x128
+    // tiles: in their own LDS epilogue below -- this one would cost them 52 more VGPRs)
+    constexpr int LDC = TN + 1;
+    static_assert((size_t)(TM * LDC + 5 * TN) * 4 <= (TM <= 64 ? 1 : 2) * C::STAGE,
+                  "bf16 epilogue tile must fit the LDS a launch gets");
+    __syncthreads();
+    float* cs = reinterpret_cast<float*>(smem);
+    float* cp = cs + TM * LDC;     // per-column [bias | rm | rsqrt(rv + eps) | gamma | beta] of the tile
+    if (threadIdx.x < TN) {        // one load of each parameter per column, by one thread
+      const int nn = min(n0 + (int)threadIdx.x, g.N - 1);
+      const ColEpi c = col_epi(g, nn);
+      cp[threadIdx.x] = g.bias ? g.bias[nn] : 0.f;
+      cp[TN + threadIdx.x] = c.rm;
+      cp[2 * TN + threadIdx.x] = c.r;
+      cp[3 * TN + threadIdx.x] = c.gamma;
+      cp[4 * TN + threadIdx.x] = c.beta;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDC + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    // a thread's 8 columns are the same in every pass (NT is a multiple of TN / 8)
+    static_assert(NT % (TN / 8) == 0, "fixed columns per thread");
+    const int nl = 8 * (threadIdx.x % (TN / 8));
+    float colb[8];
+    ColEpi ce[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      colb[c] = cp[nl + c];
+      ce[c] = ColEpi{cp[TN + nl + c], cp[2 * TN + nl + c], cp[3 * TN + nl + c], cp[4 * TN + nl + c]};
+    }
+#pragma unroll 1
+    for (int e = threadIdx.x; e < TM * (TN / 8); e += NT) {
+      const int ml = e / (TN / 8);
+      const int m = m0 + ml, n = n0 + nl;
+      if (m >= g.M || n >= g.N) continue;
+      float y[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int nn = min(n + c, g.N - 1);
+        float v = g.alpha * cs[ml * LDC + nl + c];
+        if (g.bias) v += colb[c];
+        y[c] = apply_epi_c(g, v, m, nn, 0ull, 0ull, ce[c]);
+      }
+      uint16_t* dst = g.c16 + (size_t)m * g.ldc + n;
+      if (n + 8 <= g.N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        *reinterpret_cast<u32x4*>(dst) = u32x4{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]),
+                                               pack_bf16x2(y[4], y[5]), pack_bf16x2(y[6], y[7])};
+      } else {
+        for (int c = 0; c < 8 && n + c < g.N; ++c) dst[c] = f2bf(y[c]);
+      }
+    }
+    return;
+  }
   if constexpr (TM <= 64) {
     if (gz > 1 && g.red_inl) {
       splitk_inlaunch<TM, TN, MI, NJ>(g, acc, m0, n0, by * gx + bx, bz, gz, lane, wm, wn, smem, step);
@@ -627,9 +772,15 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * (TN + 1) + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    // each thread stays on one column (NT is a multiple of TN): its bias / BN parameters load once
+    static_assert(NT % TN == 0, "fixed column per thread");
+    const int nl = threadIdx.x % TN;
+    const int nc = min(n0 + nl, g.N - 1);
+    const float colb = g.bias ? g.bias[nc] : 0.f;
+    const ColEpi ce = col_epi(g, nc);
     __syncthreads();
     for (int e = threadIdx.x; e < TM * TN; e += NT) {
-      const int ml = e / TN, nl = e - ml * TN;
+      const int ml = e / TN;
       const int m = m0 + ml, n = n0 + nl;
       if (m >= g.M || n >= g.N) continue;
       const float v0 = cs[ml * (TN + 1) + nl];
@@ -638,12 +789,28 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         continue;
       }
       float v = g.alpha * v0;
+      if constexpr (BIN) {
+        if (g.c16) {     // bf16 output (unsplit, beta = 0): consecutive threads, consecutive columns
+          if (g.bias) v += colb;
+          g.c16[(size_t)m * g.ldc + n] = f2bf(apply_epi_c(g, v, m, n, 0ull, 0ull, ce));
+          continue;
+        }
+      }
       float* cp = g.c + (size_t)m * g.ldc + n;
       if (g.beta != 0.f) v += g.beta * (*cp);
-      if (g.bias) v += g.bias[n];
-      st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
+      if (g.bias) v += colb;
+      st_out(g.c, (size_t)m * g.ldc + n, apply_epi_c(g, v, m, n, step, (uint64_t)m * g.N + n, ce), g.wt);
     }
     return;
+  }
+  // a lane's columns depend on j only: bias and BN parameters load once per column
+  float colb[NJ];
+  ColEpi ce[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nc = min(n0 + wn * WN + j * 16 + (lane & 15), g.N - 1);
+    colb[j] = (g.bias && gz == 1) ? g.bias[nc] : 0.f;
+    ce[j] = gz == 1 ? col_epi(g, nc) : ColEpi{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -662,18 +829,33 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float v = g.alpha * v0;
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
-        if (g.bias) v += g.bias[n];
-        st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
+        if (g.bias) v += colb[j];
+        st_out(g.c, (size_t)m * g.ldc + n, apply_epi_c(g, v, m, n, step, (uint64_t)m * g.N + n, ce[j]), g.wt);
       }
   if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
 }
 
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN>
+// LDS is sized per launch (gemm_smem_bytes): a GEMM whose K-slice is one burst uses one stage
+// buffer, so a 64x64-tile launch over a short K fits 4 workgroups per CU instead of 2.
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<F32, TM, TN>::STAGE];
-  gemm_tile<TA, TB, F32, VEC, TM, TN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z, smem);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
+                                           smem);
+}
+
+// stage buffers a launch needs: two when a K-slice spans several bursts, else one -- unless the
+// epilogue stages the whole fp32 tile (128x128 tiles) and needs both
+static size_t gemm_smem_bytes(const GemmArgs& g) {
+  const int T = g.tile;
+  size_t stage;
+  if (g.f32) stage = T == 32 ? Cfg<true, 32, 32>::STAGE : (T == 128 ? Cfg<true, 128, 128>::STAGE : Cfg<true, 64, 64>::STAGE);
+  else stage = T == 32 ? Cfg<false, 32, 32>::STAGE : (T == 128 ? Cfg<false, 128, 128>::STAGE : Cfg<false, 64, 64>::STAGE);
+  const int KC = g.f32 ? Cfg<true, 64, 64>::KC / (T >= 128 ? 2 : 1) : Cfg<false, 64, 64>::KC / (T >= 128 ? 2 : 1);
+  const bool one_burst = g.kchunk <= KC;
+  return (one_burst && T <= 64) ? stage : 2 * stage;
 }
 
 // Two independent GEMMs in ONE launch (horizontal fusion): the first n1 workgroups run GEMM 1's
@@ -743,7 +925,7 @@ static dim3 gemm_prepare(GemmArgs& g) {
   const int T = g.tile == 32 ? 32 : (g.tile == 128 ? 128 : 64);   // square output tile
   g.tile = T;
   const int tm = (g.M + T - 1) / T, tn = (g.N + T - 1) / T;
-  if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr) g.splitk = 1;
+  if (g.splitk < 1 || g.K <= 0 || g.ws == nullptr || g.c16 != nullptr) g.splitk = 1;
   g.splitk = std::min(g.splitk, GEMM_MAX_SPLITS);   // the epilogue holds every slab value in registers
   int kchunk = (std::max(g.K, 1) + g.splitk - 1) / g.splitk;
   kchunk = ((kchunk + KC - 1) / KC) * KC;   // whole bursts per split
@@ -767,12 +949,19 @@ static dim3 gemm_prepare(GemmArgs& g) {
 static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
   const dim3 block(NT);
   const int T = g.tile;
+  const size_t lds = gemm_smem_bytes(g);
+  if (g.bin) {   // bf16 operands: C = A B^T only (checked on the host)
+    if (T == 32) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 32, 32, true>), grid, block, lds, stream, g);
+    else if (T == 128) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 128, 128, true>), grid, block, lds, stream, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 64, 64, true>), grid, block, lds, stream, g);
+    return;
+  }
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, 0, stream, g);       \
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT>), grid, block, 0, stream, g); \
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT>), grid, block, 0, stream, g);   \
-  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT>), grid, block, 0, stream, g);
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, lds, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT>), grid, block, lds, stream, g); \
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT>), grid, block, lds, stream, g);   \
+  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT>), grid, block, lds, stream, g);
 #define FEDTGAN_GEMM_TILES(F, V)       \
   if (T == 32) {                       \
     FEDTGAN_GEMM_LAYOUTS(F, V, 32)     \
@@ -843,7 +1032,7 @@ void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
   const dim3 d1 = gemm_prepare(g1), d2 = gemm_prepare(g2);
   const Grid3 a{(int)d1.x, (int)d1.y, (int)d1.z}, b{(int)d2.x, (int)d2.y, (int)d2.z};
   bool fused = false;
-  if (!g1.f32 && !g2.f32 && g_gemm_pairs) {
+  if (!g1.f32 && !g2.f32 && !g1.bin && !g2.bin && !g1.c16 && !g2.c16 && g_gemm_pairs) {
     if (g1.vec && g2.vec) fused = gemm_pair_vec<true, true>(g1, a, g2, b, stream);
     else if (g1.vec) fused = gemm_pair_vec<true, false>(g1, a, g2, b, stream);
     else if (g2.vec) fused = gemm_pair_vec<false, true>(g1, a, g2, b, stream);

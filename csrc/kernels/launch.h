@@ -67,6 +67,14 @@ struct GemmArgs {
   // gemm_splitk_epilogue launch).  red_inl is set by the launcher where the shape allows it.
   unsigned* tile_cnt;
   int red_inl;
+  // bf16 storage (generation): bin = 1 -> both operands are bf16 rows (a16 [M, K] / b16 [N, K], k
+  // contiguous, 16-B aligned, ld % 8 == 0), staged into LDS without conversion; c16 (nullable) ->
+  // the epilogue writes bf16 (no split-K, no beta).  The values are the ones the fp32 path rounds
+  // to bf16 at staging, so a bf16 activation buffer gives bit-identical products.
+  const uint16_t* a16;
+  const uint16_t* b16;
+  uint16_t* c16;
+  int bin;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -82,6 +90,10 @@ struct SampleArgs {
   int B, E, C, Dd, n_col, maxw, n_rows;
   float* h;            // generator input rows: z at h[r*ldh + zc], cond at h[r*ldh + cc]
   int ldh, zc, cc;
+  // generation into a bf16 activation buffer (nullable): z as bf16 at h16[r*ldh16 + zc16]; h and
+  // the one-hot block are then not written (the GEMMs gather the condition from col / opt)
+  uint16_t* h16;
+  int ldh16, zc16;
   float* xf;           // fake block of the D input (cond copy at xf[r*ldx + Dd]); nullable
   float* xr;           // real block [data row | cond of the permuted fake row]; nullable
   int ldx;
@@ -224,6 +236,10 @@ struct DecodeArgs {
   uint32_t rng_stream;
   int dim;              // logits per row
   const int* ecol;      // [dim] element -> output column whose argmax it enters (-1: none, e.g. alpha)
+  // [n_quads][2] (nullable): every run of up to 4 logits of one column that share a Philox word:
+  // {column | count << 24, offset-in-span << 16 | position}
+  const int* quads;
+  int n_quads;
 };
 void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
 

@@ -94,6 +94,10 @@ class EngineConfig:
     onehot: bool = True
     onehot_trans: bool = False   # training: gather from per-step [C, N] copies (A/B knob; generation always does)
     dw0_tile: int = 0            # HIP: output tile of D0's weight-gradient GEMM (0 = planner's choice)
+    # HIP, bf16 precision: generation keeps its activations and weight copies in bf16 (the values the
+    # fp32 path rounds to bf16 when staging its GEMM operands, so the output is bit-identical) --
+    # half the GEMM operand bytes and no one-hot block written into the activation buffer
+    gen_bf16: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -783,7 +787,7 @@ class CTGANEngine:
         out = torch.empty(n, self.Dd, device=self.device)
         for a in range(0, n, self.cfg.gen_chunk):
             b = min(n, a + self.cfg.gen_chunk)
-            H, logits, col, opt = self._gen_buffers(b - a)
+            H, logits, col, opt = self._gen_buffers(b - a, bf16=False)
             self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
             self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt, True))
             self.ops.activate(logits, out[a:b], self.spans, self.cfg.tau, stream_id=22)
@@ -812,18 +816,65 @@ class CTGANEngine:
         return out
 
     def _gen_pass(self, n: int, out: torch.Tensor, bufs):
+        w16 = self._gen_weights16() if self.gen16 else None
         for a in range(0, n, self.cfg.gen_chunk):
             b = min(n, a + self.cfg.gen_chunk)
             H, logits, col, opt = bufs(b - a)
             self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21)
-            self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt, True))
+            if w16 is None:
+                self._g_forward(H, logits, training=False, nhat=False, cond=(col, opt, True))
+            else:
+                self._g_forward16(H, logits, w16, (col, opt))
             self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23)
+
+    @property
+    def gen16(self) -> bool:
+        """Generation in bf16 storage (EngineConfig.gen_bf16): HIP bf16 backend, one-hot generator
+        GEMMs, and 8-aligned column offsets (16-B bf16 operand rows)."""
+        return (self.cfg.gen_bf16 and self.ops.name == "hip" and not getattr(self.ops, "f32", True) and
+                self.use_onehot and all(o % 8 == 0 for o in self.off))
+
+    def _gen_h16(self, rows: int) -> torch.Tensor:
+        """bf16 generator activations [rows, ceil8(c0)]: [out_{L-1} | ... | out_0 | z] (no one-hot block)."""
+        return torch.zeros(rows, -(-self.c_cols[0] // 8) * 8, dtype=torch.bfloat16, device=self.device)
+
+    def _gen_weights16(self) -> List[torch.Tensor]:
+        """bf16 copies of the generator weights' dense columns, refreshed from the current fp32
+        weights (inside the generation graph, so every replay sees the aggregated model)."""
+        c0 = self.c_cols[0]
+        names = [f"G.{i}.W" for i in range(len(self.gdims))] + ["G.out.W"]
+        starts = list(self.off[:len(self.gdims)]) + [0]
+        if getattr(self, "_gw16", None) is None:
+            self._gw16 = [torch.zeros(self.p[nm].shape[0], -(-(c0 - a) // 8) * 8, dtype=torch.bfloat16,
+                                      device=self.device) for nm, a in zip(names, starts)]
+        for w16, nm, a in zip(self._gw16, names, starts):
+            w16[:, :c0 - a].copy_(self.p[nm][:, :c0 - a])
+        return self._gw16
+
+    def _g_forward16(self, H16, logits, w16, cond):
+        """Eval-mode generator on the bf16 buffer: each layer's GEMM reads bf16 rows and weights,
+        gathers the one-hot block from col / opt, and writes bf16 (BN-eval + ReLU epilogue); the output
+        layer writes fp32 logits."""
+        o, p = self.ops, self.p
+        c0 = self.c_cols[0]
+        col, opt = cond
+        for i, g in enumerate(self.gdims):
+            a, b_ = self.off[i], self.off[i + 1]
+            W = p[f"G.{i}.W"]
+            oh = (W[:, c0 - a:].t().contiguous(), col, opt, self._cond_off, True)
+            o.linear_bn_relu(H16[:, a:c0], w16[i], p[f"G.{i}.b"], p[f"G.{i}.gamma"], p[f"G.{i}.beta"], H16[:, b_:a],
+                             None, None, None, None, p[f"G.{i}.rm"], p[f"G.{i}.rv"], False, self.cfg.bn_momentum,
+                             self.cfg.bn_eps, onehot=oh)
+        W = p["G.out.W"]
+        oh = (W[:, c0:].t().contiguous(), col, opt, self._cond_off, True)
+        o.gemm(H16[:, :c0], w16[-1], logits, tb=True, bias=p["G.out.b"], onehot=oh)
 
     def _capture_gen(self, n: int):
         """Capture generate_decoded(n) with its own static buffers (graphs hold no tensor refs)."""
         from ..utils.devsync import CAPTURE_LOCK
         m = min(n, self.cfg.gen_chunk)
-        H, lg = _padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device)
+        H = self._gen_h16(m) if self.gen16 else _padded_rows(m, self.Hw, self.device)
+        lg = _padded_rows(m, self.Dd, self.device)
         col, opt = (torch.zeros(m, dtype=torch.int32, device=self.device) for _ in range(2))
         out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
         bufs = lambda k: (H[:k], lg[:k], col[:k], opt[:k])  # noqa: E731
@@ -840,10 +891,13 @@ class CTGANEngine:
         self._gen_graphs[n] = (g, H, lg, out, col, opt)
         return self._gen_graphs[n]
 
-    def _gen_buffers(self, n: int):
-        if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n:
+    def _gen_buffers(self, n: int, bf16: bool | None = None):
+        bf16 = self.gen16 if bf16 is None else bf16
+        if self._gen_bufs is None or self._gen_bufs[0].shape[0] < n or \
+                (self._gen_bufs[0].dtype == torch.bfloat16) != bf16:
             m = max(n, min(self.cfg.gen_chunk, n))
-            self._gen_bufs = (_padded_rows(m, self.Hw, self.device), _padded_rows(m, self.Dd, self.device),
+            H = self._gen_h16(m) if bf16 else _padded_rows(m, self.Hw, self.device)
+            self._gen_bufs = (H, _padded_rows(m, self.Dd, self.device),
                               torch.zeros(m, dtype=torch.int32, device=self.device),
                               torch.zeros(m, dtype=torch.int32, device=self.device))
         H, lg, col, opt = self._gen_bufs

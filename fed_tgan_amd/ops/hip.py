@@ -183,6 +183,8 @@ class HipOps:
         tile_p, sk = _plan(M, N, K, kc)
         tile = self.tile_override or tile or tile_p
         sk = _effective_splits(K, self.split_override or sk, kc)
+        if c.dtype == torch.bfloat16:
+            sk = 1          # a bf16 output is written by the GEMM's own epilogue
         ws = cnt = None
         if sk > 1:
             ws = self._workspace(sk * M * N, held=group == 1)
@@ -364,9 +366,30 @@ class HipOps:
             self._dec[key] = e
         return e
 
+    def _decode_quads(self, tabs, dim: int):
+        """[n, 2] int32: every run of up to 4 logits of one column that share a Philox word
+        ({column | count << 24, offset-in-span << 16 | position}), the quad decode kernel's work list."""
+        key = ("quads", id(tabs), int(dim))
+        q = self._dec.get(key)
+        if q is None:
+            ent = []
+            for j, (kk, s, w, _, _) in enumerate(tabs["cols"]):
+                off = s + 1 if kk == 0 else s
+                for i0 in range(0, w, 4):
+                    cnt = min(4, w - i0)
+                    if off + i0 + cnt > dim or j >= (1 << 24):
+                        raise ValueError("decode tables do not fit the logits")
+                    ent.append((j | (cnt << 24), (i0 << 16) | (off + i0)))
+            q = torch.tensor(ent if ent else [(0, 0)], dtype=torch.int32, device=self.device).view(-1, 2)
+            if not ent:
+                q = q[:0]
+            self._dec[key] = q
+        return q
+
     def sample_decode(self, logits, out, tabs, stream_id=0):
         kind, start, width, cont, code_off, codes, mu, sd = self._decode_tables(tabs)
         self.L.sample_decode(logits, out, kind, start, width, cont, code_off, codes, mu, sd, self.seed, self.ctr,
-                             int(stream_id) * 16, self._decode_ecol(tabs, logits.shape[1]))
+                             int(stream_id) * 16, self._decode_ecol(tabs, logits.shape[1]),
+                             self._decode_quads(tabs, logits.shape[1]))
         self.L.rng_bump(self.ctr)
         return out

@@ -199,3 +199,32 @@ def test_onehot_generator_matches_dense():
     assert torch.allclose(la, lb, atol=1e-4, rtol=1e-4)
     assert torch.allclose(ma, mb, atol=1e-5, rtol=1e-5) and torch.allclose(va, vb, atol=1e-5, rtol=1e-5)
     assert torch.allclose(ea, eb, atol=1e-3)     # same Philox draws: identical up to GEMM rounding
+
+
+@pytest.mark.parametrize("n", [40000, 3000, 77])
+def test_bf16_generation_is_bit_identical(n):
+    """EngineConfig.gen_bf16: generation on a bf16 activation buffer with bf16 weight copies gives
+    exactly the fp32-storage path's table (the GEMMs round their staged operands to bf16 either way),
+    graph-replayed and eager, including after a weight update (the copies refresh every pass)."""
+    from fed_tgan_amd.models.samplers import CondTables
+    eng, tr = _engine()
+    _, _, _, _, _, _, _, X = small_table()
+    eng.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+    ctr0 = eng.ops.ctr.clone()
+
+    def run(bf16, graph):
+        eng.cfg.gen_bf16 = bf16
+        eng._gen_graphs, eng._gen_bufs = {}, None
+        eng.ops.ctr.copy_(ctr0)
+        out = [eng.generate_decoded(n, use_graph=graph) for _ in range(2)]
+        assert eng.gen16 == bf16
+        return out
+
+    for graph in (True, False):
+        ref, got = run(False, graph), run(True, graph)
+        for r, g in zip(ref, got):
+            assert torch.equal(r, g)
+    eng.train_steps(2)       # new weights: a replayed bf16 graph must pick them up
+    ref, got = run(False, True), run(True, True)
+    assert torch.equal(ref[0], got[0])
+    eng.cfg.gen_bf16 = True

@@ -695,8 +695,9 @@ def test_adam_folded_dot_over_own_parameters_reads_pre_update_values(hip):
 
 
 def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
-    """One wave per row (LDS 64-bit max per column) draws the same Gumbel noise per logit as the
-    one-thread-per-cell decode, so both give the same table bit for bit."""
+    """One wave per row (LDS 64-bit max per column; element per lane, or one Philox quad per lane)
+    draws the same Gumbel noise per logit as the one-thread-per-cell decode, so all three give the
+    same table bit for bit."""
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from fed_tgan_amd.models.samplers import CondTables
     tr, X, spans, cond = _spans()
@@ -706,7 +707,7 @@ def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
     logits = mat(rows, X.shape[1], seed=120) * 3
     logits[:7] = 0.0                      # flat spans: the choice is the Gumbel noise alone
     res = []
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         out = torch.zeros(rows, len(tr.meta), dtype=torch.float64, device=DEV)
         ctr0 = eng.ops.ctr.clone()
         prev = torch.ops.fedtgan.set_tuning("decode_rows", mode)
@@ -714,10 +715,10 @@ def test_sample_decode_row_kernel_matches_per_cell_kernel(hip):
             eng.ops.sample_decode(logits, out, eng.gen_tables)
         finally:
             torch.ops.fedtgan.set_tuning("decode_rows", prev)
-        eng.ops.ctr.copy_(ctr0)           # same counter for both kernels
+        eng.ops.ctr.copy_(ctr0)           # same counter for every kernel
         torch.cuda.synchronize()
         res.append(out)
-    assert torch.equal(res[0], res[1])
+    assert torch.equal(res[0], res[1]) and torch.equal(res[0], res[2])
 
 
 @pytest.mark.parametrize("trans", [False, True])

@@ -124,7 +124,7 @@ def gen_only(eng, tr, X, dev):
     # decode kernel alone on one 40000-row chunk: one thread per cell vs one wave per row
     logits = torch.randn(40000, X.shape[1], device=dev) * 3
     out = torch.zeros(40000, len(tr.meta), dtype=torch.float64, device=dev)
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         prev = torch.ops.fedtgan.set_tuning("decode_rows", mode)
         try:
             us = per_call(lambda: eng.ops.sample_decode(logits, out, eng.gen_tables), dev, n=20, reps=10)
