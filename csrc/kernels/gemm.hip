@@ -803,15 +803,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
     return;
   }
-  // a lane's columns depend on j only: bias and BN parameters load once per column
-  float colb[NJ];
-  ColEpi ce[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int nc = min(n0 + wn * WN + j * 16 + (lane & 15), g.N - 1);
-    colb[j] = (g.bias && gz == 1) ? g.bias[nc] : 0.f;
-    ce[j] = gz == 1 ? col_epi(g, nc) : ColEpi{0.f, 0.f, 0.f, 0.f};
-  }
+  // (the training GEMMs' register epilogue keeps per-element bias loads: hoisting them per column,
+  // as the LDS epilogues do, measured 1 us slower per step -- profiles/README.md)
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -829,8 +822,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float v = g.alpha * v0;
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
-        if (g.bias) v += colb[j];
-        st_out(g.c, (size_t)m * g.ldc + n, apply_epi_c(g, v, m, n, step, (uint64_t)m * g.N + n, ce[j]), g.wt);
+        if (g.bias) v += g.bias[n];
+        st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
   if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
 }

@@ -17,6 +17,8 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # FEDTGAN_CHECKED=1: the device bounds-checked build (csrc/build.py --checked)
 CHECKED = os.environ.get("FEDTGAN_CHECKED", "0") not in ("", "0")
 LIB_PATH = os.path.join(PKG_DIR, "_C_checked.so" if CHECKED else "_C.so")
+# FEDTGAN_LIB=<path>: load another build of the same ops (A/B of kernel revisions on one box)
+LIB_PATH = os.environ.get("FEDTGAN_LIB") or LIB_PATH
 
 CHECK_NAMES = {0: "sampler CSR pick outside the row lists", 1: "sampler data row outside the training matrix",
                2: "sampler condition outside the span tables", 3: "decode code index outside the code table",
