@@ -144,6 +144,17 @@ __device__ __forceinline__ float apply_epi(const GemmArgs& g, float v, int m, in
 // instruction than with dword loads); otherwise every element is a clamped dword load.
 // Out-of-range elements are zeroed when the burst is staged into LDS, so nothing waits on a
 // burst's loads before its turn comes (PIPE bursts stay in flight).
+// bf16 LDS images staged from COLUMN-major operands (rows contiguous in memory) are stored with the
+// 16-B k-chunks of a row XOR-permuted by lds_swz(row): the staging writes of 16 lanes then hit 16
+// distinct banks instead of 4 (a row is 68 words, 16 words mod 64, so four consecutive row-quads
+// alias), and the MFMA fragment reads stay conflict-free (rocprofv3 SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE was 55-75 % on these GEMMs; profiles/pmc_step_r2.txt).  Row-major images are
+// stored unpermuted.
+template <int KC>
+__device__ __forceinline__ int lds_swz(int row) {
+  return (3 * (row >> 4)) & (KC / 8 - 1);
+}
+
 template <int KC, bool ROWMAJ, int R>
 struct Chunk {
   static constexpr int NV = R * KC / (4 * NT);   // float4 per thread
@@ -236,9 +247,12 @@ struct Chunk {
       for (int i = 0; i < NV / 2; ++i) {
         const int rq = t % RQ, kp = t / RQ + (NT / RQ) * i;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          *reinterpret_cast<uint32_t*>(&s[(4 * rq + e) * (KC + 8) + 2 * kp]) =
+        for (int e = 0; e < 4; ++e) {
+          const int row = 4 * rq + e;
+          const int pk = (((2 * kp) >> 3) ^ lds_swz<KC>(row)) * 8 + ((2 * kp) & 7);   // swizzled k position
+          *reinterpret_cast<uint32_t*>(&s[row * (KC + 8) + pk]) =
               pack_bf16x2(ok_cm(i, 0, e) ? v[2 * i][e] : 0.f, ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f);
+        }
       }
     }
   }
@@ -612,12 +626,19 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       const int nsteps = (kvalid + 31) / 32;
       for (int s = 0; s < nsteps; ++s) {
         bf16x8 af[MI], bfr[NJ];
+        const int ck = 4 * s + (lane >> 4);   // 16-B k-chunk of this lane's fragment
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(&A[(wm * WM + i * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
+        for (int i = 0; i < MI; ++i) {
+          const int row = wm * WM + i * 16 + (lane & 15);
+          const int pc = TA ? (ck ^ lds_swz<KC>(row)) : ck;     // A image staged column-major iff TA
+          af[i] = *reinterpret_cast<const bf16x8*>(&A[row * C::LD + 8 * pc]);
+        }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(&B[(wn * WN + j * 16 + (lane & 15)) * C::LD + 32 * s + 8 * (lane >> 4)]);
+        for (int j = 0; j < NJ; ++j) {
+          const int row = wn * WN + j * 16 + (lane & 15);
+          const int pc = TB ? ck : (ck ^ lds_swz<KC>(row));     // B image staged column-major iff !TB
+          bfr[j] = *reinterpret_cast<const bf16x8*>(&B[row * C::LD + 8 * pc]);
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
