@@ -11,6 +11,7 @@
 // Rows are formatted in parallel blocks by worker threads and written with one fwrite each.
 #include "csv_writer.h"
 
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -23,107 +24,143 @@
 namespace fedtgan {
 namespace {
 
-void append_py_float(std::string& out, double x) {
-  if (std::isnan(x)) return;  // pandas writes NaN as an empty field
+// Python repr() of a double written at p (at most 26 bytes); returns the end.  NaN writes nothing
+// (pandas na_rep).  Shortest round-trip digits from std::to_chars, laid out as repr does.
+char* put_py_float(char* p, double x) {
+  if (std::isnan(x)) return p;
   if (std::isinf(x)) {
-    out += (x > 0) ? "inf" : "-inf";
-    return;
+    if (x < 0) *p++ = '-';
+    std::memcpy(p, "inf", 3);
+    return p + 3;
   }
-  char buf[64];
-  auto res = std::to_chars(buf, buf + sizeof(buf), x, std::chars_format::scientific);
-  *res.ptr = '\0';
+  char buf[40];
+  const auto res = std::to_chars(buf, buf + sizeof(buf), x, std::chars_format::scientific);
   // buf: [-]d[.ddd]e[+-]XX
-  const char* p = buf;
-  bool neg = false;
-  if (*p == '-') {
-    neg = true;
-    ++p;
+  const char* q = buf;
+  if (*q == '-') {
+    *p++ = '-';
+    ++q;
   }
-  char digits[32];
+  char digits[24];
   int nd = 0;
-  while (*p && *p != 'e') {
-    if (*p != '.') digits[nd++] = *p;
-    ++p;
-  }
+  for (; q < res.ptr && *q != 'e'; ++q)
+    if (*q != '.') digits[nd++] = *q;
   int e10 = 0;
-  if (*p == 'e') e10 = std::atoi(p + 1);
-  // strip trailing zeros of the mantissa (to_chars shortest never emits them, but keep it robust)
-  while (nd > 1 && digits[nd - 1] == '0') --nd;
-  const int decpt = e10 + 1;  // value = 0.d1d2... x 10^decpt
-  if (neg) out.push_back('-');
+  if (q < res.ptr) {   // 'e', sign, digits
+    ++q;
+    const bool eneg = *q == '-';
+    ++q;
+    for (; q < res.ptr; ++q) e10 = e10 * 10 + (*q - '0');
+    if (eneg) e10 = -e10;
+  }
+  while (nd > 1 && digits[nd - 1] == '0') --nd;   // (to_chars shortest never emits them; robustness)
+  const int decpt = e10 + 1;                      // value = 0.d1d2... x 10^decpt
   if (decpt > -4 && decpt <= 16) {
     if (decpt <= 0) {
-      out += "0.";
-      out.append((size_t)(-decpt), '0');
-      out.append(digits, (size_t)nd);
+      *p++ = '0';
+      *p++ = '.';
+      for (int i = 0; i < -decpt; ++i) *p++ = '0';
+      std::memcpy(p, digits, (size_t)nd);
+      p += nd;
     } else if (decpt < nd) {
-      out.append(digits, (size_t)decpt);
-      out.push_back('.');
-      out.append(digits + decpt, (size_t)(nd - decpt));
+      std::memcpy(p, digits, (size_t)decpt);
+      p += decpt;
+      *p++ = '.';
+      std::memcpy(p, digits + decpt, (size_t)(nd - decpt));
+      p += nd - decpt;
     } else {
-      out.append(digits, (size_t)nd);
-      out.append((size_t)(decpt - nd), '0');
-      out += ".0";
+      std::memcpy(p, digits, (size_t)nd);
+      p += nd;
+      for (int i = 0; i < decpt - nd; ++i) *p++ = '0';
+      *p++ = '.';
+      *p++ = '0';
     }
   } else {
-    out.push_back(digits[0]);
+    *p++ = digits[0];
     if (nd > 1) {
-      out.push_back('.');
-      out.append(digits + 1, (size_t)(nd - 1));
+      *p++ = '.';
+      std::memcpy(p, digits + 1, (size_t)(nd - 1));
+      p += nd - 1;
     }
     const int ex = decpt - 1;
-    out.push_back('e');
-    out.push_back(ex < 0 ? '-' : '+');
+    *p++ = 'e';
+    *p++ = ex < 0 ? '-' : '+';
     const int ax = ex < 0 ? -ex : ex;
-    if (ax < 10) out.push_back('0');
-    out += std::to_string(ax);
+    if (ax >= 100) *p++ = (char)('0' + ax / 100);
+    *p++ = (char)('0' + (ax / 10) % 10);
+    *p++ = (char)('0' + ax % 10);
   }
+  return p;
 }
 
-void append_field(std::string& out, const std::string& s) {
-  bool q = s.find_first_of(",\"\n\r") != std::string::npos;
-  if (!q) {
-    out += s;
-    return;
-  }
-  out.push_back('"');
-  for (char ch : s) {
-    if (ch == '"') out.push_back('"');
-    out.push_back(ch);
-  }
-  out.push_back('"');
+void append_py_float(std::string& out, double x) {
+  char b[40];
+  out.append(b, (size_t)(put_py_float(b, x) - b));
 }
+
+std::string quote_field(const std::string& s) {
+  if (s.find_first_of(",\"\n\r") == std::string::npos) return s;
+  std::string q = "\"";
+  for (char ch : s) {
+    if (ch == '"') q.push_back('"');
+    q.push_back(ch);
+  }
+  q.push_back('"');
+  return q;
+}
+
+void append_field(std::string& out, const std::string& s) { out += quote_field(s); }
 
 }  // namespace
 
+// Rows [r0, r1) into one string.  Every vocabulary entry is quoted once up front and each row is
+// written through a raw pointer into a buffer sized for its worst case (26 bytes per number), so the
+// hot loop does no allocation, no searching and no growing appends.
 std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, int64_t r0, int64_t r1,
                             const std::vector<int>& kinds, const std::vector<std::vector<std::string>>& vocabs) {
+  (void)rows;
+  std::vector<std::vector<std::string>> qv(vocabs.size());
+  size_t row_max = 1;
+  for (int64_t j = 0; j < cols; ++j) {
+    size_t w = 26;
+    if (kinds[(size_t)j] == 1) {
+      w = 0;
+      for (const auto& e : vocabs[(size_t)j]) {
+        qv[(size_t)j].push_back(quote_field(e));
+        w = std::max(w, qv[(size_t)j].back().size());
+      }
+    }
+    row_max += w + 1;
+  }
   std::string out;
-  out.reserve((size_t)(r1 - r0) * (size_t)cols * 12);
+  out.resize((size_t)(r1 - r0) * row_max);
+  char* p = &out[0];
   for (int64_t r = r0; r < r1; ++r) {
     const double* row = values + r * cols;
     for (int64_t j = 0; j < cols; ++j) {
-      if (j) out.push_back(',');
+      if (j) *p++ = ',';
       const double x = row[j];
       switch (kinds[(size_t)j]) {
         case 1: {  // vocabulary
-          const auto& voc = vocabs[(size_t)j];
-          int64_t k = (int64_t)x;
+          const auto& voc = qv[(size_t)j];
+          const int64_t k = (int64_t)x;
           if (k < 0 || k >= (int64_t)voc.size()) throw std::runtime_error("csv: category code out of range");
-          append_field(out, voc[(size_t)k]);
+          const std::string& f = voc[(size_t)k];
+          std::memcpy(p, f.data(), f.size());
+          p += f.size();
           break;
         }
-        case 2: {  // non-negative column, already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
-          if (x == -1.0) out.push_back(' ');
-          else append_py_float(out, x);
+        case 2:    // non-negative column, already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
+          if (x == -1.0) *p++ = ' ';
+          else p = put_py_float(p, x);
           break;
-        }
         default:
-          append_py_float(out, x);
+          p = put_py_float(p, x);
       }
     }
-    out.push_back('\n');
+    *p++ = '\n';
   }
+  out.resize((size_t)(p - out.data()));
   return out;
 }
 

@@ -33,6 +33,16 @@ def main():
         csvio.write_table(path, vals, names, kinds, vocabs, threads=th)
         dt = time.perf_counter() - t0
         print(f"threads={th:2d}: {dt * 1e3:7.2f} ms  ({os.path.getsize(path) / 1e6:.1f} MB)", flush=True)
+    # the same formatting with the bytes going nowhere: formatting cost vs file-write cost
+    for th in (16, 0):
+        t0 = time.perf_counter()
+        csvio.write_table(os.devnull, vals, names, kinds, vocabs, threads=th)
+        print(f"threads={th:2d} -> /dev/null: {(time.perf_counter() - t0) * 1e3:7.2f} ms", flush=True)
+    import numpy as np
+    t0 = time.perf_counter()
+    for _ in range(10):
+        np.array(vals, dtype=np.float64, copy=True)
+    print(f"host copy of the table: {(time.perf_counter() - t0) * 100:7.2f} ms", flush=True)
 
 
 if __name__ == "__main__":
