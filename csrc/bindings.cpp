@@ -601,6 +601,26 @@ void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, 
   fedtgan::launch_sample_decode(a, cur_stream());
 }
 
+void gen_weight_prep(const std::vector<Tensor>& w, std::vector<int64_t> kd, const std::vector<Tensor>& w16,
+                     const std::vector<Tensor>& wt) {
+  const size_t n = w.size();
+  TORCH_CHECK(n >= 1 && n <= 4 && kd.size() == n && w16.size() == n && wt.size() == n, "gen_weight_prep: 1-4 jobs");
+  fedtgan::GenWeightPrep a{};
+  a.n_jobs = (int)n;
+  for (size_t j = 0; j < n; ++j) {
+    check_f32_2d(w[j], "gen_weight_prep w");
+    const int64_t N = w[j].size(0), K = w[j].size(1);
+    TORCH_CHECK(kd[j] >= 0 && kd[j] <= K, "gen_weight_prep: kd");
+    TORCH_CHECK(w16[j].is_cuda() && w16[j].scalar_type() == at::kBFloat16 && w16[j].dim() == 2 && w16[j].size(0) == N &&
+                    w16[j].size(1) >= kd[j] && w16[j].stride(1) == 1, "gen_weight_prep: w16 [N, >= kd] bf16");
+    check_f32_2d(wt[j], "gen_weight_prep wt");
+    TORCH_CHECK(wt[j].is_contiguous() && wt[j].size(0) == K - kd[j] && wt[j].size(1) == N, "gen_weight_prep: wt [C, N]");
+    a.jobs[j] = fedtgan::GenWeightJob{cfp(w[j]), (int)N, ld_of(w[j]), (int)kd[j], (int)(K - kd[j]), hp(w16[j]),
+                                      (int)w16[j].stride(0), fp(wt[j])};
+  }
+  fedtgan::launch_gen_weight_prep(a, cur_stream());
+}
+
 void rng_bump(const Tensor& ctr) {
   TORCH_CHECK(ctr.scalar_type() == at::kLong && ctr.is_cuda(), "rng_bump: cuda int64");
   fedtgan::launch_rng_bump(reinterpret_cast<uint64_t*>(ctr.data_ptr<int64_t>()), cur_stream());
@@ -810,6 +830,7 @@ int64_t set_tuning(const std::string& key, int64_t value) {
 }  // namespace
 
 TORCH_LIBRARY(fedtgan, m) {
+  m.def("gen_weight_prep(Tensor[] w, int[] kd, Tensor(a!)[] w16, Tensor(b!)[] wt) -> ()");
   m.def(
       "gemm(Tensor a, Tensor b, Tensor(a!) c, bool ta, bool tb, float alpha, float beta, Tensor? bias, int epi, "
       "Tensor(b!)? ms, float slope, float p_drop, Tensor(d!)? ws, int splitk, int seed, Tensor? rng_ctr, int stream, "
@@ -881,6 +902,7 @@ TORCH_LIBRARY(fedtgan, m) {
 
 TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("gemm", &gemm);
+  m.impl("gen_weight_prep", &gen_weight_prep);
   m.impl("sample", &sample);
   m.impl("activate", &activate);
   m.impl("act_bwd_ce", &act_bwd_ce);

@@ -1932,6 +1932,37 @@ void launch_sample_decode(const DecodeArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(sample_decode_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
 }
 
+// Generation weight views in one launch (EngineConfig.gen_bf16): for every generator layer, the
+// dense columns [0, kd) of W as a bf16 copy (the values the GEMM's staging would round) and the
+// one-hot block [kd, kd + C) transposed to [C, N] fp32 (coalesced epilogue gathers).  Replaces six
+// small copy launches per generation pass.
+__global__ __launch_bounds__(256) void gen_weight_prep_kernel(GenWeightPrep a) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int j = 0; j < a.n_jobs; ++j) {
+    const GenWeightJob& J = a.jobs[j];
+    const int64_t nd = (int64_t)J.N * J.kd, nc = (int64_t)J.N * J.C;
+    if (e < nd) {
+      const int n = (int)(e / J.kd), k = (int)(e % J.kd);
+      J.w16[(size_t)n * J.ld16 + k] = f2bf(J.w[(size_t)n * J.ldw + k]);
+      return;
+    }
+    e -= nd;
+    if (e < nc) {
+      const int n = (int)(e / J.C), c = (int)(e % J.C);
+      J.wt[(size_t)c * J.N + n] = J.w[(size_t)n * J.ldw + J.kd + c];
+      return;
+    }
+    e -= nc;
+  }
+}
+
+void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream) {
+  int64_t total = 0;
+  for (int j = 0; j < a.n_jobs; ++j) total += (int64_t)a.jobs[j].N * (a.jobs[j].kd + a.jobs[j].C);
+  if (total == 0) return;
+  hipLaunchKernelGGL(gen_weight_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a);
+}
+
 __global__ void rng_bump_kernel(uint64_t* ctr) { ctr[0] += 1ull; }
 
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream) {

@@ -245,6 +245,19 @@ void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
 
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream);
 
+struct GenWeightJob {
+  const float* w;   // [N, ldw] fp32 weight
+  int N, ldw, kd, C;
+  uint16_t* w16;    // [N, ld16] bf16: columns [0, kd)
+  int ld16;
+  float* wt;        // [C, N] fp32: columns [kd, kd + C) transposed
+};
+struct GenWeightPrep {
+  GenWeightJob jobs[4];
+  int n_jobs;
+};
+void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream);
+
 // VGM encode (kernels/vgm.hip): one thread per (row, column) cell of the label-encoded table
 struct VgmEncodeArgs {
   const double* x;      // [n_rows, ldx] label codes / continuous values

@@ -838,36 +838,38 @@ class CTGANEngine:
         """bf16 generator activations [rows, ceil8(c0)]: [out_{L-1} | ... | out_0 | z] (no one-hot block)."""
         return torch.zeros(rows, -(-self.c_cols[0] // 8) * 8, dtype=torch.bfloat16, device=self.device)
 
-    def _gen_weights16(self) -> List[torch.Tensor]:
-        """bf16 copies of the generator weights' dense columns, refreshed from the current fp32
-        weights (inside the generation graph, so every replay sees the aggregated model)."""
+    def _gen_weights16(self):
+        """Generation views of the generator weights, refreshed from the current fp32 weights inside
+        the generation graph (every replay sees the aggregated model), in ONE launch: per layer the
+        bf16 copy of the dense columns and the one-hot block transposed to [C, N] fp32.
+        Returns (bf16 copies, transposed blocks), one per layer (G-out last)."""
         c0 = self.c_cols[0]
         names = [f"G.{i}.W" for i in range(len(self.gdims))] + ["G.out.W"]
         starts = list(self.off[:len(self.gdims)]) + [0]
         if getattr(self, "_gw16", None) is None:
             self._gw16 = [torch.zeros(self.p[nm].shape[0], -(-(c0 - a) // 8) * 8, dtype=torch.bfloat16,
                                       device=self.device) for nm, a in zip(names, starts)]
-        for w16, nm, a in zip(self._gw16, names, starts):
-            w16[:, :c0 - a].copy_(self.p[nm][:, :c0 - a])
-        return self._gw16
+            self._gwt = [torch.zeros(self.p[nm].shape[1] - (c0 - a), self.p[nm].shape[0], device=self.device)
+                         for nm, a in zip(names, starts)]
+        self.ops.L.gen_weight_prep([self.p[nm] for nm in names], [c0 - a for a in starts], self._gw16, self._gwt)
+        return self._gw16, self._gwt
 
     def _g_forward16(self, H16, logits, w16, cond):
         """Eval-mode generator on the bf16 buffer: each layer's GEMM reads bf16 rows and weights,
         gathers the one-hot block from col / opt, and writes bf16 (BN-eval + ReLU epilogue); the output
-        layer writes fp32 logits."""
+        layer writes fp32 logits.  w16 = _gen_weights16()."""
         o, p = self.ops, self.p
         c0 = self.c_cols[0]
         col, opt = cond
+        wd, wt = w16
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
-            W = p[f"G.{i}.W"]
-            oh = (W[:, c0 - a:].t().contiguous(), col, opt, self._cond_off, True)
-            o.linear_bn_relu(H16[:, a:c0], w16[i], p[f"G.{i}.b"], p[f"G.{i}.gamma"], p[f"G.{i}.beta"], H16[:, b_:a],
+            oh = (wt[i], col, opt, self._cond_off, True)
+            o.linear_bn_relu(H16[:, a:c0], wd[i], p[f"G.{i}.b"], p[f"G.{i}.gamma"], p[f"G.{i}.beta"], H16[:, b_:a],
                              None, None, None, None, p[f"G.{i}.rm"], p[f"G.{i}.rv"], False, self.cfg.bn_momentum,
                              self.cfg.bn_eps, onehot=oh)
-        W = p["G.out.W"]
-        oh = (W[:, c0:].t().contiguous(), col, opt, self._cond_off, True)
-        o.gemm(H16[:, :c0], w16[-1], logits, tb=True, bias=p["G.out.b"], onehot=oh)
+        oh = (wt[-1], col, opt, self._cond_off, True)
+        o.gemm(H16[:, :c0], wd[-1], logits, tb=True, bias=p["G.out.b"], onehot=oh)
 
     def _capture_gen(self, n: int):
         """Capture generate_decoded(n) with its own static buffers (graphs hold no tensor refs)."""

@@ -40,7 +40,7 @@ def main():
         eng._gen_graphs, eng._gen_bufs = {}, None
         eng.generate_decoded(n)
         _, H, lg, out, col, opt = eng._gen_graphs[n]
-        w16 = eng._gen_weights16() if bf16 else None
+        w16 = eng._gen_weights16()[0] if bf16 else None
         res = []
         for i, g in enumerate(eng.gdims):
             a, b_ = eng.off[i], eng.off[i + 1]
@@ -76,7 +76,7 @@ def main():
         from fed_tgan_amd.ops.hip import EPI_BN_EVAL_RELU, EPI_NONE
         layers_for(True)
         _, H, lg, out, col, opt = eng._gen_graphs[n]
-        w16 = eng._gen_weights16()
+        w16 = eng._gen_weights16()[0]
         a, b_ = eng.off[0], eng.off[1]
         W = p["G.0.W"]
         oh = (W[:, c0 - a:].t().contiguous(), col, opt, eng._cond_off, True)
