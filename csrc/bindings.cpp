@@ -158,7 +158,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.head_v = cfp(*head_v);
   }
   if (oh_w.has_value() && oh_w->defined()) {
-    TORCH_CHECK(tb && !ta, "gemm: the one-hot block needs C = A B^T");
+    TORCH_CHECK(!ta, "gemm: the one-hot block needs row-major A (its rows carry the conditions)");
     TORCH_CHECK(alpha == 1.0, "gemm: the one-hot block needs alpha = 1 (it is folded into the accumulators)");
     check_f32_2d(*oh_w, "oh_w");
     TORCH_CHECK(oh_trans ? oh_w->size(1) == N : oh_w->size(0) == N, "gemm: oh_w must be [N, C] (or [C, N] transposed)");
@@ -608,14 +608,18 @@ void gen_weight_prep(const std::vector<Tensor>& w, std::vector<int64_t> kd, cons
   fedtgan::GenWeightPrep a{};
   a.n_jobs = (int)n;
   for (size_t j = 0; j < n; ++j) {
-    check_f32_2d(w[j], "gen_weight_prep w");
+    // the weight as stored: [N, K] rows (unit k stride) or input-major (EngineConfig.g_wt: unit n stride)
+    TORCH_CHECK(w[j].is_cuda() && w[j].scalar_type() == at::kFloat && w[j].dim() == 2 &&
+                    (w[j].stride(1) == 1 || w[j].stride(0) == 1), "gen_weight_prep w: 2-D fp32, one unit stride");
     const int64_t N = w[j].size(0), K = w[j].size(1);
     TORCH_CHECK(kd[j] >= 0 && kd[j] <= K, "gen_weight_prep: kd");
     TORCH_CHECK(w16[j].is_cuda() && w16[j].scalar_type() == at::kBFloat16 && w16[j].dim() == 2 && w16[j].size(0) == N &&
                     w16[j].size(1) >= kd[j] && w16[j].stride(1) == 1, "gen_weight_prep: w16 [N, >= kd] bf16");
     check_f32_2d(wt[j], "gen_weight_prep wt");
     TORCH_CHECK(wt[j].is_contiguous() && wt[j].size(0) == K - kd[j] && wt[j].size(1) == N, "gen_weight_prep: wt [C, N]");
-    a.jobs[j] = fedtgan::GenWeightJob{cfp(w[j]), (int)N, ld_of(w[j]), (int)kd[j], (int)(K - kd[j]), hp(w16[j]),
+    const bool kmaj = w[j].stride(1) == 1;
+    a.jobs[j] = fedtgan::GenWeightJob{cfp(w[j]), (int)N, kmaj ? ld_of(w[j]) : 1, kmaj ? 1 : (int)w[j].stride(1),
+                                      (int)kd[j], (int)(K - kd[j]), hp(w16[j]),
                                       (int)w16[j].stride(0), fp(wt[j])};
   }
   fedtgan::launch_gen_weight_prep(a, cur_stream());

@@ -1943,13 +1943,13 @@ __global__ __launch_bounds__(256) void gen_weight_prep_kernel(GenWeightPrep a) {
     const int64_t nd = (int64_t)J.N * J.kd, nc = (int64_t)J.N * J.C;
     if (e < nd) {
       const int n = (int)(e / J.kd), k = (int)(e % J.kd);
-      J.w16[(size_t)n * J.ld16 + k] = f2bf(J.w[(size_t)n * J.ldw + k]);
+      J.w16[(size_t)n * J.ld16 + k] = f2bf(J.w[(size_t)n * J.ldw + (size_t)k * J.skw]);
       return;
     }
     e -= nd;
     if (e < nc) {
       const int n = (int)(e / J.C), c = (int)(e % J.C);
-      J.wt[(size_t)c * J.N + n] = J.w[(size_t)n * J.ldw + J.kd + c];
+      J.wt[(size_t)c * J.N + n] = J.w[(size_t)n * J.ldw + (size_t)(J.kd + c) * J.skw];
       return;
     }
     e -= nc;

@@ -246,8 +246,8 @@ void launch_sample_decode(const DecodeArgs& a, hipStream_t stream);
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream);
 
 struct GenWeightJob {
-  const float* w;   // [N, ldw] fp32 weight
-  int N, ldw, kd, C;
+  const float* w;   // fp32 weight, element (n, k) at w[n * ldw + k * skw] (skw = 1: [N, K] rows; ldw = 1: input-major storage)
+  int N, ldw, skw, kd, C;
   uint16_t* w16;    // [N, ld16] bf16: columns [0, kd)
   int ld16;
   float* wt;        // [C, N] fp32: columns [kd, kd + C) transposed

@@ -586,7 +586,8 @@ class FedRuntime:
         e = self.engine
         state = {"epoch": epoch, "flat": e.flat.cpu(), "mG": e.mG.cpu(), "vG": e.vG.cpu(), "mD": e.mD.cpu(),
                  "vD": e.vD.cpu(), "stepG": e.stepG.cpu(), "stepD": e.stepD.cpu(), "bn_batches": e.bn_batches,
-                 "round_times": self.epoch_stamps(), "cpu_rng": torch.get_rng_state()}
+                 "round_times": self.epoch_stamps(), "cpu_rng": torch.get_rng_state(),
+                 "g_wt": bool(e.cfg.g_wt)}       # flat-buffer layout of the generator weights
         if hasattr(e.ops, "ctr"):          # HIP backend: the device Philox step counter
             state["rng_ctr"] = e.ops.ctr.cpu()
         torch.save(state, self._ckpt_path())
@@ -597,6 +598,9 @@ class FedRuntime:
             return
         st = torch.load(p, weights_only=True)
         e = self.engine
+        if bool(st.get("g_wt", False)) != bool(e.cfg.g_wt):
+            raise RuntimeError(f"{p}: checkpoint generator layout g_wt={st.get('g_wt', False)} differs from the "
+                               f"engine's ({e.cfg.g_wt})")
         for k in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
             getattr(e, k).copy_(st[k])
         e.bn_batches = int(st["bn_batches"])

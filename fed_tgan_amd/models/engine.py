@@ -98,6 +98,11 @@ class EngineConfig:
     # fp32 path rounds to bf16 when staging its GEMM operands, so the output is bit-identical) --
     # half the GEMM operand bytes and no one-hot block written into the activation buffer
     gen_bf16: bool = True
+    # generator weights stored input-major (W^T, [in, out] rows) in the flat buffer: the one-hot block's
+    # weights for a condition are then one contiguous row, so the epilogue gathers of G0 / G1 / G-out
+    # read whole cache lines (with [out, in] rows a gather touches one line per output column).  The
+    # views self.p / self.g stay the logical [out, in] (transposed views); state dicts are unchanged.
+    g_wt: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -185,7 +190,11 @@ class CTGANEngine:
         # that stay zero under Adam, L2 decay and aggregation) and every tensor starts 16-B
         # aligned, so the GEMMs read them with 16-B loads; self.p / self.g expose the logical
         # [rows, cols] views, _ext() widens them to the padded width
-        store = [(s[0], _ceil4(s[1])) if len(s) == 2 else s for _, s, _ in spec]
+        # input-major generator weights (cfg.g_wt): stored [ceil4(in), ceil4(out)] -- the zero rows past
+        # `in` let _kpad widen K to a multiple of 4 exactly as the padded columns of [out, ceil4(in)] do
+        self.wt_names = {n for n, s, grp in spec if grp == "G" and len(s) == 2} if self.cfg.g_wt else set()
+        store = [((_ceil4(s[1]), _ceil4(s[0])) if nm in self.wt_names else (s[0], _ceil4(s[1]))) if len(s) == 2
+                 else s for nm, s, _ in spec]
         sizes = [int(np.prod(s)) for s in store]
         # every group starts 64-byte aligned (vectorised optimizer / aggregation kernels)
         align = 16
@@ -202,12 +211,14 @@ class CTGANEngine:
         self.p: Dict[str, torch.Tensor] = {}
         self.group_range = {}
 
-        def view(buf, o, n, shape, st):
+        def view(buf, o, n, shape, st, name):
             v = buf[o:o + n].view(st)
+            if name in self.wt_names:
+                return v[:shape[1], :shape[0]].t()
             return v[:, :shape[1]] if len(shape) == 2 else v
 
         for (name, shape, grp), n, o, st in zip(spec, sizes, offsets, store):
-            self.p[name] = view(self.flat, o, n, shape, st)
+            self.p[name] = view(self.flat, o, n, shape, st, name)
             a, _ = self.group_range.get(grp, (o, o))
             self.group_range[grp] = (a, (o + n + align - 1) // align * align)
         gA, gB = self.group_range["G"]
@@ -222,7 +233,7 @@ class CTGANEngine:
             if grp == "S":
                 continue
             base = o - (gA if grp == "G" else dA)
-            self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st)
+            self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st, name)
         self.mG = torch.zeros_like(self.gradG)
         self.vG = torch.zeros_like(self.gradG)
         self.mD = torch.zeros_like(self.gradD)
@@ -413,7 +424,9 @@ class CTGANEngine:
         stride allows it (16-B GEMM loads along K); otherwise the logical views."""
         x = H[:, a:]
         kp = _ceil4(x.shape[1])
-        if kp != x.shape[1] and H.stride(0) >= a + kp and W.stride(0) >= kp:
+        # room along K: the row stride of [out, in] storage; input-major storage has ceil4(in) rows
+        room = W.stride(0) if W.stride(1) == 1 else _ceil4(W.shape[1])
+        if kp != x.shape[1] and H.stride(0) >= a + kp and room >= kp:
             return _ext(x, kp), _ext(W, kp)
         return x, W
 
@@ -428,6 +441,9 @@ class CTGANEngine:
             return x, Wk, None
         c0 = self.c_cols[0]
         kd = c0 - a
+        if W.stride(0) == 1 and W.stride(1) != 1:
+            # input-major storage: the block is already [C, N] rows (ops normalise transposed views)
+            return H[:, a:c0], W[:, :kd], (W[:, kd:], cond[0], cond[1], self._cond_off)
         if len(cond) > 2 and cond[2]:
             return H[:, a:c0], W[:, :kd], (W[:, kd:].t().contiguous(), cond[0], cond[1], self._cond_off, True)
         return H[:, a:c0], W[:, :kd], (W[:, kd:], cond[0], cond[1], self._cond_off)

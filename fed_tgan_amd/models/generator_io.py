@@ -91,6 +91,7 @@ def load_generator(path: str, device: Optional[torch.device] = None, backend: st
     device = device or (torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu"))
     cfg = json.loads(st["engine_cfg"])
     cfg = {k: tuple(v) if isinstance(v, list) else v for k, v in cfg.items()}
+    cfg.setdefault("g_wt", False)     # files written before input-major generator storage existed
     ecfg = EngineConfig(**cfg)
     tr = VGMTransformer.from_dict(json.loads(st["transformer"]))
     eng = CTGANEngine(tr.layout, ecfg, device, backend=backend, seed=seed)

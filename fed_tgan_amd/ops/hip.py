@@ -53,6 +53,17 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
     return 32, int(max(1, min(want, -(-bursts // 2), cap_ws)))
 
 
+def _is_transposed(t) -> bool:
+    """A 2-D view whose rows are strided and whose columns are contiguous in memory (W.t() of a
+    row-major W) -- the GEMM library takes row-major operands, so such a view is passed as W."""
+    return t is not None and t.dim() == 2 and t.shape[0] > 1 and t.shape[1] > 1 and t.stride(0) == 1 \
+        and t.stride(1) != 1
+
+
+def _rowmajor(t, flag: bool):
+    return (t.t(), not flag) if _is_transposed(t) else (t, flag)
+
+
 GEMM_MAX_SPLITS = 64   # gemm.hip: the split-K epilogue keeps every slab value in registers
 
 
@@ -175,7 +186,21 @@ class HipOps:
         columns; the trailing one-hot block contributes W_c[n, cond_offset[col[m]] + opt[m]] (a gather, no
         MFMA).  transposed: W_c is given as [C, N] (contiguous rows: coalesced gathers).
         group 1 holds this GEMM, group 2 launches it together with the held one in ONE kernel (the
-        two must be independent); 0 launches now."""
+        two must be independent); 0 launches now.
+        Transposed views (unit row stride, e.g. the input-major generator weights of EngineConfig.g_wt)
+        are passed as their row-major storage with the transposition flag flipped; a transposed C is
+        computed as C^T = op(B)^T op(A)^T (plain epilogue only)."""
+        a, ta = _rowmajor(a, ta)
+        b, tb = _rowmajor(b, tb)
+        if _is_transposed(c):
+            if bias is not None or epi != EPI_NONE or onehot is not None or head is not None or bn is not None \
+                    or bn_part is not None:
+                raise ValueError("gemm: a transposed output takes no bias / epilogue / one-hot term")
+            a, b, ta, tb, c = b, a, not tb, not ta, c.t()
+        if onehot is not None and _is_transposed(onehot[0]):
+            if len(onehot) > 4 and onehot[4]:
+                raise ValueError("gemm: one-hot block given transposed twice")
+            onehot = (onehot[0].t(), onehot[1], onehot[2], onehot[3], True)
         M = a.shape[1] if ta else a.shape[0]
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]

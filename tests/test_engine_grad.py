@@ -7,6 +7,7 @@ with torch autograd in float64-free fp32, using the exact random draws the engin
 mask*slope buffers).
 """
 import numpy as np
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -40,9 +41,9 @@ class RecordingOps(TorchOps):
         self.rec["interp"] = out.clone()
 
 
-def _setup(gen_dims=(256, 256), dis_dims=(256, 256), batch=100):
+def _setup(gen_dims=(256, 256), dis_dims=(256, 256), batch=100, g_wt=False):
     _, _, _, _, _, _, tr, X = small_table()
-    cfg = EngineConfig(gen_dims=gen_dims, dis_dims=dis_dims, batch_size=batch)
+    cfg = EngineConfig(gen_dims=gen_dims, dis_dims=dis_dims, batch_size=batch, g_wt=g_wt)
     torch.manual_seed(0)
     eng = CTGANEngine(tr.layout, cfg, "cpu", backend="torch")
     eng.ops = RecordingOps()
@@ -110,8 +111,10 @@ def test_d_step_matches_autograd():
         assert torch.allclose(eng.p[n], t.detach(), rtol=1e-5, atol=1e-7), n
 
 
-def test_g_step_matches_autograd():
-    eng, tr = _setup()
+@pytest.mark.parametrize("g_wt", [False, True])
+def test_g_step_matches_autograd(g_wt):
+    """(g_wt: generator weights stored input-major; the logical views and the math are the same)"""
+    eng, tr = _setup(g_wt=g_wt)
     B, nP, Dd = eng.B, eng.nP, eng.Dd
     eng._d_step()
     before = {n: t.detach().clone() for n, t in eng.p.items()}
@@ -198,11 +201,13 @@ def test_deeper_discriminator_gp():
         assert (eng.g[n] - ref).abs().max() / scale < 2e-4, n
 
 
-def test_padded_storage_stays_zero():
+@pytest.mark.parametrize("g_wt", [False, True])
+def test_padded_storage_stays_zero(g_wt):
     """Weights live in rows padded to 4 floats (16-B GEMM loads); the padding columns and the
-    activation buffers' padding must stay exactly zero through training (they enter K sums)."""
+    activation buffers' padding must stay exactly zero through training (they enter K sums).
+    g_wt: input-major generator weights, padded to 4 along both dimensions."""
     from fed_tgan_amd.models.engine import _ceil4, _ext
-    eng, _ = _setup(batch=100)
+    eng, _ = _setup(batch=100, g_wt=g_wt)
     eng.ops = type(eng.ops).__mro__[1]()       # plain TorchOps
     eng.train_steps(3, use_graph=False)
     padded = 0
@@ -217,6 +222,16 @@ def test_padded_storage_stays_zero():
             assert torch.count_nonzero(_ext(buf, _ceil4(buf.shape[1]))[:, buf.shape[1]:]) == 0
     x, W = eng._kpad(eng.H, 0, eng.p["G.out.W"])
     assert x.shape[1] % 4 == 0 and W.shape[1] == x.shape[1]
+    if g_wt:
+        # every generator weight is a transposed view of [ceil4(in), ceil4(out)] storage, and the whole
+        # storage block outside the logical [in, out] corner is zero
+        for n in eng.wt_names:
+            t = eng.p[n]
+            assert t.stride(0) == 1 and t.stride(1) == _ceil4(t.shape[0])
+            o = t.storage_offset()
+            blk = eng.flat[o:o + _ceil4(t.shape[1]) * _ceil4(t.shape[0])].view(_ceil4(t.shape[1]), -1)
+            assert torch.equal(blk[:t.shape[1], :t.shape[0]], t.t())
+            assert torch.count_nonzero(blk) == torch.count_nonzero(t), n
 
 
 def test_paired_prepare_equals_two_phase_forwards():

@@ -19,12 +19,13 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def _engine(precision="bf16"):
+def _engine(precision="bf16", g_wt=False):
     from fed_tgan_amd.ops import native
     native.require()
     _, _, _, _, _, _, tr, X = small_table()
     torch.manual_seed(0)
-    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision), DEV, backend="hip", seed=11)
+    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, g_wt=g_wt), DEV, backend="hip",
+                      seed=11)
     eng.set_training_data(X)
     return eng, tr
 
@@ -80,9 +81,9 @@ def test_hip_d_update_matches_autograd(precision):
         assert _rel(eng.g[n], t.grad) < TOL[precision], (n, _rel(eng.g[n], t.grad))
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
-def test_hip_g_update_matches_autograd(precision):
-    eng, tr = _engine(precision)
+@pytest.mark.parametrize("precision,g_wt", [("bf16", False), ("fp32", False), ("bf16", True), ("fp32", True)])
+def test_hip_g_update_matches_autograd(precision, g_wt):
+    eng, tr = _engine(precision, g_wt)
     B, nP, Dd = eng.B, eng.nP, eng.Dd
     eng._d_step()
     before = {n: t.detach().clone() for n, t in eng.p.items()}
@@ -228,3 +229,45 @@ def test_bf16_generation_is_bit_identical(n):
     ref, got = run(False, True), run(True, True)
     assert torch.equal(ref[0], got[0])
     eng.cfg.gen_bf16 = True
+
+
+def test_input_major_generator_weights_match_row_major():
+    """EngineConfig.g_wt: the generator weights stored input-major ([in, out] rows; transposed views
+    into the GEMMs, one-hot gathers from contiguous rows) train like the [out, in] layout from the same
+    initial weights and Philox draws, and generate bit-identical tables from the same weights (the
+    generation copies are built from the same logical values)."""
+    from fed_tgan_amd.models.samplers import CondTables
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    cond = CondTables.from_encoded(X, tr.layout)
+    engs = []
+    for g_wt in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32", g_wt=g_wt), DEV, backend="hip",
+                          seed=4)
+        eng.set_training_data(X)
+        eng.set_generation_tables(cond, tr)
+        engs.append(eng)
+    a, b = engs
+    b.load_g_state_dict(a.g_state_dict())
+    b.load_d_state_dict(a.d_state_dict())
+    assert torch.equal(b.p["G.out.W"], a.p["G.out.W"]) and b.p["G.out.W"].stride(0) == 1
+    ga, gb = a.generate_decoded(4000), b.generate_decoded(4000)
+    assert torch.equal(ga, gb)
+    for e in engs:
+        e._prepare_paired()
+    torch.cuda.synchronize()
+    assert torch.allclose(a.logits2, b.logits2, atol=1e-4, rtol=1e-4)
+    for e in engs:
+        e.train_steps(4, use_graph=True)
+    torch.cuda.synchronize()
+    for n in a.p:
+        # (a hidden layer's Linear bias feeds BatchNorm: its gradient is rounding noise around 0, which
+        # Adam turns into +-lr steps of either sign -- compared loosely)
+        loose = n.startswith("G.") and n.endswith(".b") and n != "G.out.b"
+        assert torch.allclose(a.p[n], b.p[n], atol=4e-3 if loose else 2e-4, rtol=1e-3), n
+    for n in ("G.out.W", "G.0.W", "G.1.W"):
+        assert torch.allclose(a.g[n], b.g[n], atol=1e-5, rtol=1e-3), n
+    la, lb = a.losses(), b.losses()
+    assert np.allclose(la, lb, rtol=1e-3, atol=1e-4), (la, lb)

@@ -63,6 +63,31 @@ def onehot_ab(eng, tr, X, dev):
                   f"generate_decoded(40000) {t_gen:8.1f} us", flush=True)
 
 
+def gwt_ab(tr, X, dev, precision):
+    """EngineConfig.g_wt A/B: generator weights stored [out, in] vs input-major; full captured step and
+    generate_decoded(40000), two engines from the same initial weights, alternating."""
+    from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+    from fed_tgan_amd.models.samplers import CondTables
+    engs = {}
+    for g_wt in (False, True):
+        e = CTGANEngine(tr.layout, EngineConfig(precision=precision, g_wt=g_wt), dev, backend="hip", seed=1)
+        e.set_training_data(X)
+        e.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
+        engs[g_wt] = e
+    engs[True].load_g_state_dict(engs[False].g_state_dict())
+    for rep in range(3):
+        for g_wt, e in engs.items():
+            t_step = per_call(e._one_step, dev, n=5, reps=20)
+            e.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            for _ in range(20):
+                e.generate_decoded(40000)
+            torch.cuda.synchronize(dev)
+            t_gen = (time.perf_counter() - t) / 20 * 1e6
+            print(f"g_wt={int(g_wt)}: full step {t_step:8.2f} us   generate_decoded(40000) {t_gen:8.1f} us", flush=True)
+
+
 def bn_ab(eng, dev):
     """BN(train) from GEMM partials (bn_relu_apply) vs the separate full-reduction BN kernel."""
     for rep in range(3):
@@ -181,6 +206,7 @@ def main():
     ap.add_argument("--bn-ab", action="store_true", help="step: BN from GEMM partials vs full-reduction BN kernel")
     ap.add_argument("--dw0-ab", action="store_true", help="step: D0 weight-gradient tile 64 vs 128")
     ap.add_argument("--inlaunch-ab", action="store_true", help="split-K: epilogue launch vs in-launch reduction")
+    ap.add_argument("--gwt-ab", action="store_true", help="step + generation: generator weights [out, in] vs input-major")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -193,6 +219,8 @@ def main():
     res = {}
     if args.step_only:
         return step_only(eng, dev)
+    if args.gwt_ab:
+        return gwt_ab(tr, X, dev, args.precision)
     if args.gen:
         return gen_only(eng, tr, X, dev)
     if args.onehot_ab:

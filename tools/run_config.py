@@ -22,6 +22,14 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 
+def _engine_cfg(ecfg, overrides):
+    for kv in overrides:
+        k, v = kv.split("=", 1)
+        cur = getattr(ecfg, k)
+        setattr(ecfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+    return ecfg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spec", default="intrusion")
@@ -38,6 +46,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--json", default=None, help="append the JSON lines to this file")
     ap.add_argument("--one-stream", action="store_true", help="emulated clients share one HIP stream")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override for A/B runs, e.g. --engine g_wt=1")
     args = ap.parse_args()
 
     from fed_tgan_amd.data.schema import get_spec
@@ -54,7 +64,7 @@ def main():
     cfg = FedConfig(spec=spec, epochs=args.epochs, synthetic_rows=args.rows, shard_mode=args.shard,
                     dirichlet_alpha=args.alpha, out_dir=out, n_sample=args.n_sample, backend=args.backend,
                     gmm_backend="torch", aggregation=args.aggregation, seed=args.seed,
-                    engine=EngineConfig(precision=args.precision), verbose=True,
+                    engine=_engine_cfg(EngineConfig(precision=args.precision), args.engine), verbose=True,
                     client_streams=not args.one_stream)
     t0 = time.time()
     if args.clients == 1:
@@ -85,6 +95,8 @@ def main():
             "rows_per_client": args.rows, "epochs": args.epochs, "weights": [round(float(w), 4) for w in rt.weights],
             "mean_sec_per_epoch_after_first": round(sum(rt.round_times[1:]) / max(len(rt.round_times) - 1, 1), 4),
             "wall_s_incl_init": round(wall, 2), "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
+    if args.engine:
+        summ["engine_overrides"] = args.engine
     print(json.dumps(summ), flush=True)
     if args.json:
         with open(args.json, "a") as f:
