@@ -8,14 +8,19 @@
 //   * categoricals: vocabulary string of the integer code (QUOTE_MINIMAL quoting)
 //   * non-negative columns: the caller maps v = exp(x) - 1 (ceil when v < 0) with numpy's exp --
 //     libm's exp differs from numpy's in the last ulp for some inputs -- and v == -1 is written " "
-// Rows are formatted in parallel blocks by worker threads and written with one fwrite each.
+// Rows are formatted in parallel by worker threads, in row chunks handed out in order, and the
+// calling thread writes each chunk as soon as it is formatted (the file write overlaps the
+// formatting of the later chunks instead of following all of it).
 #include "csv_writer.h"
 
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
+#include <future>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -181,13 +186,29 @@ void write_csv_file(const std::string& path, const double* values, int64_t rows,
   }
   const int64_t min_rows = 2048;
   threads = (int)std::max<int64_t>(1, std::min<int64_t>(threads, (rows + min_rows - 1) / min_rows));
-  std::vector<std::string> parts((size_t)threads);
+  // ~4 chunks per thread (at least 512 rows each): the first chunk is ready after ~1/(4*threads) of
+  // the formatting time, and the write of chunk c overlaps the formatting of chunks > c
+  const int64_t chunk = std::max<int64_t>(512, (rows + 4 * threads - 1) / (4 * threads));
+  const int nchunks = (int)std::max<int64_t>(1, (rows + chunk - 1) / chunk);
+  std::vector<std::string> parts((size_t)nchunks);
+  std::vector<std::promise<void>> ready((size_t)nchunks);
+  std::vector<std::future<void>> done;
+  done.reserve((size_t)nchunks);
+  for (auto& r : ready) done.push_back(r.get_future());
+  std::atomic<int> next{0};
   std::vector<std::thread> pool;
-  const int64_t per = (rows + threads - 1) / threads;
   for (int t = 0; t < threads; ++t) {
-    const int64_t r0 = t * per, r1 = std::min(rows, r0 + per);
-    if (r0 >= r1) continue;
-    pool.emplace_back([&, t, r0, r1]() { parts[(size_t)t] = format_csv_rows(values, rows, cols, r0, r1, kinds, vocabs); });
+    pool.emplace_back([&]() {
+      for (int c = next.fetch_add(1); c < nchunks; c = next.fetch_add(1)) {
+        try {
+          const int64_t r0 = (int64_t)c * chunk, r1 = std::min(rows, r0 + chunk);
+          parts[(size_t)c] = format_csv_rows(values, rows, cols, r0, r1, kinds, vocabs);
+          ready[(size_t)c].set_value();
+        } catch (...) {
+          ready[(size_t)c].set_exception(std::current_exception());
+        }
+      }
+    });
   }
   std::string header;
   for (int64_t j = 0; j < cols; ++j) {
@@ -195,12 +216,22 @@ void write_csv_file(const std::string& path, const double* values, int64_t rows,
     append_field(header, names[(size_t)j]);
   }
   header.push_back('\n');
-  for (auto& th : pool) th.join();
   FILE* f = std::fopen(path.c_str(), "wb");
-  if (!f) throw std::runtime_error("csv: cannot open " + path);
-  std::fwrite(header.data(), 1, header.size(), f);
-  for (auto& p : parts) std::fwrite(p.data(), 1, p.size(), f);
-  std::fclose(f);
+  std::exception_ptr err;
+  if (!f) err = std::make_exception_ptr(std::runtime_error("csv: cannot open " + path));
+  else std::fwrite(header.data(), 1, header.size(), f);
+  for (int c = 0; c < nchunks; ++c) {
+    try {
+      done[(size_t)c].get();
+    } catch (...) {
+      if (!err) err = std::current_exception();
+    }
+    if (f && !err) std::fwrite(parts[(size_t)c].data(), 1, parts[(size_t)c].size(), f);
+    std::string().swap(parts[(size_t)c]);
+  }
+  for (auto& th : pool) th.join();
+  if (f) std::fclose(f);
+  if (err) std::rethrow_exception(err);
 }
 
 }  // namespace fedtgan
