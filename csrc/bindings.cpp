@@ -66,6 +66,20 @@ const uint64_t* ctr_ptr(const optional<Tensor>& t) {
   return reinterpret_cast<const uint64_t*>(t->data_ptr<int64_t>());
 }
 
+// pairing state of gemm(..., group): a GEMM held for launch_gemm_pair (group 1 / 2) or for the next
+// adam_cs launch (group 3)
+thread_local fedtgan::GemmArgs held{};
+thread_local bool has_held = false;
+thread_local hipStream_t held_stream = nullptr;
+struct AdamHeld {
+  fedtgan::GemmArgs g;
+  hipStream_t stream;
+  float* c;
+  int64_t M, N, ldc;
+  bool active;
+};
+thread_local AdamHeld g_adam_held{};
+
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
@@ -193,11 +207,17 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.tile_cnt = reinterpret_cast<unsigned*>(tile_cnt->data_ptr<int>());
   }
   // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
-  // must be independent -- neither reads what the other writes); group 0: launch now
-  thread_local fedtgan::GemmArgs held{};
-  thread_local bool has_held = false;
-  thread_local hipStream_t held_stream = nullptr;
+  // must be independent -- neither reads what the other writes); group 3: hold it for the next
+  // adam_cs launch on this stream (a weight gradient inside that optimizer's gradient buffer: the
+  // two become one launch, gemm_adam_kernel); group 0: launch now
   const hipStream_t hs = cur_stream();
+  if (group == 3) {
+    TORCH_CHECK(!g_adam_held.active, "gemm: a GEMM is already held for the Adam launch");
+    TORCH_CHECK(epi == fedtgan::EPI_NONE && beta == 0.0 && !g.bias && !g.oh_w && !g.head_a && !g.bn_part && !cbf && !bin,
+                "gemm: a GEMM fused with Adam takes a plain epilogue (no bias / beta / one-hot / head / BN partials)");
+    g_adam_held = AdamHeld{g, hs, c.data_ptr<float>(), (int64_t)M, (int64_t)N, (int64_t)g.ldc, true};
+    return;
+  }
   if (group == 1) {
     TORCH_CHECK(!has_held, "gemm: a GEMM is already held for pairing");
     held = g;
@@ -495,6 +515,7 @@ void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Te
 
 void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& step, double lr, double b1,
           double b2, double eps, double wd, const optional<Tensor>& rng_bump) {
+  TORCH_CHECK(!g_adam_held.active, "adam: a GEMM held for the Adam launch needs adam_cs (the column-sum form)");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam: contiguous");
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: sizes");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0,
@@ -551,8 +572,29 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
   }
   uint64_t* bump = nullptr;
   if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
+  const hipStream_t hs = cur_stream();
+  if (g_adam_held.active) {
+    // the held weight-gradient GEMM (gemm(..., group=3)) writes rows [0, M) x [0, N) at stride ldc of a
+    // block inside g: Adam over that whole block is left to the GEMM's tiles (elements of the block
+    // outside M x N -- padding -- keep their values, as their gradient is zero)
+    AdamHeld h = g_adam_held;
+    g_adam_held.active = false;
+    TORCH_CHECK(h.stream == hs, "adam_cs: the GEMM held for it was issued on another stream");
+    const int64_t off = h.c - g0, len = (h.M - 1) * h.ldc + h.N;
+    TORCH_CHECK(h.c >= g0 && off % 4 == 0 && h.ldc % 4 == 0 && off + (h.M * h.ldc) <= n && len > 0,
+                "adam_cs: the held GEMM's output must be a 4-aligned block inside the gradient buffer");
+    for (int k = 0; k < cs.n_jobs; ++k)
+      TORCH_CHECK(off >= cs.own_hi[k] || off + h.M * h.ldc <= cs.own_lo[k], "adam_cs: the held GEMM overlaps a job output");
+    cs.skip_lo = off;
+    cs.skip_hi = off + h.M * h.ldc;
+    if (fedtgan::launch_gemm_adam(h.g, fp(p), cfp(g), fp(m), fp(v), cfp(step), n, (float)lr, (float)b1, (float)b2,
+                                  (float)eps, (float)wd, bump, cs, hs))
+      return;
+    cs.skip_lo = cs.skip_hi = 0;      // shape not instantiated: the GEMM, then the plain launch
+    fedtgan::launch_gemm(h.g, hs);
+  }
   fedtgan::launch_adam_colsum(fp(p), cfp(g), fp(m), fp(v), cfp(step), p.numel(), (float)lr, (float)b1, (float)b2,
-                              (float)eps, (float)wd, bump, cs, cur_stream());
+                              (float)eps, (float)wd, bump, cs, hs);
 }
 
 void sample_decode(const Tensor& logits, const Tensor& out, const Tensor& kind, const Tensor& start,

@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "adam_cs.h"
 
 namespace fedtgan {
 
@@ -1491,17 +1492,6 @@ int g_adam_store = 16;
 int g_adam_max_blocks = 65535;
 
 template <int AUX>
-__device__ __forceinline__ void adam_store4(float4* base, __amdgpu_buffer_rsrc_t rs, int64_t i, float4 x) {
-  if constexpr (AUX == 0) {
-    base[i] = x;
-  } else {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 u = *reinterpret_cast<const u32x4*>(&x);
-    __builtin_amdgcn_raw_buffer_store_b128(u, rs, (int)(i * 16), 0, AUX);
-  }
-}
-
-template <int AUX>
 __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v,
                                                    const float* __restrict__ step, int64_t n4, float lr, float b1,
@@ -1521,12 +1511,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
     float* mf = reinterpret_cast<float*>(&mm);
     float* vf = reinterpret_cast<float*>(&vv);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float gq = gf[q] + wd * pf[q];
-      mf[q] = b1 * mf[q] + (1.f - b1) * gq;
-      vf[q] = b2 * vf[q] + (1.f - b2) * gq * gq;
-      pf[q] -= sz * mf[q] / (sqrtf(vf[q]) / bc2s + eps);
-    }
+    for (int q = 0; q < 4; ++q) adam_elem(gf[q], pf[q], mf[q], vf[q], b1, b2, eps, wd, sz, bc2s);
     adam_store4<AUX>(p, rp, i, pp);
     adam_store4<AUX>(m, rm, i, mm);
     adam_store4<AUX>(v, rv, i, vv);
@@ -1541,10 +1526,11 @@ __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, c
   const float t = step[0];
   const float bc1 = 1.f - powf(b1, t);
   const float bc2s = sqrtf(1.f - powf(b2, t));
-  const float gq = g[i] + wd * p[i];
-  m[i] = b1 * m[i] + (1.f - b1) * gq;
-  v[i] = b2 * v[i] + (1.f - b2) * gq * gq;
-  p[i] -= (lr / bc1) * m[i] / (sqrtf(v[i]) / bc2s + eps);
+  float pe = p[i], me = m[i], ve = v[i];
+  adam_elem(g[i], pe, me, ve, b1, b2, eps, wd, lr / bc1, bc2s);
+  p[i] = pe;
+  m[i] = me;
+  v[i] = ve;
 }
 
 // ---- Adam with the step's column sums folded in: one launch instead of colsum + Adam.
@@ -1559,146 +1545,7 @@ __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, con
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       const float* __restrict__ step, int64_t n4, float lr, float b1,
                                                       float b2, float eps, float wd, uint64_t* rng_bump, AdamColsum cs) {
-  const float t = step[0];
-  const float bc1 = 1.f - powf(b1, t);
-  const float bc2s = sqrtf(1.f - powf(b2, t));
-  const float sz = lr / bc1;
-  const int nb = cs.blk_start[cs.n_jobs];
-  if ((int)blockIdx.x < nb) {
-    // 4 float4 column quads x 64 row groups; a 500-row job is 8 loads per thread
-    __shared__ float part[2][ACS_GROUPS][ACS_COLS + 1];
-    int j = 0;
-    while (j + 1 < cs.n_jobs && (int)blockIdx.x >= cs.blk_start[j + 1]) ++j;
-    const ColsumJob jb = cs.jobs[j];
-    const int cb = (int)blockIdx.x - cs.blk_start[j];
-    const int qd = threadIdx.x & 3, grp = threadIdx.x >> 2;
-    const int c0 = cb * ACS_COLS + qd * 4;
-    // the Adam operands of this block's owned elements are fetched first, so their round trip
-    // overlaps the column-sum loads instead of following them
-    const int64_t e = cs.own_lo[j] + cb * ACS_COLS + (int)threadIdx.x;
-    const bool upd = threadIdx.x < ACS_COLS && e < cs.own_hi[j];
-    float pe = 0.f, me = 0.f, ve = 0.f;
-    if (upd) {
-      pe = p[e];
-      me = m[e];
-      ve = v[e];
-    }
-    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), d4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const bool two = jb.dot_w != nullptr;   // a second column sum with the dot's row weights
-    if (cs.vec[j]) {   // 16-B aligned rows padded to >= ceil4(cols): whole quads are in bounds
-      const int cq = min(c0, ((jb.cols + 3) & ~3) - 4);
-#pragma unroll 4
-      for (int r = grp; r < jb.rows; r += ACS_GROUPS) {
-        const float wr = jb.w ? jb.w[r] : 1.f;
-        const float ur = two ? jb.dot_w[r] : 0.f;
-        const float4 x = *reinterpret_cast<const float4*>(jb.a + (size_t)r * jb.lda + cq);
-        s4.x += wr * x.x;
-        s4.y += wr * x.y;
-        s4.z += wr * x.z;
-        s4.w += wr * x.w;
-        d4.x += ur * x.x;
-        d4.y += ur * x.y;
-        d4.z += ur * x.z;
-        d4.w += ur * x.w;
-      }
-    } else {
-      const int last = jb.cols - 1;
-      for (int r = grp; r < jb.rows; r += ACS_GROUPS) {
-        const float wr = jb.w ? jb.w[r] : 1.f;
-        const float ur = two ? jb.dot_w[r] : 0.f;
-        const float* ar = jb.a + (size_t)r * jb.lda;
-        const float x0 = ar[min(c0, last)], x1 = ar[min(c0 + 1, last)];
-        const float x2 = ar[min(c0 + 2, last)], x3 = ar[min(c0 + 3, last)];
-        s4.x += wr * x0;
-        s4.y += wr * x1;
-        s4.z += wr * x2;
-        s4.w += wr * x3;
-        d4.x += ur * x0;
-        d4.y += ur * x1;
-        d4.z += ur * x2;
-        d4.w += ur * x3;
-      }
-    }
-    part[0][grp][qd * 4 + 0] = s4.x;
-    part[0][grp][qd * 4 + 1] = s4.y;
-    part[0][grp][qd * 4 + 2] = s4.z;
-    part[0][grp][qd * 4 + 3] = s4.w;
-    part[1][grp][qd * 4 + 0] = d4.x;
-    part[1][grp][qd * 4 + 1] = d4.y;
-    part[1][grp][qd * 4 + 2] = d4.z;
-    part[1][grp][qd * 4 + 3] = d4.w;
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;   // wave 0: lane = column (lane & 15) x quarter of the row groups
-    float tsum = 0.f, tdot = 0.f;
-#pragma unroll
-    for (int i = 0; i < ACS_GROUPS / 4; ++i) {
-      tsum += part[0][(lane >> 4) * (ACS_GROUPS / 4) + i][lane & 15];
-      tdot += part[1][(lane >> 4) * (ACS_GROUPS / 4) + i][lane & 15];
-    }
-    tsum += __shfl_xor(tsum, 16);
-    tsum += __shfl_xor(tsum, 32);
-    tdot += __shfl_xor(tdot, 16);
-    tdot += __shfl_xor(tdot, 32);
-    if (!two) tdot = tsum;
-    const int col = cb * ACS_COLS + lane;
-    const bool live = lane < ACS_COLS && col < jb.cols;
-    if (live && jb.out) jb.out[col] = tsum;
-    if (jb.dot_v) {
-      // a dot over this job's own parameters reads them as they were before this launch (the
-      // prefetched value of the lane that updates them): no other workgroup writes them
-      const float vc = live ? (cs.dot_self[j] ? pe : jb.dot_v[col]) : 0.f;
-      float d = tdot * vc;
-      if (cb == 0 && jb.dot_e) {   // + e * sum_r u[r], once per job
-        const float* uw = two ? jb.dot_w : jb.w;
-        float ws = 0.f;
-        for (int r = lane; r < jb.rows; r += 64) ws += uw ? uw[r] : 1.f;
-        d += wave_sum(ws) * (lane == 0 ? jb.dot_e[0] : 0.f);
-      }
-      d = wave_sum(d);
-      if (lane == 0) atomicAdd(jb.dot_out, d);
-    }
-    if (upd) {
-      const float gq = (live ? tsum : 0.f) + wd * pe;
-      const float mq = b1 * me + (1.f - b1) * gq;
-      const float vq = b2 * ve + (1.f - b2) * gq * gq;
-      m[e] = mq;
-      v[e] = vq;
-      p[e] = pe - sz * mq / (sqrtf(vq) / bc2s + eps);
-    }
-    return;
-  }
-  const int bytes = (int)(n4 * 16);
-  float4* p4 = reinterpret_cast<float4*>(p);
-  float4* m4 = reinterpret_cast<float4*>(m);
-  float4* v4 = reinterpret_cast<float4*>(v);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(p4, 0, bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(m4, 0, bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(v4, 0, bytes, 0x00020000);
-  const int64_t stride = (int64_t)(gridDim.x - nb) * blockDim.x;
-  for (int64_t i = (int64_t)(blockIdx.x - nb) * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int64_t e = i * 4;
-    bool owned = false;
-    for (int k = 0; k < cs.n_jobs; ++k) owned |= e >= cs.own_lo[k] && e < cs.own_hi[k];
-    if (owned) continue;
-    float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
-    float* pf = reinterpret_cast<float*>(&pp);
-    float* gf = reinterpret_cast<float*>(&gg);
-    float* mf = reinterpret_cast<float*>(&mm);
-    float* vf = reinterpret_cast<float*>(&vv);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float gq = gf[q] + wd * pf[q];
-      mf[q] = b1 * mf[q] + (1.f - b1) * gq;
-      vf[q] = b2 * vf[q] + (1.f - b2) * gq * gq;
-      pf[q] -= sz * mf[q] / (sqrtf(vf[q]) / bc2s + eps);
-    }
-    adam_store4<AUX>(p4, rp, i, pp);
-    adam_store4<AUX>(m4, rm, i, mm);
-    adam_store4<AUX>(v4, rv, i, vv);
-  }
-  if (rng_bump && (int)blockIdx.x == nb && threadIdx.x == 0) rng_bump[0] += 1ull;
+  adam_cs_body<AUX>((int)blockIdx.x, (int)gridDim.x, p, g, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs);
 }
 
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,

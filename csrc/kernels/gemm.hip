@@ -37,6 +37,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "adam_cs.h"
 
 namespace fedtgan {
 
@@ -538,7 +539,7 @@ __device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (
 // 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
 // The body of one output tile; (bx, by, bz) index the tile within a (gx, gy, gz) tile grid.  Called by
 // gemm_kernel (one GEMM per launch) and gemm_pair_kernel (two independent GEMMs in one launch).
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false>
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool ADAM = false>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int gx, int gy, int gz,
                                           unsigned char* __restrict__ smem) {
   static_assert(!BIN || (!TA && TB && !F32), "bf16 operands: C = A B^T, both k-contiguous, bf16 MFMA");
@@ -824,6 +825,34 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
     return;
   }
+  if constexpr (ADAM) {
+    // weight gradient -> Adam (gemm_adam_kernel; unsplit, plain epilogue, checked on the host): each
+    // lane's gradients and the same elements' parameter and moments, updated in registers with the
+    // float4 Adam's expression (adam_elem); the gradient is also stored (grad-flow diagnostics)
+    const float t = g.adam_step[0];
+    const float bc1 = 1.f - powf(g.adam_b1, t);
+    const float bc2s = sqrtf(1.f - powf(g.adam_b2, t));
+    const float sz = g.adam_lr / bc1;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WN + j * 16 + (lane & 15);
+          if (m >= g.M || n >= g.N) continue;
+          const size_t e = (size_t)m * g.ldc + n;
+          const float gr = g.alpha * acc[i][j][r];
+          float pe = g.adam_p[e], me = g.adam_m[e], ve = g.adam_v[e];
+          adam_elem(gr, pe, me, ve, g.adam_b1, g.adam_b2, g.adam_eps, g.adam_wd, sz, bc2s);
+          g.c[e] = gr;
+          g.adam_m[e] = me;
+          g.adam_v[e] = ve;
+          g.adam_p[e] = pe;
+        }
+    return;
+  }
   // (the training GEMMs' register epilogue keeps per-element bias loads: hoisting them per column,
   // as the LDS epilogues do, measured 1 us slower per step -- profiles/README.md)
 #pragma unroll
@@ -909,11 +938,11 @@ int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch
 int g_gemm_splitk_inlaunch = 1;   // 1: split-K reduced by the last-arriving slice (GemmArgs::tile_cnt)
 
 template <int SMAX>
-__global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
+__device__ __forceinline__ void splitk_epilogue_body(const GemmArgs& g, int bid, int nblk) {
   const int splits = g.splitk;
   const size_t total = (size_t)g.M * g.N;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
-  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+  for (size_t idx = (size_t)bid * blockDim.x + threadIdx.x; idx < total; idx += (size_t)nblk * blockDim.x) {
     const int m = (int)(idx / g.N), n = (int)(idx % g.N);
     float part[SMAX];
 #pragma unroll
@@ -928,6 +957,34 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
     if (g.bias) v += g.bias[n];
     if (g.oh_w) v += onehot_term(g, m, n);
     st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, idx), g.wt);
+  }
+}
+
+template <int SMAX>
+__global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
+  splitk_epilogue_body<SMAX>(g, (int)blockIdx.x, (int)gridDim.x);
+}
+
+
+
+// A weight-gradient GEMM and its optimizer's Adam in ONE launch: the first nt workgroups are the
+// GEMM's tiles, which apply Adam to their own outputs (gemm_tile<..., ADAM>); the rest run the
+// flat-buffer Adam with its folded column sums (adam_cs_body), skipping the GEMM's range.  The step's
+// last two launches (the generator's first-layer weight gradient, then the generator's Adam) become
+// one: none of the other Adam work waits for that gradient.
+template <bool VEC, int TM, int AUX>
+__global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, float* p, const float* gr, float* m,
+                                                       float* v, const float* step, int64_t n4, float lr, float b1,
+                                                       float b2, float eps, float wd, uint64_t* rng_bump,
+                                                       AdamColsum cs) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, TM, TM>::STAGE];
+  const int nt = gd.x * gd.y * gd.z;
+  const int b = blockIdx.x;
+  if (b < nt) {
+    gemm_tile<true, false, false, VEC, TM, TM, false, true>(g, b % gd.x, (b / gd.x) % gd.y, b / (gd.x * gd.y), gd.x,
+                                                             gd.y, gd.z, smem);
+  } else {
+    adam_cs_body<AUX>(b - nt, (int)gridDim.x - nt, p, gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs);
   }
 }
 
@@ -1058,6 +1115,46 @@ void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
   }
   gemm_epilogue_launch(g1, stream);
   gemm_epilogue_launch(g2, stream);
+}
+
+bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v, const float* step, int64_t n,
+                      float lr, float b1, float b2, float eps, float wd, uint64_t* rng_ctr_bump,
+                      const AdamColsum& cs_in, hipStream_t stream) {
+  if (g.M <= 0 || g.N <= 0 || g.f32 || g.bin || g.c16 || !g.ta || g.tb || n % 4 != 0) return false;
+  const dim3 d = gemm_prepare(g);
+  if (g.splitk != 1 || (g.tile != 32 && g.tile != 64)) return false;
+  g.adam_p = p + (g.c - gr);
+  g.adam_m = m + (g.c - gr);
+  g.adam_v = v + (g.c - gr);
+  g.adam_step = step;
+  g.adam_lr = lr;
+  g.adam_b1 = b1;
+  g.adam_b2 = b2;
+  g.adam_eps = eps;
+  g.adam_wd = wd;
+  AdamColsum cs = cs_in;
+  cs.n_jobs = std::min(cs.n_jobs, 8);
+  cs.blk_start[0] = 0;
+  for (int k = 0; k < cs.n_jobs; ++k) cs.blk_start[k + 1] = cs.blk_start[k] + (cs.jobs[k].cols + ACS_COLS - 1) / ACS_COLS;
+  const int64_t n4 = n / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
+  const Grid3 gd{(int)d.x, (int)d.y, (int)d.z};
+  const int grid = gd.x * gd.y * gd.z + std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
+#define FEDTGAN_GEMM_ADAM(V, T, AUX)                                                                               \
+  hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX>), dim3(grid), dim3(NT), 0, stream, g, gd, p, gr, m, v, step, n4, lr, \
+                     b1, b2, eps, wd, rng_ctr_bump, cs)
+#define FEDTGAN_GEMM_ADAM_T(V, T)                                 \
+  if (g_adam_store == 2) FEDTGAN_GEMM_ADAM(V, T, 2);              \
+  else if (g_adam_store == 16) FEDTGAN_GEMM_ADAM(V, T, 16);       \
+  else FEDTGAN_GEMM_ADAM(V, T, 0);
+  if (g.vec) {
+    if (g.tile == 32) { FEDTGAN_GEMM_ADAM_T(true, 32) } else { FEDTGAN_GEMM_ADAM_T(true, 64) }
+  } else {
+    if (g.tile == 32) { FEDTGAN_GEMM_ADAM_T(false, 32) } else { FEDTGAN_GEMM_ADAM_T(false, 64) }
+  }
+#undef FEDTGAN_GEMM_ADAM_T
+#undef FEDTGAN_GEMM_ADAM
+  return true;
 }
 
 }  // namespace fedtgan

@@ -75,6 +75,15 @@ struct GemmArgs {
   const uint16_t* b16;
   uint16_t* c16;
   int bin;
+  // Adam applied in the epilogue (gemm_adam_kernel only; nullable): the output is a weight gradient
+  // inside an optimizer's flat gradient buffer; adam_p / adam_m / adam_v point at the same offset of
+  // the parameter / moment buffers, so output (m, n) updates element m * ldc + n of each.  The
+  // gradient itself is still written to c.
+  float* adam_p;
+  float* adam_m;
+  float* adam_v;
+  const float* adam_step;
+  float adam_lr, adam_b1, adam_b2, adam_eps, adam_wd;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -188,10 +197,17 @@ struct AdamColsum {
   int blk_start[9];   // filled by the launcher
   int64_t own_lo[8], own_hi[8];
   int dot_self[8];    // dot_v is this job's own output's parameters: use the pre-update values
+  int64_t skip_lo, skip_hi;   // elements updated by a fused GEMM's Adam epilogue (gemm_adam_kernel)
 };
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
                         float b2, float eps, float wd, uint64_t* rng_ctr_bump, const AdamColsum& cs,
                         hipStream_t stream);
+// a weight-gradient GEMM (g.adam_* set, unsplit) and the Adam + column-sum launch of the same
+// optimizer (its flat range [cs.skip_lo, cs.skip_hi) left to the GEMM) in ONE launch; returns false
+// (nothing launched) where that GEMM shape is not instantiated
+bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v, const float* step, int64_t n,
+                      float lr, float b1, float b2, float eps, float wd, uint64_t* rng_ctr_bump, const AdamColsum& cs,
+                      hipStream_t stream);
 
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through

@@ -103,6 +103,9 @@ class EngineConfig:
     # read whole cache lines (with [out, in] rows a gather touches one line per output column).  The
     # views self.p / self.g stay the logical [out, in] (transposed views); state dicts are unchanged.
     g_wt: bool = True
+    # HIP: the generator's first-layer weight gradient (the step's last GEMM) runs in the same launch
+    # as the generator's Adam, its tiles applying Adam to their own outputs (gemm_adam_kernel)
+    fuse_g_adam: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -673,7 +676,10 @@ class CTGANEngine:
                        group=2 if pair else 0)
             else:
                 x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
-                o.gemm(self.da[i], x, dW, ta=True)
+                # held for the Adam launch that follows (fold_colsum: _g_adam(jobs) is next on this stream)
+                fuse = fold_colsum and self.lanes is None and self.cfg.fuse_g_adam and \
+                    getattr(o, "gemm_adam", False)
+                o.gemm(self.da[i], x, dW, ta=True, group=3 if fuse else 0)
         self._join(1, 2, 3)
         return jobs if fold_colsum else None
 

@@ -81,6 +81,7 @@ def _effective_splits(K: int, sk: int, kc: int) -> int:
 class HipOps:
     name = "hip"
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
+    gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
 
     def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16"):
         self.L = native.require()
@@ -186,7 +187,9 @@ class HipOps:
         columns; the trailing one-hot block contributes W_c[n, cond_offset[col[m]] + opt[m]] (a gather, no
         MFMA).  transposed: W_c is given as [C, N] (contiguous rows: coalesced gathers).
         group 1 holds this GEMM, group 2 launches it together with the held one in ONE kernel (the
-        two must be independent); 0 launches now.
+        two must be independent); group 3 holds a weight gradient (plain epilogue, inside an optimizer's
+        gradient buffer) for the next adam(..., jobs=...), which then runs both in ONE kernel, the GEMM's
+        tiles applying Adam to their outputs; 0 launches now.
         Transposed views (unit row stride, e.g. the input-major generator weights of EngineConfig.g_wt)
         are passed as their row-major storage with the transposition flag flipped; a transposed C is
         computed as C^T = op(B)^T op(A)^T (plain epilogue only)."""

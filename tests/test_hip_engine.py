@@ -274,3 +274,32 @@ def test_input_major_generator_weights_match_row_major():
         assert _rel(b.g[n], a.g[n]) < 2e-3, (n, _rel(b.g[n], a.g[n]))
     la, lb = a.losses(), b.losses()
     assert np.allclose(la, lb, rtol=1e-3, atol=1e-4), (la, lb)
+
+
+@pytest.mark.parametrize("knob", ["fuse_g_adam"])
+def test_fused_adam_launches_match_separate_launches(knob):
+    """EngineConfig.fuse_g_adam: the generator's first-layer weight gradient and the generator's Adam
+    in one launch (the GEMM's tiles update their own outputs) give the same gradients, parameters and
+    moments as the separate launches (one Adam expression everywhere: bitwise)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    engs = []
+    for fuse in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, **{knob: fuse}), DEV, backend="hip", seed=6)
+        eng.set_training_data(X)
+        engs.append(eng)
+    a, b = engs
+    b.flat.copy_(a.flat)
+    for e in engs:
+        e.train_steps(1, use_graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a.g["G.0.W"], b.g["G.0.W"]) and torch.equal(a.g["D.0.W"], b.g["D.0.W"])
+    for buf in ("flat", "mG", "vG", "mD", "vD"):       # one Adam expression (adam_elem) in both kernels
+        x, y = getattr(a, buf), getattr(b, buf)
+        assert torch.equal(x, y), (buf, float((x - y).abs().max()))
+    for e in engs:
+        e.train_steps(8, use_graph=True)
+    torch.cuda.synchronize()
+    assert np.isfinite(b.losses()).all() and bool(torch.isfinite(b.flat).all())

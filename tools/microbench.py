@@ -63,14 +63,15 @@ def onehot_ab(eng, tr, X, dev):
                   f"generate_decoded(40000) {t_gen:8.1f} us", flush=True)
 
 
-def gwt_ab(tr, X, dev, precision):
-    """EngineConfig.g_wt A/B: generator weights stored [out, in] vs input-major; full captured step and
-    generate_decoded(40000), two engines from the same initial weights, alternating."""
+def gwt_ab(tr, X, dev, precision, key="g_wt"):
+    """A/B of a boolean EngineConfig field (default g_wt: generator weights stored [out, in] vs
+    input-major); full captured step and generate_decoded(40000), two engines from the same initial
+    weights, alternating."""
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from fed_tgan_amd.models.samplers import CondTables
     engs = {}
     for g_wt in (False, True):
-        e = CTGANEngine(tr.layout, EngineConfig(precision=precision, g_wt=g_wt), dev, backend="hip", seed=1)
+        e = CTGANEngine(tr.layout, EngineConfig(precision=precision, **{key: g_wt}), dev, backend="hip", seed=1)
         e.set_training_data(X)
         e.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
         engs[g_wt] = e
@@ -85,7 +86,44 @@ def gwt_ab(tr, X, dev, precision):
                 e.generate_decoded(40000)
             torch.cuda.synchronize(dev)
             t_gen = (time.perf_counter() - t) / 20 * 1e6
-            print(f"g_wt={int(g_wt)}: full step {t_step:8.2f} us   generate_decoded(40000) {t_gen:8.1f} us", flush=True)
+            print(f"{key}={int(g_wt)}: full step {t_step:8.2f} us   generate_decoded(40000) {t_gen:8.1f} us", flush=True)
+
+
+def fork_probe(eng, dev):
+    """Cost of a forked branch inside the captured step: the one-stream step vs the same step with a
+    second sampler launch (into scratch buffers) on a side stream, forked after the G phase's dlogits
+    and joined at the end of the step (what hiding step t+1's sampler behind step t's G backward
+    would look like)."""
+    o, B = eng.ops, eng.B
+    side = torch.cuda.Stream(dev)
+    H2s, Xs, Xr = eng.H2.clone(), eng.Xall[2 * B:4 * B].clone(), eng.X_real.clone()
+    col, opt = eng.col2.clone(), eng.opt2.clone()
+    sD, sG, met = eng.stepD.clone(), eng.stepG.clone(), eng.metrics.clone()
+    ctr_s = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def forked(work: bool):
+        def step():
+            cur = torch.cuda.current_stream(dev)
+            eng._prepare_paired()
+            eng._d_update()
+            eng._g_dlogits()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                if work:
+                    o.sample_train(eng.tables, H2s, eng.z_cols, eng.c_cols, Xs, Xr, eng.Dd, col, opt,
+                                   step_counter=(sD, sG), metrics=met, zero_metrics=True, stream_id=1)
+                else:
+                    o.L.rng_bump(ctr_s)
+            eng._g_adam(eng._g_backward(fold_colsum=True))
+            cur.wait_stream(side)
+        return step
+
+    for _ in range(3):
+        base = per_call(eng._one_step, dev, n=5, reps=20)
+        f0 = per_call(forked(False), dev, n=5, reps=20)
+        f1 = per_call(forked(True), dev, n=5, reps=20)
+        print(f"one stream {base:8.2f} us   fork+join (1-thread kernel) {f0:8.2f} us   "
+              f"fork+join (concurrent sampler) {f1:8.2f} us", flush=True)
 
 
 def bn_ab(eng, dev):
@@ -207,6 +245,8 @@ def main():
     ap.add_argument("--dw0-ab", action="store_true", help="step: D0 weight-gradient tile 64 vs 128")
     ap.add_argument("--inlaunch-ab", action="store_true", help="split-K: epilogue launch vs in-launch reduction")
     ap.add_argument("--gwt-ab", action="store_true", help="step + generation: generator weights [out, in] vs input-major")
+    ap.add_argument("--cfg-ab", default=None, metavar="FIELD", help="step + generation: a boolean EngineConfig field off / on")
+    ap.add_argument("--fork-probe", action="store_true", help="step: cost of a forked side-stream branch in the graph")
     args = ap.parse_args()
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
@@ -219,8 +259,12 @@ def main():
     res = {}
     if args.step_only:
         return step_only(eng, dev)
+    if args.fork_probe:
+        return fork_probe(eng, dev)
     if args.gwt_ab:
         return gwt_ab(tr, X, dev, args.precision)
+    if args.cfg_ab:
+        return gwt_ab(tr, X, dev, args.precision, key=args.cfg_ab)
     if args.gen:
         return gen_only(eng, tr, X, dev)
     if args.onehot_ab:
