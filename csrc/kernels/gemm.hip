@@ -937,35 +937,81 @@ int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
 int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)
 int g_gemm_splitk_inlaunch = 1;   // 1: split-K reduced by the last-arriving slice (GemmArgs::tile_cnt)
 
+// the reduced, epilogue-applied value of output idx = m * N + n (stored to C by the caller)
 template <int SMAX>
-__device__ __forceinline__ void splitk_epilogue_body(const GemmArgs& g, int bid, int nblk) {
+__device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int m, int n, uint64_t step) {
   const int splits = g.splitk;
   const size_t total = (size_t)g.M * g.N;
-  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
-  for (size_t idx = (size_t)bid * blockDim.x + threadIdx.x; idx < total; idx += (size_t)nblk * blockDim.x) {
-    const int m = (int)(idx / g.N), n = (int)(idx % g.N);
-    float part[SMAX];
+  float part[SMAX];
 #pragma unroll
-    for (int z = 0; z < SMAX; ++z) part[z] = g.ws[(size_t)min(z, splits - 1) * total + idx];
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < SMAX; ++z) part[z] = g.ws[(size_t)min(z, splits - 1) * total + idx];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int z = 0; z < SMAX; ++z)
-      if (z < splits) acc[z & 3] += part[z];
-    float v = g.alpha * ((acc[0] + acc[1]) + (acc[2] + acc[3]));
-    float* cp = g.c + (size_t)m * g.ldc + n;
-    if (g.beta != 0.f) v += g.beta * (*cp);
-    if (g.bias) v += g.bias[n];
-    if (g.oh_w) v += onehot_term(g, m, n);
-    st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, idx), g.wt);
-  }
+  for (int z = 0; z < SMAX; ++z)
+    if (z < splits) acc[z & 3] += part[z];
+  float v = g.alpha * ((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  float* cp = g.c + (size_t)m * g.ldc + n;
+  if (g.beta != 0.f) v += g.beta * (*cp);
+  if (g.bias) v += g.bias[n];
+  if (g.oh_w) v += onehot_term(g, m, n);
+  return apply_epi(g, v, m, n, step, idx);
 }
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
-  splitk_epilogue_body<SMAX>(g, (int)blockIdx.x, (int)gridDim.x);
+  const size_t total = (size_t)g.M * g.N;
+  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(idx / g.N), n = (int)(idx % g.N);
+    st_out(g.c, (size_t)m * g.ldc + n, splitk_value<SMAX>(g, idx, m, n, step), g.wt);
+  }
 }
 
-
+// The discriminator's R chain, two links in one launch (GemmArgs::rc_out): R0 = epi(split-K sum)
+// (SMAX > 0; SMAX = 0: R0 is already in C) and the next link R1[m, :] = (R0[m, :] W1^T) * MS1[m, :] as
+// fp32 dot products.  Workgroup (m, s) reduces row m of R0 into LDS (s == 0 also stores it) and computes
+// R1[m, 64 s .. 64 s + 64): 64 outputs x 4 K-quarters per 256 threads, each thread reading 16-B chunks
+// of one W1 row.  As its own GEMM R1 (50 x 256 x 256) was a launch of its own.
+constexpr int RC_MAXK = 1024, RC_COLS = 64;
+template <int SMAX>
+__global__ __launch_bounds__(256) void rchain_epilogue_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float row[RC_MAXK];
+  __shared__ float part[4][RC_COLS];
+  const int m = blockIdx.x, s = blockIdx.y;
+  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
+    float v;
+    if constexpr (SMAX > 0) {
+      v = splitk_value<SMAX>(g, (size_t)m * g.N + n, m, n, step);
+      if (s == 0) st_out(g.c, (size_t)m * g.ldc + n, v, g.wt);
+    } else {
+      v = g.c[(size_t)m * g.ldc + n];
+    }
+    row[n] = v;
+  }
+  __syncthreads();
+  const int jl = threadIdx.x & (RC_COLS - 1), kq = threadIdx.x >> 6;
+  const int j = s * RC_COLS + jl;
+  const int q4 = g.N / 16;                       // float4 per K-quarter (host: N % 16 == 0)
+  float a0 = 0.f, a1 = 0.f;
+  if (j < g.rc_n1) {
+    const float4* w4 = reinterpret_cast<const float4*>(g.rc_w + (size_t)j * g.rc_ldw) + kq * q4;
+    const float4* r4 = reinterpret_cast<const float4*>(row) + kq * q4;
+#pragma unroll 4
+    for (int k = 0; k < q4; ++k) {
+      const float4 w = w4[k], x = r4[k];
+      a0 = fmaf(w.x, x.x, a0);
+      a1 = fmaf(w.y, x.y, a1);
+      a0 = fmaf(w.z, x.z, a0);
+      a1 = fmaf(w.w, x.w, a1);
+    }
+  }
+  part[kq][jl] = a0 + a1;
+  __syncthreads();
+  if (kq == 0 && j < g.rc_n1)
+    g.rc_out[(size_t)m * g.rc_ldo + j] =
+        ((part[0][jl] + part[1][jl]) + (part[2][jl] + part[3][jl])) * g.rc_ms[(size_t)m * g.rc_ldms + j];
+}
 
 // A weight-gradient GEMM and its optimizer's Adam in ONE launch: the first nt workgroups are the
 // GEMM's tiles, which apply Adam to their own outputs (gemm_tile<..., ADAM>); the rest run the
@@ -1058,6 +1104,15 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
 }
 
 static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
+  if (g.rc_out) {     // the next R-chain link rides on this GEMM's reduction launch (or follows it)
+    const dim3 grid(g.M, (g.rc_n1 + RC_COLS - 1) / RC_COLS), block(256);
+    if (g.splitk <= 1 || g.red_inl) hipLaunchKernelGGL(rchain_epilogue_kernel<0>, grid, block, 0, stream, g);
+    else if (g.splitk <= 8) hipLaunchKernelGGL(rchain_epilogue_kernel<8>, grid, block, 0, stream, g);
+    else if (g.splitk <= 16) hipLaunchKernelGGL(rchain_epilogue_kernel<16>, grid, block, 0, stream, g);
+    else if (g.splitk <= 32) hipLaunchKernelGGL(rchain_epilogue_kernel<32>, grid, block, 0, stream, g);
+    else hipLaunchKernelGGL(rchain_epilogue_kernel<64>, grid, block, 0, stream, g);
+    return;
+  }
   if (g.splitk <= 1 || g.red_inl) return;
   const size_t total = (size_t)g.M * g.N;
   int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);

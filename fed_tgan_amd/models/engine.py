@@ -106,6 +106,9 @@ class EngineConfig:
     # HIP: the generator's first-layer weight gradient (the step's last GEMM) runs in the same launch
     # as the generator's Adam, its tiles applying Adam to their own outputs (gemm_adam_kernel)
     fuse_g_adam: bool = True
+    # HIP, two hidden D layers: R1 = (R0 W1^T) * MS1 is computed in R0's split-K reduction launch, so
+    # D1's weight gradient is the last D GEMM and shares its launch with the D Adam (as fuse_g_adam)
+    fuse_d_adam: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -580,12 +583,22 @@ class CTGANEngine:
         inp = self.X[I]
         prev = self.X
         pair = self.lanes is None     # weight gradient + R product of a layer: one launch
+        # two hidden layers: R1 rides on R0's split-K reduction launch, and dW1 (then the last D GEMM)
+        # is held for the D Adam launch (gemm_adam_kernel)
+        fuse_d = pair and L == 2 and self.cfg.fuse_d_adam and getattr(o, "gemm_adam", False) and \
+            self.ddims[0] % 16 == 0 and self.ddims[0] <= 1024 and o.gemm_is_split(self.nP, self.ddims[0], self.K1)
         for i in range(L):
+            last_fused = fuse_d and i == L - 1
             with self._lane(1 + i % 2):
                 kw = {"tile": self.cfg.dw0_tile} if (i == 0 and self.cfg.dw0_tile and self.ops.name == "hip") else {}
-                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=1 if pair else 0, **kw)
+                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=3 if last_fused else (1 if pair else 0),
+                       **kw)
+            if last_fused:
+                break              # R_{L-1} was computed with R_{L-2}
+            rk = {"rchain": (self.p[f"D.{i + 1}.W"], self.ms[i + 1][I], self.dl[i + 1][I])} \
+                if (fuse_d and i == L - 2) else {}
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
-                   group=2 if pair else 0)
+                   group=2 if pair else 0, **rk)
             inp = self.dl[i][I]
             prev = self.dl[i]
         # (the column sums are folded into the Adam launch: those workgroups update the bias / head
