@@ -79,6 +79,16 @@ struct AdamHeld {
   bool active;
 };
 thread_local AdamHeld g_adam_held{};
+// a chain tail (gemm(..., group=4)) waiting for its head (gemm(..., chain=True)); the head's launch copies
+// the tail's arguments by value when it enqueues the reduction kernel
+struct ChainTail {
+  fedtgan::GemmArgs g;
+  const void* a;
+  int64_t M, K;
+  bool active;
+};
+thread_local ChainTail g_chain_tail{};
+thread_local fedtgan::GemmArgs g_chain_args{};
 
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
@@ -88,8 +98,7 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& head_v, const optional<Tensor>& head_a, int64_t tile, int64_t group,
           const optional<Tensor>& oh_w, const optional<Tensor>& oh_col, const optional<Tensor>& oh_opt,
           const optional<Tensor>& oh_off, bool oh_trans, const optional<Tensor>& bn_part, int64_t bn_rpg,
-          const optional<Tensor>& tile_cnt, const optional<Tensor>& rc_w, const optional<Tensor>& rc_ms,
-          const optional<Tensor>& rc_out) {
+          const optional<Tensor>& tile_cnt, bool chain) {
   const bool bin = a.scalar_type() == at::kBFloat16;
   const bool cbf = c.scalar_type() == at::kBFloat16;
   if (bin) {
@@ -207,26 +216,29 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
                     tile_cnt->numel() >= tiles, "gemm: tile_cnt must hold one int32 per output tile");
     g.tile_cnt = reinterpret_cast<unsigned*>(tile_cnt->data_ptr<int>());
   }
-  if (rc_out.has_value() && rc_out->defined()) {
-    // the next R-chain link computed in this GEMM's reduction launch (rchain_epilogue_kernel)
-    TORCH_CHECK(rc_w.has_value() && rc_w->defined() && rc_ms.has_value() && rc_ms->defined(), "gemm: rc_w / rc_ms");
-    check_f32_2d(*rc_w, "rc_w");
-    check_f32_2d(*rc_ms, "rc_ms");
-    check_f32_2d(*rc_out, "rc_out");
-    const int64_t n1 = rc_w->size(0);
-    TORCH_CHECK(!cbf && !bin && N <= 1024 && N % 16 == 0 && rc_w->size(1) == N && ld_of(*rc_w) % 4 == 0 &&
-                    (reinterpret_cast<uintptr_t>(rc_w->data_ptr()) & 15) == 0,
-                "gemm: the R-chain link needs fp32 C with N <= 1024, N % 16 == 0, and a 16-B aligned W [n1, N] "
-                "with ld % 4 == 0");
-    TORCH_CHECK(rc_ms->size(0) == M && rc_ms->size(1) == n1 && rc_out->size(0) == M && rc_out->size(1) == n1,
-                "gemm: rc_ms / rc_out must be [M, n1]");
-    g.rc_w = cfp(*rc_w);
-    g.rc_ldw = ld_of(*rc_w);
-    g.rc_n1 = (int)n1;
-    g.rc_ms = cfp(*rc_ms);
-    g.rc_ldms = ld_of(*rc_ms);
-    g.rc_out = fp(*rc_out);
-    g.rc_ldo = ld_of(*rc_out);
+  if (group == 4) {
+    // the tail of a chain (held for the next gemm(..., chain=True), whose output is this GEMM's A): its
+    // own epilogue, computed row by row in the head's reduction launch (chain_epilogue_kernel)
+    TORCH_CHECK(!g_chain_tail.active, "gemm: a chain tail is already held");
+    TORCH_CHECK(!ta && tb && !bin && !cbf && !g.oh_w && !g.bn_part && beta == 0.0 && K <= 1024 && K % 16 == 0 &&
+                    ld_of(b) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(b.data_ptr()) & 15) == 0,
+                "gemm: a chain tail is C = A B^T with fp32 16-B aligned B rows (ld % 4 == 0), K <= 1024, K % 16 == 0, "
+                "no one-hot block / BN partials");
+    g.splitk = 1;
+    g_chain_tail = ChainTail{g, a.data_ptr(), (int64_t)M, (int64_t)K, true};
+    return;
+  }
+  if (chain) {
+    TORCH_CHECK(g_chain_tail.active && group != 1, "gemm: chain=True needs a tail held with group=4 (and no group 1)");
+    const ChainTail& t = g_chain_tail;
+    TORCH_CHECK(t.a == c.data_ptr() && t.M == M && t.K == N && !cbf,
+                "gemm: the chain tail's A must be this GEMM's fp32 output (same rows, K = N)");
+    g_chain_args = t.g;
+    g_chain_tail.active = false;
+    g.chain = &g_chain_args;
+  } else {
+    TORCH_CHECK(!g_chain_tail.active || group == 1, "gemm: a chain tail is held; the next unpaired GEMM must be its head");
   }
   // group 1: hold this GEMM; group 2: launch it together with the held one (launch_gemm_pair: the two
   // must be independent -- neither reads what the other writes); group 3: hold it for the next
@@ -905,7 +917,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor? bn_gamma, Tensor? bn_beta, Tensor? bn_rm, Tensor? bn_rv, float bn_eps, bool f32, Tensor? head_coef, "
       "Tensor? head_v, Tensor(e!)? head_a, int tile, int group=0, Tensor? oh_w=None, Tensor? oh_col=None, "
       "Tensor? oh_opt=None, Tensor? oh_off=None, bool oh_trans=False, Tensor(f!)? bn_part=None, int bn_rpg=0, "
-      "Tensor(g!)? tile_cnt=None, Tensor? rc_w=None, Tensor? rc_ms=None, Tensor(h!)? rc_out=None) -> ()");
+      "Tensor(g!)? tile_cnt=None, bool chain=False) -> ()");
   m.def(
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "

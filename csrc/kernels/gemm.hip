@@ -967,16 +967,19 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
   }
 }
 
-// The discriminator's R chain, two links in one launch (GemmArgs::rc_out): R0 = epi(split-K sum)
-// (SMAX > 0; SMAX = 0: R0 is already in C) and the next link R1[m, :] = (R0[m, :] W1^T) * MS1[m, :] as
-// fp32 dot products.  Workgroup (m, s) reduces row m of R0 into LDS (s == 0 also stores it) and computes
-// R1[m, 64 s .. 64 s + 64): 64 outputs x 4 K-quarters per 256 threads, each thread reading 16-B chunks
-// of one W1 row.  As its own GEMM R1 (50 x 256 x 256) was a launch of its own.
-constexpr int RC_MAXK = 1024, RC_COLS = 64;
+// Two GEMMs of a chain in one launch (GemmArgs::chain): the head's output row m is final in its split-K
+// reduction (SMAX > 0; SMAX = 0: already in C), and the tail -- whose A operand is exactly that output,
+// C2[m, :] = epi2(C[m, :] B2^T + bias2) -- needs only that row.  Workgroup (m, s) reduces row m into LDS
+// (s == 0 also stores it) and forms C2[m, 64 s .. 64 s + 64): 64 outputs x 4 K-quarters per 256 threads,
+// each thread reading 16-B chunks of one B2 row, then the tail's epilogue (bias, LeakyReLU + Philox
+// dropout with the same mask indices as the GEMM epilogue, the D head's seed, or the mask product).
+// The discriminator's second layer (150 or 50 x 256 x 256) and its R-chain link R1 = (R0 W1^T) . MS1
+// were launches of their own after D0's / R0's reduction.
+constexpr int CH_MAXK = 1024, CH_COLS = 64;
 template <int SMAX>
-__global__ __launch_bounds__(256) void rchain_epilogue_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float row[RC_MAXK];
-  __shared__ float part[4][RC_COLS];
+__global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
+  __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
+  __shared__ float part[4][CH_COLS];
   const int m = blockIdx.x, s = blockIdx.y;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
@@ -990,12 +993,12 @@ __global__ __launch_bounds__(256) void rchain_epilogue_kernel(GemmArgs g) {
     row[n] = v;
   }
   __syncthreads();
-  const int jl = threadIdx.x & (RC_COLS - 1), kq = threadIdx.x >> 6;
-  const int j = s * RC_COLS + jl;
+  const int jl = threadIdx.x & (CH_COLS - 1), kq = threadIdx.x >> 6;
+  const int j = s * CH_COLS + jl;
   const int q4 = g.N / 16;                       // float4 per K-quarter (host: N % 16 == 0)
   float a0 = 0.f, a1 = 0.f;
-  if (j < g.rc_n1) {
-    const float4* w4 = reinterpret_cast<const float4*>(g.rc_w + (size_t)j * g.rc_ldw) + kq * q4;
+  if (j < t.N) {
+    const float4* w4 = reinterpret_cast<const float4*>(t.b + (size_t)j * t.ldb) + kq * q4;
     const float4* r4 = reinterpret_cast<const float4*>(row) + kq * q4;
 #pragma unroll 4
     for (int k = 0; k < q4; ++k) {
@@ -1008,9 +1011,12 @@ __global__ __launch_bounds__(256) void rchain_epilogue_kernel(GemmArgs g) {
   }
   part[kq][jl] = a0 + a1;
   __syncthreads();
-  if (kq == 0 && j < g.rc_n1)
-    g.rc_out[(size_t)m * g.rc_ldo + j] =
-        ((part[0][jl] + part[1][jl]) + (part[2][jl] + part[3][jl])) * g.rc_ms[(size_t)m * g.rc_ldms + j];
+  if (kq == 0 && j < t.N) {
+    float v = t.alpha * ((part[0][jl] + part[1][jl]) + (part[2][jl] + part[3][jl]));
+    if (t.bias) v += t.bias[j];
+    const uint64_t st = (t.epi == EPI_LRELU_DROPOUT && t.rng_ctr) ? *t.rng_ctr : 0ull;
+    t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+  }
 }
 
 // A weight-gradient GEMM and its optimizer's Adam in ONE launch: the first nt workgroups are the
@@ -1104,13 +1110,16 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
 }
 
 static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
-  if (g.rc_out) {     // the next R-chain link rides on this GEMM's reduction launch (or follows it)
-    const dim3 grid(g.M, (g.rc_n1 + RC_COLS - 1) / RC_COLS), block(256);
-    if (g.splitk <= 1 || g.red_inl) hipLaunchKernelGGL(rchain_epilogue_kernel<0>, grid, block, 0, stream, g);
-    else if (g.splitk <= 8) hipLaunchKernelGGL(rchain_epilogue_kernel<8>, grid, block, 0, stream, g);
-    else if (g.splitk <= 16) hipLaunchKernelGGL(rchain_epilogue_kernel<16>, grid, block, 0, stream, g);
-    else if (g.splitk <= 32) hipLaunchKernelGGL(rchain_epilogue_kernel<32>, grid, block, 0, stream, g);
-    else hipLaunchKernelGGL(rchain_epilogue_kernel<64>, grid, block, 0, stream, g);
+  if (g.chain) {     // the chained tail GEMM rides on this GEMM's reduction launch (or follows it)
+    GemmArgs h = g;
+    const GemmArgs t = *g.chain;
+    h.chain = nullptr;
+    const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS), block(256);
+    if (g.splitk <= 1 || g.red_inl) hipLaunchKernelGGL(chain_epilogue_kernel<0>, grid, block, 0, stream, h, t);
+    else if (g.splitk <= 8) hipLaunchKernelGGL(chain_epilogue_kernel<8>, grid, block, 0, stream, h, t);
+    else if (g.splitk <= 16) hipLaunchKernelGGL(chain_epilogue_kernel<16>, grid, block, 0, stream, h, t);
+    else if (g.splitk <= 32) hipLaunchKernelGGL(chain_epilogue_kernel<32>, grid, block, 0, stream, h, t);
+    else hipLaunchKernelGGL(chain_epilogue_kernel<64>, grid, block, 0, stream, h, t);
     return;
   }
   if (g.splitk <= 1 || g.red_inl) return;

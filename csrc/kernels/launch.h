@@ -84,12 +84,10 @@ struct GemmArgs {
   float* adam_v;
   const float* adam_step;
   float adam_lr, adam_b1, adam_b2, adam_eps, adam_wd;
-  // next R-chain link (nullable; rchain_epilogue_kernel): after this GEMM's output R0 [M, N] is final,
-  // rc_out[m, j] = (sum_k R0[m, k] rc_w[j, k]) * rc_ms[m, j] for j < rc_n1 (N <= 1024)
-  const float* rc_w;
-  const float* rc_ms;
-  float* rc_out;
-  int rc_ldw, rc_ldms, rc_ldo, rc_n1;
+  // chained GEMM (host-side pointer, nullable; chain_epilogue_kernel): once this GEMM's output C [M, N]
+  // is final, the tail C2 = epi2(C B2^T + bias2) (the tail's own GemmArgs: op(A2) = this C, row-local,
+  // K2 = N <= 1024) is computed in this GEMM's reduction launch, as fp32 dot products
+  const struct GemmArgs* chain;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);

@@ -109,6 +109,9 @@ class EngineConfig:
     # HIP, two hidden D layers: R1 = (R0 W1^T) * MS1 is computed in R0's split-K reduction launch, so
     # D1's weight gradient is the last D GEMM and shares its launch with the D Adam (as fuse_g_adam)
     fuse_d_adam: bool = True
+    # HIP, two hidden D layers: the second layer's forward is computed row by row in the first layer's
+    # split-K reduction launch (chain_epilogue_kernel)
+    chain_d1: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
@@ -484,15 +487,27 @@ class CTGANEngine:
         writes the head's backward seed A_{L-1} = coef * v * MS_{L-1} (no separate head launch;
         the head's WGAN value is folded into a later column-sum launch, see _wgan_job)."""
         o = self.ops
-        inp = (self.X if X is None else X)[rows]
+        Xs = self.X if X is None else X
+        inp = Xs[rows]
         L = len(self.ddims)
+        # two hidden layers: D1 (150 or 50 x 256 x 256) computed row by row in D0's split-K reduction launch
+        chain = L == 2 and self.cfg.chain_d1 and hasattr(o, "gemm_is_split") and self.ddims[0] % 16 == 0 and \
+            self.ddims[0] <= 1024 and o.gemm_is_split(inp.shape[0], self.ddims[0], inp.shape[1])
         for i in range(L):
             head = None
             if coef is not None and i == L - 1:
                 head = (coef, self.p["D.out.W"].view(-1), self.A[L - 1][rows])
+            kw = {"chain": True} if (chain and i == 0) else {}
+            if chain and i == 0:
+                h1 = (coef, self.p["D.out.W"].view(-1), self.A[1][rows]) if coef is not None else None
+                o.gemm(self.dl[0][rows], self.p["D.1.W"], self.dl[1][rows], tb=True, bias=self.p["D.1.b"],
+                       epi=EPI_LRELU_DROPOUT, ms=self.ms[1][rows], slope=self.cfg.lrelu_slope,
+                       p_drop=self.cfg.dropout_p, stream_id=stream_base + 1, head=h1, group=4)
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][rows], tb=True, bias=self.p[f"D.{i}.b"], epi=EPI_LRELU_DROPOUT,
                    ms=self.ms[i][rows], slope=self.cfg.lrelu_slope, p_drop=self.cfg.dropout_p,
-                   stream_id=stream_base + i, head=head)
+                   stream_id=stream_base + i, head=head, **kw)
+            if chain:
+                break
             inp = self.dl[i][rows]
 
     def _g_loss_metric(self):
@@ -595,8 +610,11 @@ class CTGANEngine:
                        **kw)
             if last_fused:
                 break              # R_{L-1} was computed with R_{L-2}
-            rk = {"rchain": (self.p[f"D.{i + 1}.W"], self.ms[i + 1][I], self.dl[i + 1][I])} \
-                if (fuse_d and i == L - 2) else {}
+            rk = {}
+            if fuse_d and i == L - 2:      # R_{i+1} = (R_i W_{i+1}^T) . MS_{i+1}, row by row in R_i's reduction
+                o.gemm(self.dl[i][I], self.p[f"D.{i + 1}.W"], self.dl[i + 1][I], tb=True, epi=EPI_MASK,
+                       ms=self.ms[i + 1][I], group=4)
+                rk = {"chain": True}
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
                    group=2 if pair else 0, **rk)
             inp = self.dl[i][I]

@@ -180,7 +180,7 @@ class HipOps:
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
              slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None,
-             bn_part=None, bn_rpg=0, tile=None, rchain=None):
+             bn_part=None, bn_rpg=0, tile=None, chain=False):
         """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
         onehot = (W_c [N, C], col [M], opt [M], cond_offset[, transposed]): A holds only the dense input
@@ -190,8 +190,9 @@ class HipOps:
         two must be independent); group 3 holds a weight gradient (plain epilogue, inside an optimizer's
         gradient buffer) for the next adam(..., jobs=...), which then runs both in ONE kernel, the GEMM's
         tiles applying Adam to their outputs; 0 launches now.
-        rchain = (W1 [n1, N], ms1 [M, n1], out1 [M, n1]): once C is final, out1 = (C W1^T) * ms1 in the
-        GEMM's split-K reduction launch (the discriminator's R chain, one link per launch saved).
+        group 4 holds a chain tail C2 = epi2(C B2^T + bias2) whose A operand is the output C of the next
+        gemm(..., chain=True): the tail is computed row by row (fp32 dots) in that GEMM's split-K
+        reduction launch (the discriminator's second layer and its R-chain link: one launch each saved).
         Transposed views (unit row stride, e.g. the input-major generator weights of EngineConfig.g_wt)
         are passed as their row-major storage with the transposition flag flipped; a transposed C is
         computed as C^T = op(B)^T op(A)^T (plain epilogue only)."""
@@ -199,7 +200,7 @@ class HipOps:
         b, tb = _rowmajor(b, tb)
         if _is_transposed(c):
             if bias is not None or epi != EPI_NONE or onehot is not None or head is not None or bn is not None \
-                    or bn_part is not None or rchain is not None:
+                    or bn_part is not None or chain:
                 raise ValueError("gemm: a transposed output takes no bias / epilogue / one-hot term")
             a, b, ta, tb, c = b, a, not tb, not ta, c.t()
         if onehot is not None and _is_transposed(onehot[0]):
@@ -226,7 +227,7 @@ class HipOps:
                     float(bn_eps), self.f32, *(head or (None, None, None)), int(tile), int(group),
                     *(onehot[:4] if onehot else (None, None, None, None)),
                     bool(onehot is not None and len(onehot) > 4 and onehot[4]), bn_part, int(bn_rpg), cnt,
-                    *(rchain or (None, None, None)))
+                    bool(chain))
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):
@@ -346,7 +347,7 @@ class HipOps:
 
     # ------------------------------------------------------------------ optimizer
     def gemm_is_split(self, M: int, N: int, K: int) -> bool:
-        """Does a GEMM of this shape get a split-K reduction launch (the launch an R-chain link rides on)?"""
+        """Does a GEMM of this shape get a split-K reduction launch (the launch a chain tail rides on)?"""
         kc = 64 if self.f32 else 128
         _, sk = _plan(M, N, K, kc)
         return _effective_splits(K, self.split_override or sk, kc) > 1 and not self.splitk_inlaunch

@@ -277,13 +277,14 @@ def test_input_major_generator_weights_match_row_major():
     assert np.allclose(la, lb, rtol=1e-3, atol=1e-4), (la, lb)
 
 
-@pytest.mark.parametrize("knob", ["fuse_g_adam", "fuse_d_adam"])
+@pytest.mark.parametrize("knob", ["fuse_g_adam", "fuse_d_adam", "chain_d1"])
 def test_fused_adam_launches_match_separate_launches(knob):
     """EngineConfig.fuse_g_adam: the generator's first-layer weight gradient and the generator's Adam
     in one launch (the GEMM's tiles update their own outputs) give the same gradients, parameters and
     moments as the separate launches (one Adam expression everywhere: bitwise).  fuse_d_adam: the same
     for D1's weight gradient and the D Adam, with R1 computed in fp32 in R0's reduction launch (instead
-    of a bf16-operand GEMM): close, not bitwise."""
+    of a bf16-operand GEMM): close, not bitwise.  chain_d1: D1's forward in D0's reduction launch (fp32,
+    the same Philox dropout masks): close."""
     from fed_tgan_amd.ops import native
     native.require()
     _, _, _, _, _, _, tr, X = small_table()
@@ -306,8 +307,8 @@ def test_fused_adam_launches_match_separate_launches(knob):
     else:
         I = a.rows_i
         assert _rel(b.dl[1][I], a.dl[1][I]) < 1e-2            # R1: fp32 dot products vs bf16 MFMA
-        for n in ("D.0.W", "D.1.W", "D.out.W", "D.0.b", "D.1.b"):
-            assert _rel(b.g[n], a.g[n]) < 2e-2, (n, _rel(b.g[n], a.g[n]))
+        for n in ("D.0.W", "D.1.W", "D.out.W", "D.0.b", "D.1.b"):    # bf16-operand GEMM tolerance (TOL)
+            assert _rel(b.g[n], a.g[n]) < TOL["bf16"], (n, _rel(b.g[n], a.g[n]))
         assert torch.equal(a.g["D.0.W"][:, :0], b.g["D.0.W"][:, :0])
         assert (a.flat - b.flat).abs().max() <= 2 * a.cfg.lr + 1e-6
     for e in engs:
