@@ -114,7 +114,6 @@ def launch(n: int, argv) -> int:
 
 # ----------------------------------------------------------------------------- one rank
 def run_rank(args) -> None:
-    import numpy as np
     import torch
 
     from fed_tgan_amd.data.schema import intrusion_spec

@@ -90,6 +90,19 @@ struct ChainTail {
 thread_local ChainTail g_chain_tail{};
 thread_local fedtgan::GemmArgs g_chain_args{};
 
+// drop every GEMM held by this thread (pairing, chain tail, Adam fusion) without launching it: called at
+// the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
+// (whose operand pointers may since have been freed) can never be launched or block the next step.
+// Returns the number of holds that were dropped.
+int64_t reset_held() {
+  const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0);
+  has_held = false;
+  held_stream = nullptr;
+  g_adam_held.active = false;
+  g_chain_tail.active = false;
+  return n;
+}
+
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
@@ -707,18 +720,49 @@ void rng_bump(const Tensor& ctr) {
 }
 
 void write_csv(const std::string& path, const Tensor& values, std::vector<std::string> names, std::vector<int64_t> kinds,
-               std::vector<std::string> vocab_flat, std::vector<int64_t> vocab_offsets, int64_t threads) {
+               std::vector<std::string> vocab_flat, std::vector<int64_t> vocab_offsets, int64_t threads,
+               std::vector<int64_t> src, std::vector<int64_t> date_desc, std::vector<int64_t> date_lut) {
+  // output column j: kinds[j], names[j], vocabulary vocab_flat[vocab_offsets[j], vocab_offsets[j + 1]), source
+  // column src[j] of values (default j).  Date columns (kind 3) take their description from date_desc, in
+  // output order: [mode, n_parts, (src, elem, lut_off, lut_len) x n_parts], code -> value tables in date_lut.
   TORCH_CHECK(!values.is_cuda() && values.scalar_type() == at::kDouble && values.is_contiguous() && values.dim() == 2,
               "write_csv: values must be a contiguous CPU float64 matrix");
   const int64_t cols = values.size(1);
-  TORCH_CHECK((int64_t)kinds.size() == cols && (int64_t)names.size() == cols &&
-                  (int64_t)vocab_offsets.size() == cols + 1,
+  const int64_t n_out = (int64_t)kinds.size();
+  TORCH_CHECK((int64_t)names.size() == n_out && (int64_t)vocab_offsets.size() == n_out + 1 &&
+                  (src.empty() ? n_out == cols : (int64_t)src.size() == n_out),
               "write_csv: descriptors");
-  std::vector<int> k(kinds.begin(), kinds.end());
-  std::vector<std::vector<std::string>> voc((size_t)cols);
-  for (int64_t j = 0; j < cols; ++j)
-    voc[(size_t)j].assign(vocab_flat.begin() + vocab_offsets[(size_t)j], vocab_flat.begin() + vocab_offsets[(size_t)j + 1]);
-  fedtgan::write_csv_file(path, values.data_ptr<double>(), values.size(0), cols, names, k, voc, (int)threads);
+  std::vector<fedtgan::CsvColumn> out((size_t)n_out);
+  size_t dp = 0;
+  for (int64_t j = 0; j < n_out; ++j) {
+    auto& c = out[(size_t)j];
+    c.kind = (int)kinds[(size_t)j];
+    TORCH_CHECK(c.kind >= fedtgan::CSV_FLOAT && c.kind <= fedtgan::CSV_DATE, "write_csv: kind");
+    c.src = (int)(src.empty() ? j : src[(size_t)j]);
+    TORCH_CHECK(vocab_offsets[(size_t)j] <= vocab_offsets[(size_t)j + 1] &&
+                    vocab_offsets[(size_t)j + 1] <= (int64_t)vocab_flat.size(), "write_csv: vocab offsets");
+    c.vocab.assign(vocab_flat.begin() + vocab_offsets[(size_t)j], vocab_flat.begin() + vocab_offsets[(size_t)j + 1]);
+    if (c.kind != fedtgan::CSV_DATE) {
+      TORCH_CHECK(c.src >= 0 && c.src < cols, "write_csv: source column out of range");
+      continue;
+    }
+    TORCH_CHECK(dp + 2 <= date_desc.size(), "write_csv: date_desc too short");
+    c.date_mode = (int)date_desc[dp++];
+    const int64_t np = date_desc[dp++];
+    TORCH_CHECK(np >= 1 && np <= 6 && dp + 4 * (size_t)np <= date_desc.size(), "write_csv: date parts");
+    for (int64_t q = 0; q < np; ++q) {
+      fedtgan::CsvDatePart part;
+      part.src = (int)date_desc[dp++];
+      part.elem = (int)date_desc[dp++];
+      const int64_t off = date_desc[dp++], len = date_desc[dp++];
+      TORCH_CHECK(part.src >= 0 && part.src < cols && part.elem >= 0 && part.elem <= 5 && off >= 0 && len >= 0 &&
+                      off + len <= (int64_t)date_lut.size(), "write_csv: date part descriptor");
+      part.lut.assign(date_lut.begin() + off, date_lut.begin() + off + len);
+      c.parts.push_back(std::move(part));
+    }
+  }
+  TORCH_CHECK(dp == date_desc.size(), "write_csv: unused date_desc entries");
+  fedtgan::write_csv_columns(path, values.data_ptr<double>(), values.size(0), cols, names, out, (int)threads);
 }
 
 void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Tensor& col_kind, const Tensor& col_pos,
@@ -973,9 +1017,10 @@ TORCH_LIBRARY(fedtgan, m) {
       "int stream) -> ()");
   m.def(
       "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
-      "int threads) -> ()");
+      "int threads, int[] src=[], int[] date_desc=[], int[] date_lut=[]) -> ()");
   m.def("py_float(float x) -> str", &py_float);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
+  m.def("reset_held() -> int", &reset_held);
   m.def("check_status() -> int", &check_status);
   m.def("is_checked() -> bool", &is_checked);
 }

@@ -8,6 +8,11 @@
 //   * categoricals: vocabulary string of the integer code (QUOTE_MINIMAL quoting)
 //   * non-negative columns: the caller maps v = exp(x) - 1 (ceil when v < 0) with numpy's exp --
 //     libm's exp differs from numpy's in the last ulp for some inputs -- and v == -1 is written " "
+//   * date columns (`Server/dtds/data/utils/transform.py:51-52`, `date.py:113-200`): re-joined from their
+//     categorical part columns (year / month / day / hour / minute / second codes -> values through
+//     per-part tables), impossible days repaired as the reference does, and printed the way pandas
+//     prints the re-joined column (date only, full timestamp, or the yymmdd integer; see
+//     resolve_date_styles)
 // Rows are formatted in parallel by worker threads, in row chunks handed out in order, and the
 // calling thread writes each chunk as soon as it is formatted (the file write overlaps the
 // formatting of the later chunks instead of following all of it).
@@ -118,55 +123,179 @@ void append_field(std::string& out, const std::string& s) { out += quote_field(s
 
 }  // namespace
 
+namespace {
+
+// Python's strptime %y: 69..99 -> 1969..1999, 0..68 -> 2000..2068
+int year_of_y2(int y2) { return y2 < 69 ? 2000 + y2 : 1900 + y2; }
+
+// one date column's fields for a row; false when any part is "empty" (the whole field is then " ")
+struct DateFields {
+  int y2 = -1, year = 1900, month = 1, day = 1, hour = 0, minute = 0, second = 0;
+};
+
+bool date_fields(const double* row, const CsvColumn& c, DateFields& f) {
+  int v[6] = {-1, -1, -1, -1, -1, -1};
+  for (const auto& p : c.parts) {
+    const int64_t code = (int64_t)row[p.src];
+    if (code < 0 || code >= (int64_t)p.lut.size()) throw std::runtime_error("csv: date part code out of range");
+    const int x = p.lut[(size_t)code];
+    if (x < 0) return false;
+    v[p.elem] = x;
+  }
+  if (v[0] >= 0) {
+    f.y2 = v[0];
+    f.year = year_of_y2(v[0]);
+  }
+  if (v[1] >= 0) f.month = v[1];
+  if (v[2] >= 0) f.day = v[2];
+  if (v[3] >= 0) f.hour = v[3];
+  if (v[4] >= 0) f.minute = v[4];
+  if (v[5] >= 0) f.second = v[5];
+  // impossible days (`Server/dtds/data/utils/date.py:113-200`, the reference's leap rule on the two-digit
+  // year: only "00" keeps February 29); applied when the first three parts are year, month, day
+  if (c.parts.size() >= 3 && v[0] >= 0 && v[1] >= 0 && v[2] >= 0) {
+    static const int dim[13] = {0, 31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    if (f.month < 1 || f.month > 12) throw std::runtime_error("csv: date month out of range");
+    if (f.day > dim[f.month]) {
+      if (f.month == 2) f.day = (f.y2 % 4 == 0 && f.y2 % 100 == 0 && f.y2 % 400 == 0) ? 29 : 28;
+      else f.day = 30;
+    }
+  }
+  return true;
+}
+
+char* put_2(char* p, int x) {
+  *p++ = (char)('0' + (x / 10) % 10);
+  *p++ = (char)('0' + x % 10);
+  return p;
+}
+
+char* put_date(char* p, const DateFields& f, int style) {
+  if (style == DATE_STYLE_YYMMDD) {   // int(ts.strftime("%y%m%d"))
+    const auto r = std::to_chars(p, p + 12, (f.year % 100) * 10000 + f.month * 100 + f.day);
+    return r.ptr;
+  }
+  const auto r = std::to_chars(p, p + 6, f.year);
+  p = r.ptr;
+  *p++ = '-';
+  p = put_2(p, f.month);
+  *p++ = '-';
+  p = put_2(p, f.day);
+  if (style == DATE_STYLE_FULL) {
+    *p++ = ' ';
+    p = put_2(p, f.hour);
+    *p++ = ':';
+    p = put_2(p, f.minute);
+    *p++ = ':';
+    p = put_2(p, f.second);
+  }
+  return p;
+}
+
+}  // namespace
+
 // Rows [r0, r1) into one string.  Every vocabulary entry is quoted once up front and each row is
 // written through a raw pointer into a buffer sized for its worst case (26 bytes per number), so the
 // hot loop does no allocation, no searching and no growing appends.
-std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, int64_t r0, int64_t r1,
-                            const std::vector<int>& kinds, const std::vector<std::vector<std::string>>& vocabs) {
-  (void)rows;
-  std::vector<std::vector<std::string>> qv(vocabs.size());
+std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, int64_t r1,
+                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style) {
+  std::vector<std::vector<std::string>> qv(out.size());
   size_t row_max = 1;
-  for (int64_t j = 0; j < cols; ++j) {
+  for (size_t j = 0; j < out.size(); ++j) {
+    const CsvColumn& c = out[j];
+    if (c.kind != CSV_DATE && (c.src < 0 || c.src >= cols)) throw std::runtime_error("csv: source column out of range");
     size_t w = 26;
-    if (kinds[(size_t)j] == 1) {
+    if (c.kind == CSV_VOCAB) {
       w = 0;
-      for (const auto& e : vocabs[(size_t)j]) {
-        qv[(size_t)j].push_back(quote_field(e));
-        w = std::max(w, qv[(size_t)j].back().size());
+      for (const auto& e : c.vocab) {
+        qv[j].push_back(quote_field(e));
+        w = std::max(w, qv[j].back().size());
       }
+    } else if (c.kind == CSV_DATE) {
+      for (const auto& p : c.parts)
+        if (p.src < 0 || p.src >= cols || p.elem < 0 || p.elem > 5) throw std::runtime_error("csv: date part");
+      w = 32;
     }
     row_max += w + 1;
   }
-  std::string out;
-  out.resize((size_t)(r1 - r0) * row_max);
-  char* p = &out[0];
+  std::string s;
+  s.resize((size_t)(r1 - r0) * row_max);
+  char* p = &s[0];
   for (int64_t r = r0; r < r1; ++r) {
     const double* row = values + r * cols;
-    for (int64_t j = 0; j < cols; ++j) {
+    for (size_t j = 0; j < out.size(); ++j) {
       if (j) *p++ = ',';
-      const double x = row[j];
-      switch (kinds[(size_t)j]) {
-        case 1: {  // vocabulary
-          const auto& voc = qv[(size_t)j];
-          const int64_t k = (int64_t)x;
+      const CsvColumn& c = out[j];
+      switch (c.kind) {
+        case CSV_VOCAB: {
+          const auto& voc = qv[j];
+          const int64_t k = (int64_t)row[c.src];
           if (k < 0 || k >= (int64_t)voc.size()) throw std::runtime_error("csv: category code out of range");
           const std::string& f = voc[(size_t)k];
           std::memcpy(p, f.data(), f.size());
           p += f.size();
           break;
         }
-        case 2:    // non-negative column, already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
+        case CSV_NONNEG: {   // already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
+          const double x = row[c.src];
           if (x == -1.0) *p++ = ' ';
           else p = put_py_float(p, x);
           break;
+        }
+        case CSV_DATE: {
+          DateFields f;
+          if (date_fields(row, c, f)) p = put_date(p, f, date_style[j]);
+          else *p++ = ' ';
+          break;
+        }
         default:
-          p = put_py_float(p, x);
+          p = put_py_float(p, row[c.src]);
       }
     }
     *p++ = '\n';
   }
-  out.resize((size_t)(p - out.data()));
+  s.resize((size_t)(p - s.data()));
+  return s;
+}
+
+std::vector<int> resolve_date_styles(const double* values, int64_t rows, int64_t cols, const std::vector<CsvColumn>& out) {
+  // pandas writes the re-joined column by its dtype, which depends on the whole column: with any "empty"
+  // row it is an object column of Timestamps (str(): "YYYY-MM-DD HH:MM:SS"); otherwise datetime64, printed
+  // date-only when every time of day is midnight.  The yymmdd form is an integer either way.
+  std::vector<int> style(out.size(), DATE_STYLE_DAY);
+  for (size_t j = 0; j < out.size(); ++j) {
+    const CsvColumn& c = out[j];
+    if (c.kind != CSV_DATE) continue;
+    if (c.date_mode == 1) {
+      style[j] = DATE_STYLE_YYMMDD;
+      continue;
+    }
+    bool any_empty = false, any_time = false;
+    for (int64_t r = 0; r < rows && !any_empty; ++r) {
+      DateFields f;
+      if (!date_fields(values + r * cols, c, f)) any_empty = true;
+      else if (f.hour || f.minute || f.second) any_time = true;
+    }
+    style[j] = (any_empty || any_time) ? DATE_STYLE_FULL : DATE_STYLE_DAY;
+  }
+  return style;
+}
+
+std::vector<CsvColumn> simple_columns(int64_t cols, const std::vector<int>& kinds,
+                                      const std::vector<std::vector<std::string>>& vocabs) {
+  std::vector<CsvColumn> out((size_t)cols);
+  for (int64_t j = 0; j < cols; ++j) {
+    out[(size_t)j].kind = kinds[(size_t)j];
+    out[(size_t)j].src = (int)j;
+    out[(size_t)j].vocab = vocabs[(size_t)j];
+  }
   return out;
+}
+
+std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, int64_t r0, int64_t r1,
+                            const std::vector<int>& kinds, const std::vector<std::vector<std::string>>& vocabs) {
+  const auto out = simple_columns(cols, kinds, vocabs);
+  return format_csv_columns(values, cols, r0, r1, out, resolve_date_styles(values, rows, cols, out));
 }
 
 std::string format_py_float(double x) {
@@ -175,11 +304,10 @@ std::string format_py_float(double x) {
   return s;
 }
 
-void write_csv_file(const std::string& path, const double* values, int64_t rows, int64_t cols,
-                    const std::vector<std::string>& names, const std::vector<int>& kinds,
-                    const std::vector<std::vector<std::string>>& vocabs, int threads) {
-  if ((int64_t)kinds.size() != cols || (int64_t)names.size() != cols || (int64_t)vocabs.size() != cols)
-    throw std::runtime_error("csv: column descriptor size mismatch");
+void write_csv_columns(const std::string& path, const double* values, int64_t rows, int64_t cols,
+                       const std::vector<std::string>& names, const std::vector<CsvColumn>& out, int threads) {
+  if (names.size() != out.size()) throw std::runtime_error("csv: column descriptor size mismatch");
+  const std::vector<int> style = resolve_date_styles(values, rows, cols, out);
   if (threads <= 0) {
     unsigned hc = std::thread::hardware_concurrency();
     threads = (int)std::min<unsigned>(hc ? hc : 4, 16);
@@ -202,7 +330,7 @@ void write_csv_file(const std::string& path, const double* values, int64_t rows,
       for (int c = next.fetch_add(1); c < nchunks; c = next.fetch_add(1)) {
         try {
           const int64_t r0 = (int64_t)c * chunk, r1 = std::min(rows, r0 + chunk);
-          parts[(size_t)c] = format_csv_rows(values, rows, cols, r0, r1, kinds, vocabs);
+          parts[(size_t)c] = format_csv_columns(values, cols, r0, r1, out, style);
           ready[(size_t)c].set_value();
         } catch (...) {
           ready[(size_t)c].set_exception(std::current_exception());
@@ -211,27 +339,41 @@ void write_csv_file(const std::string& path, const double* values, int64_t rows,
     });
   }
   std::string header;
-  for (int64_t j = 0; j < cols; ++j) {
+  for (size_t j = 0; j < names.size(); ++j) {
     if (j) header.push_back(',');
-    append_field(header, names[(size_t)j]);
+    append_field(header, names[j]);
   }
   header.push_back('\n');
   FILE* f = std::fopen(path.c_str(), "wb");
   std::exception_ptr err;
+  // a short write (full disk, I/O error) or a failed close is an error like a formatting failure: the
+  // caller must not record a truncated table as written
+  auto put = [&](const std::string& b) {
+    if (f && !err && std::fwrite(b.data(), 1, b.size(), f) != b.size())
+      err = std::make_exception_ptr(std::runtime_error("csv: short write to " + path));
+  };
   if (!f) err = std::make_exception_ptr(std::runtime_error("csv: cannot open " + path));
-  else std::fwrite(header.data(), 1, header.size(), f);
+  else put(header);
   for (int c = 0; c < nchunks; ++c) {
     try {
       done[(size_t)c].get();
     } catch (...) {
       if (!err) err = std::current_exception();
     }
-    if (f && !err) std::fwrite(parts[(size_t)c].data(), 1, parts[(size_t)c].size(), f);
+    put(parts[(size_t)c]);
     std::string().swap(parts[(size_t)c]);
   }
   for (auto& th : pool) th.join();
-  if (f) std::fclose(f);
+  if (f && std::fclose(f) != 0 && !err) err = std::make_exception_ptr(std::runtime_error("csv: close failed for " + path));
   if (err) std::rethrow_exception(err);
+}
+
+void write_csv_file(const std::string& path, const double* values, int64_t rows, int64_t cols,
+                    const std::vector<std::string>& names, const std::vector<int>& kinds,
+                    const std::vector<std::vector<std::string>>& vocabs, int threads) {
+  if ((int64_t)kinds.size() != cols || (int64_t)names.size() != cols || (int64_t)vocabs.size() != cols)
+    throw std::runtime_error("csv: column descriptor size mismatch");
+  write_csv_columns(path, values, rows, cols, names, simple_columns(cols, kinds, vocabs), threads);
 }
 
 }  // namespace fedtgan

@@ -21,7 +21,8 @@ New flags: -config (dataset spec JSON or builtin name), -backend {auto,hip,torch
 -precision {bf16,fp32}, -data_backend {auto,gloo,nccl}, -synthetic_rows, -shard
 {independent,iid,dirichlet,skew}, -alpha, -n_sample, -aggregation {weighted,uniform}, -gmm
 {torch,sklearn}, -seed, -out_dir, -ckpt_every, -resume, -local_clients K (K clients per process,
-as threads sharing its GPU; with -world_size N: N*K clients over N ranks), -drop_client_prob (fault injection), -metrics_log, -mode {fedavg,mdgan},
+as threads sharing its GPU; with -world_size N: N*K clients over N ranks), -drop_client_prob (fault
+injection), -metrics_log, -mode {fedavg,mdgan},
 -init {independent,broadcast} (initial weights; independent = the reference's per-client init).
 """
 from __future__ import annotations

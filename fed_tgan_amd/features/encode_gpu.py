@@ -131,7 +131,7 @@ def encode_on_device(tr: VGMTransformer, data: np.ndarray, device, seed: int = 0
     lay = tr.layout
     out = torch.zeros(n, lay.data_dim, dtype=torch.float32, device=device)
     opt = torch.zeros(n, lay.n_col, dtype=torch.int32, device=device)
-    L.vgm_encode(x, out, opt, t["kind"], t["pos"], t["aux"], t["span"], t["lut_n"], t["consts"], t["means"], t["prec"], t["stds"],
-                 t["vrank"], t["lut"], int(seed) & ((1 << 62) - 1), 41)
+    L.vgm_encode(x, out, opt, t["kind"], t["pos"], t["aux"], t["span"], t["lut_n"], t["consts"], t["means"], t["prec"],
+                 t["stds"], t["vrank"], t["lut"], int(seed) & ((1 << 62) - 1), 41)
     rows, counts = row_index_on_device(opt, lay)
     return DeviceEncoded(out, opt, counts, rows)

@@ -42,10 +42,10 @@ import pandas as pd
 import torch
 
 from ..data.constants import CATEGORICAL
-from ..data.decode import csv_columns, decode_frame, meta_column_names
+from ..data.decode import csv_layout, decode_frame
 from ..data.schema import DatasetSpec
 from ..data.synthetic import generate, shard
-from ..data.table import TablePreprocessor, dump_meta_json, load_table
+from ..data.table import TablePreprocessor, dump_meta_json
 from ..data.vocab import CategoryVocab
 from ..features.gmm import VGMBank, fit_vgm
 from ..features.transformer import VGMTransformer
@@ -53,9 +53,8 @@ from ..models.engine import CTGANEngine, EngineConfig
 from ..models.samplers import CondTables
 from ..parallel.comm import Comm
 from ..utils.metrics import MetricsLog, PhaseTimer
-from ..utils.devsync import PendingHost, device_sync, stream_sync
-from .stats import (aggregation_weights, continuous_client_distances, merge_categorical_metas,
-                    normalise_over_clients, uniform_weights, wasserstein_1d)
+from ..utils.devsync import PendingHost, stream_sync
+from .stats import aggregation_weights, continuous_client_distances, merge_categorical_metas, uniform_weights
 
 
 @dataclasses.dataclass
@@ -293,7 +292,7 @@ class FedRuntime:
         self.steps = [n // cfg.engine.batch_size for n in self.rows]
         if cfg.resume:
             self.load_checkpoint()
-        self.csv_cols = csv_columns(merged, self.vocabs) if not spec.date_dic else None
+        self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
         c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
@@ -436,8 +435,7 @@ class FedRuntime:
         if use_native:
             from ..utils import csvio
             if csvio.available() or self.cfg.csv_writer == "native":
-                names, kinds, vocab_lists = self.csv_cols
-                csvio.write_table(path, values, names, kinds, vocab_lists, threads=self.cfg.csv_threads)
+                csvio.write_layout(path, values, self.csv_cols, threads=self.cfg.csv_threads)
                 return path
         decode_frame(values, self.global_meta, self.vocabs).to_csv(path, index=False)
         return path

@@ -38,7 +38,7 @@ from __future__ import annotations
 
 import contextlib
 import dataclasses
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Tuple
 
 import numpy as np
 import torch
@@ -751,6 +751,16 @@ class CTGANEngine:
     def _one_step(self):
         if hasattr(self.ops, "begin_step"):
             self.ops.begin_step(self)
+        try:
+            self._issue_step()
+        except BaseException:
+            # a raise between a held GEMM (ops.gemm group 1/3/4) and its consumer must not leave the hold
+            # behind for the next step on this thread
+            if hasattr(self.ops, "reset_held"):
+                self.ops.reset_held()
+            raise
+
+    def _issue_step(self):
         if self.lanes is None and self.cfg.paired:
             # both batches drawn and generated up front (G is unchanged by the D update)
             self._prepare_paired()

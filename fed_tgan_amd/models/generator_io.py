@@ -24,7 +24,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..data.decode import csv_columns, decode_frame
+from ..data.decode import csv_layout, decode_frame
 from ..data.vocab import CategoryVocab
 from ..features.transformer import VGMTransformer
 from .engine import CTGANEngine, EngineConfig
@@ -73,11 +73,11 @@ class LoadedGenerator:
 
     def write_csv(self, path: str, n: int, threads: int = 0) -> str:
         vals = self.sample(n)
-        if not self.meta.get("date_info"):
+        lay = csv_layout(self.meta, self.vocabs)
+        if lay is not None:
             from ..utils import csvio
             if csvio.available():
-                names, kinds, vocab_lists = csv_columns(self.meta, self.vocabs)
-                csvio.write_table(path, vals, names, kinds, vocab_lists, threads=threads)
+                csvio.write_layout(path, vals, lay, threads=threads)
                 return path
         decode_frame(vals, self.meta, self.vocabs).to_csv(path, index=False)
         return path

@@ -112,6 +112,20 @@ class HipOps:
         self._bnp: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ helpers
+    def reset_held(self) -> int:
+        """Drop every GEMM this thread holds for pairing / a chain / the Adam launch (see gemm's
+        ``group``), unlaunched; returns how many there were."""
+        return int(self.L.reset_held())
+
+    def begin_step(self, engine) -> None:
+        """A step starts with no GEMM held: a previous step that raised between a hold and its consumer
+        leaves nothing behind (a stale hold would refuse every later GEMM, or be launched with operand
+        pointers that no longer belong to it)."""
+        n = self.reset_held()
+        if n:
+            import warnings
+            warnings.warn(f"dropped {n} GEMM hold(s) left by an interrupted step", RuntimeWarning)
+
     def check(self) -> None:
         """Checked native build (FEDTGAN_CHECKED=1): raise if a kernel flagged an out-of-range table
         index since the last check (synchronises).  Release build: nothing."""

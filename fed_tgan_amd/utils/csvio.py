@@ -5,16 +5,16 @@ pandas ``Transform.inverse`` pass (`Server/dtds/distributed.py:584-590`), ~1.1 s
 the survey box.  The native path formats the numeric decode output directly in C++
 (``csrc/host/csv_writer.cpp``: Python-``repr``-compatible shortest round-trip floats, vocab
 lookups for categoricals, the non-negative ``exp(x)-1`` / ceil rule, multi-threaded over
-row blocks) and writes the file in one call.  Byte-for-byte the output equals the pandas
-path for tables without date columns (tested).
+row blocks, date columns re-joined from their part codes) and writes the file in one call.
+Byte-for-byte the output equals the pandas path (tested, date schemas included).
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import Sequence
 
 import numpy as np
 
-from ..data.decode import KIND_FLOAT, KIND_NONNEG, KIND_VOCAB
+from ..data.decode import KIND_FLOAT, KIND_NONNEG, KIND_VOCAB, CsvLayout
 
 
 def _native():
@@ -64,21 +64,34 @@ def _quote(s: str) -> str:
 
 def write_table(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
                 vocabs: Sequence[Sequence[str]], threads: int = 0) -> None:
+    """One output column per value column (kinds 0..2)."""
+    write_layout(path, values, CsvLayout(list(names), list(kinds), [list(v) for v in vocabs], list(range(len(kinds)))),
+                 threads)
+
+
+def write_layout(path: str, values: np.ndarray, layout: CsvLayout, threads: int = 0) -> None:
+    """Write the decoded value matrix as ``layout`` (``data.decode.csv_layout``) describes it."""
     values = np.array(values, dtype=np.float64, copy=True)
-    for j, k in enumerate(kinds):
+    for j, k in enumerate(layout.kinds):
         if k == KIND_NONNEG:     # exp(x)-1 with numpy's exp (bit-identical to the pandas path)
-            w = np.exp(values[:, j]) - 1.0
+            c = layout.src[j]
+            w = np.exp(values[:, c]) - 1.0
             neg = w < 0
             w[neg] = np.ceil(w[neg])
-            values[:, j] = w
+            values[:, c] = w
     lib = _native()
     if lib is not None:
         from ..ops import native
-        native.write_csv(path, values, names, kinds, vocabs, threads)
+        native.write_csv(path, values, layout.names, layout.kinds, layout.vocabs, threads, layout.src,
+                         layout.date_desc, layout.date_lut)
         return
-    kinds_py = [KIND_FLOAT if k == KIND_NONNEG else k for k in kinds]
+    if layout.has_dates:
+        raise RuntimeError("the Python CSV formatter has no date columns (native library not loaded)")
+    vals = values[:, layout.src]
+    kinds_py = [KIND_FLOAT if k == KIND_NONNEG else k for k in layout.kinds]
     with open(path, "wb") as f:
-        f.write(format_table_py(values, names, kinds_py, vocabs, empty_minus_one=[k == KIND_NONNEG for k in kinds]))
+        f.write(format_table_py(vals, layout.names, kinds_py, layout.vocabs,
+                                empty_minus_one=[k == KIND_NONNEG for k in layout.kinds]))
 
 
 class AsyncTableWriter:

@@ -12,7 +12,6 @@ import json
 import time
 from typing import Dict
 
-import torch
 from .devsync import stream_sync
 
 

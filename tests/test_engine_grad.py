@@ -6,7 +6,6 @@ with torch autograd in float64-free fp32, using the exact random draws the engin
 (recorded Gumbel noise and slerp output; dropout keep-masks recovered from the saved
 mask*slope buffers).
 """
-import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F

@@ -1,6 +1,5 @@
 """VGM banks, the VGM transformer, samplers and the alternative transformers."""
 import numpy as np
-import pytest
 from sklearn.mixture import BayesianGaussianMixture
 
 from fed_tgan_amd.features.alt_transformers import (DiscretizeTransformer, GeneralTransformer, GMMTransformer,

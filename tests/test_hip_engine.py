@@ -320,3 +320,33 @@ def test_fused_adam_launches_match_separate_launches(knob):
         e.train_steps(8, use_graph=True)
     torch.cuda.synchronize()
     assert np.isfinite(b.losses()).all() and bool(torch.isfinite(b.flat).all())
+
+
+def test_interrupted_hold_does_not_poison_next_step():
+    """a raise between gemm(group=3 / 4 / 1) and its consumer must not leave the hold behind."""
+    eng, _ = _engine()
+    eng.train_steps(1, use_graph=False)
+    o = eng.ops
+    # hold a weight gradient for the Adam launch and a chain tail, then "fail" before their consumers
+    g0 = eng.gdims[0]
+    o.gemm(eng.da[0], eng.H[:, :g0], torch.zeros(g0, g0, device=DEV), ta=True, group=3)
+    with pytest.raises(RuntimeError):
+        o.gemm(eng.A[0], eng.X, eng.g["D.0.W"], ta=True, group=3)     # a second hold is refused
+    assert o.reset_held() == 1
+    assert o.reset_held() == 0
+
+    def boom(*a, **k):
+        raise RuntimeError("injected failure after the hold")
+    real_adam = o.adam
+    o.adam = boom
+    try:
+        with pytest.raises(RuntimeError, match="injected"):
+            eng.train_steps(1, use_graph=False)
+    finally:
+        del o.adam
+    assert o.adam == real_adam
+    assert o.reset_held() == 0          # the engine dropped the hold on the way out
+    eng.train_steps(2, use_graph=False)
+    eng.train_steps(8)                  # and graph capture still works
+    ld, lg = eng.losses()
+    assert np.isfinite(ld) and np.isfinite(lg)

@@ -47,7 +47,6 @@ def columns():
 
 def _sklearn(x, seed):
     from sklearn.cluster import KMeans
-    from sklearn.exceptions import ConvergenceWarning
     from sklearn.mixture import BayesianGaussianMixture
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")

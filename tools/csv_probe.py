@@ -25,18 +25,18 @@ def main():
     rt.initialize()
     rt.run_round(0)
     vals = rt.engine.generate_decoded(40000).cpu().numpy()
-    names, kinds, vocabs = rt.csv_cols
+    lay = rt.csv_cols
     path = os.path.join(out, "probe.csv")
     print(f"cpus {os.cpu_count()} affinity {len(os.sched_getaffinity(0))}")
     for th in (1, 2, 4, 8, 16, 0, 0):
         t0 = time.perf_counter()
-        csvio.write_table(path, vals, names, kinds, vocabs, threads=th)
+        csvio.write_layout(path, vals, lay, threads=th)
         dt = time.perf_counter() - t0
         print(f"threads={th:2d}: {dt * 1e3:7.2f} ms  ({os.path.getsize(path) / 1e6:.1f} MB)", flush=True)
     # the same formatting with the bytes going nowhere: formatting cost vs file-write cost
     for th in (16, 0):
         t0 = time.perf_counter()
-        csvio.write_table(os.devnull, vals, names, kinds, vocabs, threads=th)
+        csvio.write_layout(os.devnull, vals, lay, threads=th)
         print(f"threads={th:2d} -> /dev/null: {(time.perf_counter() - t0) * 1e3:7.2f} ms", flush=True)
     import numpy as np
     t0 = time.perf_counter()

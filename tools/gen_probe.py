@@ -73,7 +73,7 @@ def main():
 
     if args.g0:
         # G0 variants: what does its time depend on (one-hot gather, BN epilogue, output dtype, tile)?
-        from fed_tgan_amd.ops.hip import EPI_BN_EVAL_RELU, EPI_NONE
+        from fed_tgan_amd.ops.hip import EPI_BN_EVAL_RELU
         layers_for(True)
         _, H, lg, out, col, opt = eng._gen_graphs[n]
         w16 = eng._gen_weights16()[0]

@@ -20,6 +20,7 @@ Nothing is imported from the reference at test time; this writes `profiles/refer
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import shutil
@@ -36,30 +37,61 @@ from make_goldens import CATEGORICAL, NONNEG, PROBLEM, SELECTED, TARGET, FakeRRe
 from real_quality import make_split  # noqa: E402  (imported before the reference goes on sys.path)
 
 
-class _AsyncCall:
+def _by_value(x):
+    """What an RPC peer receives: a copy (PyTorch RPC pickles every argument and return value)."""
+    return copy.deepcopy(x)
+
+
+class _ByValue:
+    """Method proxy with RPC by-value semantics: arguments and the result are copied.
+
+    The in-process stand-ins of `make_goldens.py` hand back the client's live objects.  Under those,
+    `MDGANServer.fit()` (`Server/dtds/distributed.py:789`) takes client 0's OWN generator as the
+    server's, and `sample()` (`:161`) then calls `generator.eval()` on it -- client 0 would train every
+    later round with eval-mode BatchNorm (running statistics, never updated).  Over real RPC the
+    server holds a pickled copy, and client 0 keeps training in train mode."""
+
+    def __init__(self, obj, wrap, copy: bool = True):
+        self.obj, self.wrap, self.copy = obj, wrap, copy
+
+    def __getattr__(self, name):
+        f = getattr(self.obj, name)
+        if not self.copy:
+            return lambda *a, **k: self.wrap(f(*a, **k))
+        return lambda *a, **k: self.wrap(_by_value(f(*_by_value(a), **_by_value(k))))
+
+
+class _Fut:
     def __init__(self, v):
         self.v = v
+
+    def to_here(self):
+        return self.v
 
     def wait(self):
         return self.v
 
 
-class _Async:
-    def __init__(self, obj):
-        self.obj = obj
-
-    def __getattr__(self, name):
-        f = getattr(self.obj, name)
-        return lambda *a, **k: _AsyncCall(f(*a, **k))
-
-
 class FakeRRefAsync(FakeRRef):
+    """RRef stand-in; ``by_value`` (default) gives RPC copy semantics, False the live-object aliasing
+    of the round-2 tool (kept to reproduce `profiles/reference_quality_r2.json`)."""
+
+    def __init__(self, obj, by_value: bool = True):
+        super().__init__(obj)
+        self.by_value = by_value
+
+    def remote(self):
+        return _ByValue(self.obj, _Fut, self.by_value)
+
+    def rpc_sync(self):
+        return _ByValue(self.obj, lambda v: v, self.by_value)
+
     def rpc_async(self):
-        return _Async(self.obj)
+        return _ByValue(self.obj, _Fut, self.by_value)
 
 
 def run_seed(ref_dir: str, work: str, seed: int, epochs: int, bootstrap: int, csv_epochs=None,
-             utility: bool = False) -> dict:
+             utility: bool = False, by_value: bool = True) -> dict:
     import pandas as pd
     import torch
     os.makedirs(work)
@@ -75,7 +107,7 @@ def run_seed(ref_dir: str, work: str, seed: int, epochs: int, bootstrap: int, cs
     t0 = time.time()
     clients = [rdist.MDGANClient(datapath.format(client=i), list(SELECTED), list(CATEGORICAL), list(NONNEG), {},
                                  TARGET, PROBLEM, epochs) for i in range(2)]
-    server = rdist.MDGANServer([FakeRRefAsync(c) for c in clients], epochs)
+    server = rdist.MDGANServer([FakeRRefAsync(c, by_value) for c in clients], epochs)
     server.uniform_meta_category()
     server.uniform_continuous_gmm()
     server.refit_local_transformer()
@@ -121,6 +153,9 @@ def main():
     ap.add_argument("--csv-epochs", type=int, nargs="*", default=None, help="only these epochs' CSVs (+ the last)")
     ap.add_argument("--utility", action="store_true", help="ML-utility gap of the last epoch")
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--aliased", action="store_true",
+                    help="round-2 harness: RRef stand-ins hand back live objects (client 0's generator is the "
+                         "server's and is switched to eval mode by the first sample_data)")
     args = ap.parse_args()
     shutil.rmtree(args.work, ignore_errors=True)
     shim = os.path.join(args.work, "shim")
@@ -134,12 +169,15 @@ def main():
     runs = []
     for seed in args.seeds:
         r = run_seed(args.reference, os.path.join(args.work, f"s{seed}"), seed, args.epochs, args.bootstrap_rows,
-                     args.csv_epochs, args.utility)
+                     args.csv_epochs, args.utility, by_value=not args.aliased)
         runs.append(r)
         print(json.dumps(r), flush=True)
     summary = {"epochs": runs[0]["epochs"],
                "avg_jsd_mean": np.mean([r["avg_jsd"] for r in runs], axis=0).round(4).tolist(),
                "avg_wd_mean": np.mean([r["avg_wd"] for r in runs], axis=0).round(4).tolist(),
+               "avg_jsd_sem": (np.std([r["avg_jsd"] for r in runs], axis=0, ddof=1) / np.sqrt(len(runs))).round(4).tolist()
+               if len(runs) > 1 else None,
+               "rpc_semantics": "aliased" if args.aliased else "by_value",
                "round_s_mean": float(np.mean([np.mean(r["round_s"]) for r in runs]))}
     if args.utility:
         summary["f1_gap_mean"] = float(np.mean([r["utility_final"]["f1_gap"] for r in runs]))
