@@ -51,9 +51,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--sync-csv", action="store_true", help="write each epoch CSV inside its round")
-    ap.add_argument("--check", action="store_true",
+    ap.add_argument("--check", action=argparse.BooleanOptionalAction, default=None,
                     help="after the timed rounds: assert every rank holds a bit-identical aggregate and the "
-                         "last epoch CSV has n_sample rows (reported as 'consistency')")
+                         "last epoch CSV has n_sample rows (reported as 'consistency'); default on for N > 1")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override for A/B measurements, e.g. --engine onehot=0")
     ap.add_argument("--force-dist", action="store_true",
@@ -112,6 +112,42 @@ def launch(n: int, argv) -> int:
     return rc
 
 
+# ----------------------------------------------------------------------------- transport record
+def _rccl_log_setup() -> str | None:
+    """Ask RCCL for its init / connection log in side files (one per rank), unless the user set
+    NCCL_DEBUG: the channel lines name the transport every ring / tree link uses (P2P/IPC over xGMI,
+    SHM, NET).  Logged at communicator setup only (the warm-up collectives), never per call."""
+    if os.environ.get("NCCL_DEBUG"):
+        return None
+    d = os.path.join(tempfile.gettempdir(), f"fedtgan_rccl_{os.environ.get('MASTER_PORT', '0')}")
+    os.makedirs(d, exist_ok=True)
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,SHM,NET"
+    os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.%h.%p.log")
+    return d
+
+
+def _rccl_transport(d: str | None) -> dict:
+    """Transport counts over every rank's connection lines ('... via P2P/IPC ...') + the version line."""
+    import glob
+    import re
+    out = {"links": {}, "files": 0}
+    if not d:
+        return out
+    pat = re.compile(r"\bvia (\S+)")
+    for f in glob.glob(os.path.join(d, "rccl.*.log")):
+        out["files"] += 1
+        with open(f, errors="replace") as fh:
+            for line in fh:
+                m = pat.search(line)
+                if m and ("->" in line or "Channel" in line):
+                    k = m.group(1).rstrip(",")
+                    out["links"][k] = out["links"].get(k, 0) + 1
+                if "version" in line and "version" not in out and ("RCCL" in line or "NCCL" in line):
+                    out["version"] = line.split("INFO", 1)[-1].strip()
+    return out
+
+
 # ----------------------------------------------------------------------------- one rank
 def run_rank(args) -> None:
     import torch
@@ -134,6 +170,7 @@ def run_rank(args) -> None:
             torch.set_num_threads(max(1, (os.cpu_count() or 8) // world))
     if args.force_dist and world == 1:
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    rccl_dir = _rccl_log_setup() if (device.type == "cuda" and (world > 1 or args.force_dist)) else None
     comm = Comm.from_env("auto", device, force_dist=args.force_dist)
     n_data = comm.data_world_size()
     if n_data != world:
@@ -157,7 +194,7 @@ def run_rank(args) -> None:
     for ep in range(args.warmup):
         rt.run_round(ep)
     rt.flush_writes()
-    rt.timer.totals.clear()          # phase breakdown over the timed rounds only
+    rt.timer.reset()                 # phase breakdown over the timed rounds only
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize(device)
@@ -173,8 +210,10 @@ def run_rank(args) -> None:
     sec_per_epoch = elapsed / max(args.steps, 1)
     last = os.path.join(out, f"{spec.name}_result", f"{spec.name}_synthesis_epoch_{cfg.epochs - 1}.csv")
 
+    rt.timer.resolve(block=True)
+    check = args.check if args.check is not None else world > 1
     consistency = None
-    if args.check:
+    if check:
         digest = hashlib.sha256(rt.engine.flat.detach().cpu().numpy().tobytes()).hexdigest()
         digests = comm.all_gather_object(digest)
         consistency = {"flat_identical": len(set(digests)) == 1, "ranks": len(digests)}
@@ -210,6 +249,16 @@ def run_rank(args) -> None:
         }
         if consistency is not None:
             rec["consistency"] = consistency
+        if comm.dist_active:
+            import torch.distributed as dist
+            ver = None
+            if device.type == "cuda":
+                try:
+                    ver = ".".join(str(x) for x in torch.cuda.nccl.version())
+                except Exception:   # pragma: no cover - build without RCCL
+                    ver = None
+            rec["comm"] = {"data_world_size": dist.get_world_size(comm.data), "data_backend": comm.data_backend,
+                           "rccl_version": ver, "transport": _rccl_transport(rccl_dir)}
         if args.engine:
             rec["engine_overrides"] = args.engine
         print(json.dumps(rec), flush=True)

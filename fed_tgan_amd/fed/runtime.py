@@ -102,9 +102,9 @@ class FedConfig:
     # sample + write the epoch CSV every N rounds (and after the last); 1 = every round (reference)
     csv_every: int = 1
     csv_epochs: Optional[List[int]] = None  # if set: sample + write only these epochs (and the last)
-    # per-collective sub-phase timers (allreduce / share / generate / gather / d2h), each a stream
-    # sync: None = on when real process groups exist (multi-rank runs, --force-dist), off otherwise
-    # (one plain GPU rank, in-process emulation: the extra syncs cost ~2-10 % of a round there)
+    # per-collective sub-phase timers (allreduce / share / generate / gather / d2h): HIP event pairs on a
+    # GPU (no host sync), wall time on the CPU.  None = on when real process groups exist (multi-rank
+    # runs, --force-dist), off otherwise
     phase_detail: Optional[bool] = None
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
@@ -176,7 +176,8 @@ class FedRuntime:
         if cfg.grad_flow and comm.is_client and comm.client_index == 0:
             from ..utils.gradflow import GradFlow
             self.gradflow = GradFlow()
-        self.timer = PhaseTimer(sync=True)    # device-synchronised phase boundaries (3 per round)
+        # phase boundaries as HIP events on a GPU (no host sync inside a round; read after the fact)
+        self.timer = PhaseTimer(events=device.type == "cuda")
         self.round_times: List[float] = []
         self.start_epoch = 0
         self.metrics = MetricsLog(cfg.metrics_log) if (cfg.metrics_log and self.is_fed) else None
@@ -596,10 +597,12 @@ class FedRuntime:
             return
         st = torch.load(p, weights_only=True)
         e = self.engine
-        if bool(st.get("g_wt", False)) != bool(e.cfg.g_wt):
-            raise RuntimeError(f"{p}: checkpoint generator layout g_wt={st.get('g_wt', False)} differs from the "
-                               f"engine's ({e.cfg.g_wt})")
-        for k in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
+        keys = ("flat", "mG", "vG", "mD", "vD")
+        # a checkpoint without the key predates input-major generator weights: [out, in] storage
+        saved_wt = bool(st.get("g_wt", False))
+        if saved_wt != bool(e.cfg.g_wt):
+            st.update(e.convert_layout({k: st[k] for k in keys}, saved_wt))
+        for k in keys + ("stepG", "stepD"):
             getattr(e, k).copy_(st[k])
         e.bn_batches = int(st["bn_batches"])
         if "cpu_rng" in st:

@@ -195,39 +195,15 @@ class CTGANEngine:
         order = {"G": 0, "D": 1, "S": 2}
         spec.sort(key=lambda t: order[t[2]])
         self.param_spec = spec
-        # 2-D weights are stored with their rows padded to a multiple of 4 floats (zero columns
-        # that stay zero under Adam, L2 decay and aggregation) and every tensor starts 16-B
-        # aligned, so the GEMMs read them with 16-B loads; self.p / self.g expose the logical
-        # [rows, cols] views, _ext() widens them to the padded width
-        # input-major generator weights (cfg.g_wt): stored [ceil4(in), ceil4(out)] -- the zero rows past
-        # `in` let _kpad widen K to a multiple of 4 exactly as the padded columns of [out, ceil4(in)] do
-        self.wt_names = {n for n, s, grp in spec if grp == "G" and len(s) == 2} if self.cfg.g_wt else set()
-        store = [((_ceil4(s[1]), _ceil4(s[0])) if nm in self.wt_names else (s[0], _ceil4(s[1]))) if len(s) == 2
-                 else s for nm, s, _ in spec]
-        sizes = [int(np.prod(s)) for s in store]
-        # every group starts 64-byte aligned (vectorised optimizer / aggregation kernels)
-        align = 16
-        offsets, pos, prev = [], 0, None
-        for (_, _, grp), n in zip(spec, sizes):
-            if grp != prev:
-                pos = (pos + align - 1) // align * align
-                prev = grp
-            pos = _ceil4(pos)
-            offsets.append(pos)
-            pos += n
-        total = (pos + align - 1) // align * align
+        self.wt_names, store, sizes, offsets, total = self._layout(bool(self.cfg.g_wt))
         self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
         self.p: Dict[str, torch.Tensor] = {}
         self.group_range = {}
-
-        def view(buf, o, n, shape, st, name):
-            v = buf[o:o + n].view(st)
-            if name in self.wt_names:
-                return v[:shape[1], :shape[0]].t()
-            return v[:, :shape[1]] if len(shape) == 2 else v
+        align = 16
+        view = self._view
 
         for (name, shape, grp), n, o, st in zip(spec, sizes, offsets, store):
-            self.p[name] = view(self.flat, o, n, shape, st, name)
+            self.p[name] = view(self.flat, o, n, shape, st, name, self.wt_names)
             a, _ = self.group_range.get(grp, (o, o))
             self.group_range[grp] = (a, (o + n + align - 1) // align * align)
         gA, gB = self.group_range["G"]
@@ -242,7 +218,7 @@ class CTGANEngine:
             if grp == "S":
                 continue
             base = o - (gA if grp == "G" else dA)
-            self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st, name)
+            self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st, name, self.wt_names)
         self.mG = torch.zeros_like(self.gradG)
         self.vG = torch.zeros_like(self.gradG)
         self.mD = torch.zeros_like(self.gradD)
@@ -250,6 +226,75 @@ class CTGANEngine:
         self.stepG = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.stepD = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.reset_parameters()
+
+    def _layout(self, g_wt: bool):
+        """Flat-buffer layout of ``self.param_spec``: (input-major names, storage shapes, sizes, offsets, total).
+
+        2-D weights are stored with their rows padded to a multiple of 4 floats (zero columns that stay
+        zero under Adam, L2 decay and aggregation) and every tensor starts 16-B aligned, so the GEMMs read
+        them with 16-B loads; self.p / self.g expose the logical [rows, cols] views, _ext() widens them to
+        the padded width.  Input-major generator weights (g_wt): stored [ceil4(in), ceil4(out)] -- the
+        zero rows past `in` let _kpad widen K to a multiple of 4 exactly as the padded columns of
+        [out, ceil4(in)] do."""
+        spec = self.param_spec
+        wt_names = {n for n, s, grp in spec if grp == "G" and len(s) == 2} if g_wt else set()
+        store = [((_ceil4(s[1]), _ceil4(s[0])) if nm in wt_names else (s[0], _ceil4(s[1]))) if len(s) == 2
+                 else s for nm, s, _ in spec]
+        sizes = [int(np.prod(s)) for s in store]
+        # every group starts 64-byte aligned (vectorised optimizer / aggregation kernels)
+        align = 16
+        offsets, pos, prev = [], 0, None
+        for (_, _, grp), n in zip(spec, sizes):
+            if grp != prev:
+                pos = (pos + align - 1) // align * align
+                prev = grp
+            pos = _ceil4(pos)
+            offsets.append(pos)
+            pos += n
+        total = (pos + align - 1) // align * align
+        return wt_names, store, sizes, offsets, total
+
+    @staticmethod
+    def _view(buf, o, n, shape, st, name, wt_names):
+        v = buf[o:o + n].view(st)
+        if name in wt_names:
+            return v[:shape[1], :shape[0]].t()
+        return v[:, :shape[1]] if len(shape) == 2 else v
+
+    def convert_layout(self, bufs: Dict[str, torch.Tensor], g_wt: bool) -> Dict[str, torch.Tensor]:
+        """State buffers (``flat`` and the group-relative ``mG`` ``vG`` ``mD`` ``vD``) saved with the
+        generator-weight layout ``g_wt`` -> this engine's layout (a transpose of the G weight blocks and
+        their Adam moments; everything else is copied).  Used to resume a checkpoint written with the
+        other ``EngineConfig.g_wt``."""
+        spec = self.param_spec
+        wt_s, st_s, n_s, off_s, _ = self._layout(bool(g_wt))
+        wt_d, st_d, n_d, off_d, _ = self._layout(bool(self.cfg.g_wt))
+
+        def base(offs, grp):
+            return min(o for (_, _, g), o in zip(spec, offs) if g == grp)
+        out = {}
+        for key, src in bufs.items():
+            grp = None if key == "flat" else key[-1]
+            if grp not in (None, "G", "D"):
+                raise ValueError(f"convert_layout: unknown buffer {key!r}")
+            src = src.detach().cpu()
+            n = self.flat.numel() if grp is None else (self.nG if grp == "G" else self.nD)
+            dst = torch.zeros(n, dtype=torch.float32)
+            for i, (name, shape, g) in enumerate(spec):
+                if grp is not None and g != grp:
+                    continue
+                bs, bd = (0, 0) if grp is None else (base(off_s, grp), base(off_d, grp))
+                sv = self._view(src, off_s[i] - bs, n_s[i], shape, st_s[i], name, wt_s)
+                dv = self._view(dst, off_d[i] - bd, n_d[i], shape, st_d[i], name, wt_d)
+                dv.copy_(sv)
+            out[key] = dst
+        return out
+
+    def _view_in(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        """Logical view of parameter ``name`` inside a group-relative buffer shaped like gradG / gradD
+        (e.g. the Adam moments mG / vD)."""
+        g = self.g[name]
+        return buf.as_strided(g.shape, g.stride(), g.storage_offset())
 
     def reset_parameters(self):
         """PyTorch default init of the reference modules (Linear kaiming-uniform, BN 1/0)."""

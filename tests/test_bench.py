@@ -62,14 +62,17 @@ def test_bench_self_launch_four_ranks():
 
 def test_bench_eight_ranks_identical_aggregate():
     """8 self-launched ranks: every rank holds a bit-identical aggregate after the last round and the
-    epoch CSV (sharded generation, gathered on rank 0) has all 40,000 rows."""
+    epoch CSV (sharded generation, gathered on rank 0) has all 40,000 rows -- checked by DEFAULT for
+    N > 1 (the driver's 8-GPU line must verify itself), with the data-plane record."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup",
-                        "1", "--rows", "1000", "--n-sample", "40000", "--quiet", "--no-eval", "--check"],
+                        "1", "--rows", "1000", "--n-sample", "40000", "--quiet", "--no-eval"],
                        capture_output=True, text=True, timeout=600, env=_env(), cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_lines(r.stdout)[0]
     assert rec["n_gpus"] == 8
     assert rec["consistency"] == {"flat_identical": True, "ranks": 8, "csv_rows": 40000}
+    assert rec["comm"]["data_world_size"] == 8 and rec["comm"]["data_backend"] == "gloo"
+    assert "transport" in rec["comm"]
 
 
 def test_bench_world_size_mismatch_fails():

@@ -90,6 +90,37 @@ def test_checkpoint_resume(tmp_path):
     assert len(rt2.round_times) == 3
 
 
+@pytest.mark.parametrize("saved_wt", [False, True])
+def test_checkpoint_resume_across_generator_layouts(tmp_path, saved_wt):
+    """a checkpoint written with the other EngineConfig.g_wt (e.g. before input-major generator
+    weights became the default: no 'g_wt' key) resumes into the same logical weights and Adam moments."""
+    import dataclasses
+    eng_a = EngineConfig(batch_size=100, g_wt=saved_wt)
+    cfg = _cfg(tmp_path, epochs=2, ckpt_every=1, engine=eng_a)
+    rt = run_local_emulation(cfg, 1, backend="torch", device=torch.device("cpu"))
+    if not saved_wt:     # the pre-g_wt checkpoint format had no layout key
+        path = rt._ckpt_path()
+        st = torch.load(path, weights_only=True)
+        st.pop("g_wt", None)
+        torch.save(st, path)
+    eng_b = dataclasses.replace(eng_a, g_wt=not saved_wt)
+    rt2 = FedRuntime(_cfg(tmp_path, epochs=3, resume=True, engine=eng_b), Comm(0, 1, [0], "gloo",
+                     device=torch.device("cpu")), torch.device("cpu"))
+    rt2.initialize()
+    assert rt2.start_epoch == 2
+    a, b = rt.engine, rt2.engine
+    for name in a.p:
+        assert torch.equal(a.p[name], b.p[name]), name
+    for name in a.g:        # Adam moments through the gradient-shaped views
+        for buf in ("m", "v"):
+            grp = "G" if name.startswith("G.") else "D"
+            va = a._view_in(getattr(a, buf + grp), name)
+            vb = b._view_in(getattr(b, buf + grp), name)
+            assert torch.equal(va, vb), (buf, name)
+    rt2.fit()
+    assert len(rt2.round_times) == 3
+
+
 def _run_cli(args, cwd, timeout=420):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     return subprocess.run([sys.executable, "-m", "dtds.distributed"] + args, cwd=cwd, env=env, capture_output=True,

@@ -105,6 +105,7 @@ def test_rccl_branches_one_rank():
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["ok"] and res["data_backend"] == "nccl" and res["data_ranks"] == 1, res
+    assert res["hier_allreduce_ok"] and res["hier_gather_ok"], res      # HierComm (K=2 threads) over RCCL
     assert "AllReduce" in (r.stdout + r.stderr)
 
 
@@ -119,6 +120,9 @@ def test_bench_one_gpu_rccl_data_plane():
     assert rec["config"]["data_plane"] == "nccl" and rec["n_gpus"] == 1
     assert rec["consistency"]["flat_identical"] and rec["consistency"]["csv_rows"] == 3000
     assert "allreduce" in rec["phase_s"]
+    # the self-verification record of the driver's multi-GPU line
+    assert rec["comm"]["data_world_size"] == 1 and rec["comm"]["data_backend"] == "nccl"
+    assert rec["comm"]["rccl_version"] and rec["comm"]["transport"]["files"] >= 1
 
 
 def test_saved_generator_on_gpu(tmp_path):

@@ -24,6 +24,51 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
+def hier_check(comm, dev, g) -> dict:
+    """``-world_size N -local_clients K`` on this box (N = 1, K = 2): two client threads, one HIP stream
+    each, combine on the GPU and thread 0 runs the process-level RCCL all-reduce / gather (HierComm)."""
+    import threading
+
+    import torch
+
+    from fed_tgan_amd.fed.local import HierComm, LocalGroup
+    group = LocalGroup(2)
+    bufs = [torch.randn(1_000_003, generator=g).to(dev) for _ in range(2)]
+    ws = [0.25, 0.75]
+    want = torch.zeros_like(bufs[0])
+    for b, w in zip(bufs, ws):
+        want.add_(b, alpha=w)
+    got, errors = [None, None], []
+
+    def worker(t):
+        try:
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(torch.cuda.Stream(dev)):
+                hc = HierComm(group, t, dev, comm)
+                f = bufs[t].clone()
+                hc.weighted_all_reduce(f, ws[t])
+                rows = torch.full((100 + t, 42), float(t + 1), device=dev)
+                out = hc.gather_rows(rows, [100, 101], [0, 1], dst=0, to_host=False)
+                torch.cuda.current_stream(dev).synchronize()
+                got[t] = (f, out)
+        except BaseException as e:   # surfaced in the result
+            errors.append(repr(e))
+            group.failed.set()
+            group.barrier.abort()
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        return {"hier_allreduce_ok": False, "hier_gather_ok": False, "hier_error": errors[0]}
+    ar = all(torch.equal(f, want) for f, _ in got)
+    out0, out1 = got[0][1], got[1][1]
+    ga = out1 is None and out0 is not None and tuple(out0.shape) == (201, 42) and \
+        bool((out0[:100] == 1).all()) and bool((out0[100:] == 2).all())
+    return {"hier_allreduce_ok": bool(ar), "hier_gather_ok": bool(ga)}
+
+
 def main() -> int:
     import torch
     import torch.distributed as dist
@@ -52,8 +97,10 @@ def main() -> int:
     comm.exchange(sends=[(src, 0)], recvs=[(dst, 0)])
     torch.cuda.synchronize()
     res["exchange_ok"] = bool(torch.equal(src, dst))
+    res.update(hier_check(comm, dev, g))
     comm.destroy()
-    ok = res["data_backend"] == "nccl" and res["allreduce_ok"] and res["gather_ok"] and res["exchange_ok"]
+    ok = res["data_backend"] == "nccl" and res["allreduce_ok"] and res["gather_ok"] and res["exchange_ok"] and \
+        res["hier_allreduce_ok"] and res["hier_gather_ok"]
     res["ok"] = bool(ok)
     print(json.dumps(res), flush=True)
     return 0 if ok else 1

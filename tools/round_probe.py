@@ -14,7 +14,7 @@ for ep in range(4):
     rt.run_round(ep)
 rt.flush_writes()
 torch.cuda.synchronize()
-rt.timer._totals.clear() if hasattr(rt.timer, "_totals") else rt.timer.totals.clear()
+rt.timer.reset()
 t0 = time.perf_counter()
 n = 12
 for ep in range(4, 4 + n):
