@@ -114,15 +114,17 @@ def launch(n: int, argv) -> int:
 
 # ----------------------------------------------------------------------------- transport record
 def _rccl_log_setup() -> str | None:
-    """Ask RCCL for its init / connection log in side files (one per rank), unless the user set
-    NCCL_DEBUG: the channel lines name the transport every ring / tree link uses (P2P/IPC over xGMI,
-    SHM, NET).  Logged at communicator setup only (the warm-up collectives), never per call."""
-    if os.environ.get("NCCL_DEBUG"):
+    """Ask RCCL for its init / connection log in side files (one per rank): the channel lines name the
+    transport every ring / tree link uses (P2P/IPC over xGMI, SHM, NET).  Logged at communicator setup
+    only (the warm-up collectives), never per call.  A user-set NCCL_DEBUG_FILE is left alone (no record);
+    a quieter NCCL_DEBUG level (e.g. WARN from the environment) is raised to INFO for the side file."""
+    if os.environ.get("NCCL_DEBUG_FILE"):
         return None
     d = os.path.join(tempfile.gettempdir(), f"fedtgan_rccl_{os.environ.get('MASTER_PORT', '0')}")
     os.makedirs(d, exist_ok=True)
-    os.environ["NCCL_DEBUG"] = "INFO"
-    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,SHM,NET"
+    if os.environ.get("NCCL_DEBUG", "").upper() not in ("INFO", "TRACE"):
+        os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,P2P,SHM,NET")
     os.environ["NCCL_DEBUG_FILE"] = os.path.join(d, "rccl.%h.%p.log")
     return d
 
@@ -131,7 +133,7 @@ def _rccl_transport(d: str | None) -> dict:
     """Transport counts over every rank's connection lines ('... via P2P/IPC ...') + the version line."""
     import glob
     import re
-    out = {"links": {}, "files": 0}
+    out = {"links": {}, "files": 0, "nccl_debug": os.environ.get("NCCL_DEBUG")}
     if not d:
         return out
     pat = re.compile(r"\bvia (\S+)")
@@ -143,7 +145,7 @@ def _rccl_transport(d: str | None) -> dict:
                 if m and ("->" in line or "Channel" in line):
                     k = m.group(1).rstrip(",")
                     out["links"][k] = out["links"].get(k, 0) + 1
-                if "version" in line and "version" not in out and ("RCCL" in line or "NCCL" in line):
+                if "version" not in out and ("RCCL version" in line or "NCCL version" in line):
                     out["version"] = line.split("INFO", 1)[-1].strip()
     return out
 
