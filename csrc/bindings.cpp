@@ -721,7 +721,8 @@ void rng_bump(const Tensor& ctr) {
 
 void write_csv(const std::string& path, const Tensor& values, std::vector<std::string> names, std::vector<int64_t> kinds,
                std::vector<std::string> vocab_flat, std::vector<int64_t> vocab_offsets, int64_t threads,
-               std::vector<int64_t> src, std::vector<int64_t> date_desc, std::vector<int64_t> date_lut) {
+               std::vector<int64_t> src, std::vector<int64_t> date_desc, std::vector<int64_t> date_lut,
+               const optional<Tensor>& aux) {
   // output column j: kinds[j], names[j], vocabulary vocab_flat[vocab_offsets[j], vocab_offsets[j + 1]), source
   // column src[j] of values (default j).  Date columns (kind 3) take their description from date_desc, in
   // output order: [mode, n_parts, (src, elem, lut_off, lut_len) x n_parts], code -> value tables in date_lut.
@@ -729,6 +730,11 @@ void write_csv(const std::string& path, const Tensor& values, std::vector<std::s
               "write_csv: values must be a contiguous CPU float64 matrix");
   const int64_t cols = values.size(1);
   const int64_t n_out = (int64_t)kinds.size();
+  const bool has_aux = aux.has_value() && aux->defined();
+  if (has_aux)
+    TORCH_CHECK(!aux->is_cuda() && aux->scalar_type() == at::kDouble && aux->is_contiguous() && aux->dim() == 2 &&
+                    aux->size(0) == values.size(0), "write_csv: aux must be a contiguous CPU float64 [rows, n] matrix");
+  const int64_t aux_cols = has_aux ? aux->size(1) : 0;
   TORCH_CHECK((int64_t)names.size() == n_out && (int64_t)vocab_offsets.size() == n_out + 1 &&
                   (src.empty() ? n_out == cols : (int64_t)src.size() == n_out),
               "write_csv: descriptors");
@@ -743,7 +749,7 @@ void write_csv(const std::string& path, const Tensor& values, std::vector<std::s
                     vocab_offsets[(size_t)j + 1] <= (int64_t)vocab_flat.size(), "write_csv: vocab offsets");
     c.vocab.assign(vocab_flat.begin() + vocab_offsets[(size_t)j], vocab_flat.begin() + vocab_offsets[(size_t)j + 1]);
     if (c.kind != fedtgan::CSV_DATE) {
-      TORCH_CHECK(c.src >= 0 && c.src < cols, "write_csv: source column out of range");
+      TORCH_CHECK(c.src >= 0 && c.src < cols + aux_cols, "write_csv: source column out of range");
       continue;
     }
     TORCH_CHECK(dp + 2 <= date_desc.size(), "write_csv: date_desc too short");
@@ -762,7 +768,8 @@ void write_csv(const std::string& path, const Tensor& values, std::vector<std::s
     }
   }
   TORCH_CHECK(dp == date_desc.size(), "write_csv: unused date_desc entries");
-  fedtgan::write_csv_columns(path, values.data_ptr<double>(), values.size(0), cols, names, out, (int)threads);
+  fedtgan::write_csv_columns(path, values.data_ptr<double>(), values.size(0), cols, names, out, (int)threads,
+                             has_aux ? aux->data_ptr<double>() : nullptr, aux_cols);
 }
 
 void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Tensor& col_kind, const Tensor& col_pos,
@@ -1017,7 +1024,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "int stream) -> ()");
   m.def(
       "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
-      "int threads, int[] src=[], int[] date_desc=[], int[] date_lut=[]) -> ()");
+      "int threads, int[] src=[], int[] date_desc=[], int[] date_lut=[], Tensor? aux=None) -> ()");
   m.def("py_float(float x) -> str", &py_float);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);

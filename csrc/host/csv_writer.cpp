@@ -198,12 +198,14 @@ char* put_date(char* p, const DateFields& f, int style) {
 // written through a raw pointer into a buffer sized for its worst case (26 bytes per number), so the
 // hot loop does no allocation, no searching and no growing appends.
 std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, int64_t r1,
-                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style) {
+                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style,
+                               const double* aux, int64_t aux_cols) {
   std::vector<std::vector<std::string>> qv(out.size());
   size_t row_max = 1;
   for (size_t j = 0; j < out.size(); ++j) {
     const CsvColumn& c = out[j];
-    if (c.kind != CSV_DATE && (c.src < 0 || c.src >= cols)) throw std::runtime_error("csv: source column out of range");
+    if (c.kind != CSV_DATE && (c.src < 0 || c.src >= cols + (aux ? aux_cols : 0)))
+      throw std::runtime_error("csv: source column out of range");
     size_t w = 26;
     if (c.kind == CSV_VOCAB) {
       w = 0;
@@ -223,13 +225,15 @@ std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, i
   char* p = &s[0];
   for (int64_t r = r0; r < r1; ++r) {
     const double* row = values + r * cols;
+    const double* arow = aux ? aux + r * aux_cols : nullptr;   // column src >= cols is arow[src - cols]
+    auto val = [&](int s) { return s < cols ? row[s] : arow[s - cols]; };
     for (size_t j = 0; j < out.size(); ++j) {
       if (j) *p++ = ',';
       const CsvColumn& c = out[j];
       switch (c.kind) {
         case CSV_VOCAB: {
           const auto& voc = qv[j];
-          const int64_t k = (int64_t)row[c.src];
+          const int64_t k = (int64_t)val(c.src);
           if (k < 0 || k >= (int64_t)voc.size()) throw std::runtime_error("csv: category code out of range");
           const std::string& f = voc[(size_t)k];
           std::memcpy(p, f.data(), f.size());
@@ -237,7 +241,7 @@ std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, i
           break;
         }
         case CSV_NONNEG: {   // already mapped by exp(x)-1 (+ceil) on the host with numpy's exp
-          const double x = row[c.src];
+          const double x = val(c.src);
           if (x == -1.0) *p++ = ' ';
           else p = put_py_float(p, x);
           break;
@@ -249,7 +253,7 @@ std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, i
           break;
         }
         default:
-          p = put_py_float(p, row[c.src]);
+          p = put_py_float(p, val(c.src));
       }
     }
     *p++ = '\n';
@@ -295,7 +299,7 @@ std::vector<CsvColumn> simple_columns(int64_t cols, const std::vector<int>& kind
 std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, int64_t r0, int64_t r1,
                             const std::vector<int>& kinds, const std::vector<std::vector<std::string>>& vocabs) {
   const auto out = simple_columns(cols, kinds, vocabs);
-  return format_csv_columns(values, cols, r0, r1, out, resolve_date_styles(values, rows, cols, out));
+  return format_csv_columns(values, cols, r0, r1, out, resolve_date_styles(values, rows, cols, out), nullptr, 0);
 }
 
 std::string format_py_float(double x) {
@@ -305,7 +309,8 @@ std::string format_py_float(double x) {
 }
 
 void write_csv_columns(const std::string& path, const double* values, int64_t rows, int64_t cols,
-                       const std::vector<std::string>& names, const std::vector<CsvColumn>& out, int threads) {
+                       const std::vector<std::string>& names, const std::vector<CsvColumn>& out, int threads,
+                       const double* aux, int64_t aux_cols) {
   if (names.size() != out.size()) throw std::runtime_error("csv: column descriptor size mismatch");
   const std::vector<int> style = resolve_date_styles(values, rows, cols, out);
   if (threads <= 0) {
@@ -330,7 +335,7 @@ void write_csv_columns(const std::string& path, const double* values, int64_t ro
       for (int c = next.fetch_add(1); c < nchunks; c = next.fetch_add(1)) {
         try {
           const int64_t r0 = (int64_t)c * chunk, r1 = std::min(rows, r0 + chunk);
-          parts[(size_t)c] = format_csv_columns(values, cols, r0, r1, out, style);
+          parts[(size_t)c] = format_csv_columns(values, cols, r0, r1, out, style, aux, aux_cols);
           ready[(size_t)c].set_value();
         } catch (...) {
           ready[(size_t)c].set_exception(std::current_exception());

@@ -29,11 +29,15 @@ std::string format_py_float(double x);
 
 std::vector<int> resolve_date_styles(const double* values, int64_t rows, int64_t cols, const std::vector<CsvColumn>& out);
 
+// aux (nullable): a second [rows, aux_cols] matrix; a column's src >= cols reads aux[r, src - cols] (e.g.
+// the non-negative columns mapped on the host, so the main matrix is read in place, never copied)
 std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, int64_t r1,
-                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style);
+                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style,
+                               const double* aux = nullptr, int64_t aux_cols = 0);
 
 void write_csv_columns(const std::string& path, const double* values, int64_t rows, int64_t cols,
-                       const std::vector<std::string>& names, const std::vector<CsvColumn>& out, int threads);
+                       const std::vector<std::string>& names, const std::vector<CsvColumn>& out, int threads,
+                       const double* aux = nullptr, int64_t aux_cols = 0);
 
 // one output column per value column (kinds 0..2)
 std::string format_csv_rows(const double* values, int64_t rows, int64_t cols, int64_t r0, int64_t r1,

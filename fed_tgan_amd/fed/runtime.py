@@ -106,6 +106,9 @@ class FedConfig:
     # GPU (no host sync), wall time on the CPU.  None = on when real process groups exist (multi-rank
     # runs, --force-dist), off otherwise
     phase_detail: Optional[bool] = None
+    # phase timers on a GPU: "events" (HIP event pairs, no host sync) or "sync" (stream-synchronised wall
+    # time at every phase boundary, the round-2 behaviour)
+    phase_timer: str = "events"
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
 
@@ -177,7 +180,8 @@ class FedRuntime:
             from ..utils.gradflow import GradFlow
             self.gradflow = GradFlow()
         # phase boundaries as HIP events on a GPU (no host sync inside a round; read after the fact)
-        self.timer = PhaseTimer(events=device.type == "cuda")
+        self.timer = PhaseTimer(events=device.type == "cuda" and cfg.phase_timer == "events",
+                                sync=cfg.phase_timer == "sync")
         self.round_times: List[float] = []
         self.start_epoch = 0
         self.metrics = MetricsLog(cfg.metrics_log) if (cfg.metrics_log and self.is_fed) else None

@@ -76,9 +76,10 @@ def check() -> None:
 
 def write_csv(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequence[int],
               vocabs: Sequence[Sequence[str]], threads: int = 0, src: Sequence[int] = (),
-              date_desc: Sequence[int] = (), date_lut: Sequence[int] = ()) -> None:
+              date_desc: Sequence[int] = (), date_lut: Sequence[int] = (), aux: np.ndarray | None = None) -> None:
     """Native CSV formatter (csrc/host/csv_writer.cpp).  Output column j has kinds[j], names[j], vocabs[j]
-    and reads value column src[j] (default j); date columns: see ``data.decode.CsvLayout``."""
+    and reads value column src[j] (default j; src >= values' width reads column src - width of ``aux``);
+    date columns: see ``data.decode.CsvLayout``."""
     L = require()
     flat, offs = [], [0]
     for v in vocabs:
@@ -86,4 +87,5 @@ def write_csv(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequen
         offs.append(len(flat))
     t = torch.from_numpy(np.ascontiguousarray(values, dtype=np.float64))
     L.write_csv(path, t, list(names), [int(k) for k in kinds], flat, offs, int(threads), [int(x) for x in src],
-                [int(x) for x in date_desc], [int(x) for x in date_lut])
+                [int(x) for x in date_desc], [int(x) for x in date_lut],
+                None if aux is None else torch.from_numpy(np.ascontiguousarray(aux, dtype=np.float64)))

@@ -69,25 +69,40 @@ def write_table(path: str, values: np.ndarray, names: Sequence[str], kinds: Sequ
                  threads)
 
 
+def _nonneg(v: np.ndarray) -> np.ndarray:
+    """exp(x)-1 with ceil for negatives, with numpy's exp (bit-identical to the pandas path)."""
+    w = np.exp(v) - 1.0
+    neg = w < 0
+    w[neg] = np.ceil(w[neg])
+    return w
+
+
 def write_layout(path: str, values: np.ndarray, layout: CsvLayout, threads: int = 0) -> None:
-    """Write the decoded value matrix as ``layout`` (``data.decode.csv_layout``) describes it."""
-    values = np.array(values, dtype=np.float64, copy=True)
-    for j, k in enumerate(layout.kinds):
-        if k == KIND_NONNEG:     # exp(x)-1 with numpy's exp (bit-identical to the pandas path)
-            c = layout.src[j]
-            w = np.exp(values[:, c]) - 1.0
-            neg = w < 0
-            w[neg] = np.ceil(w[neg])
-            values[:, c] = w
+    """Write the decoded value matrix as ``layout`` (``data.decode.csv_layout``) describes it.
+
+    The matrix is read in place: only the non-negative columns are mapped (into a small side matrix
+    the formatter reads them from).  A full host copy of a 40k-row table costs ~2 ms of GIL-holding
+    memcpy per epoch -- in the background writer that stalls the main thread's graph launches."""
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    nn = [j for j, k in enumerate(layout.kinds) if k == KIND_NONNEG]
     lib = _native()
     if lib is not None:
         from ..ops import native
-        native.write_csv(path, values, layout.names, layout.kinds, layout.vocabs, threads, layout.src,
-                         layout.date_desc, layout.date_lut)
+        src = list(layout.src)
+        aux = None
+        if nn:
+            aux = np.empty((values.shape[0], len(nn)), dtype=np.float64)
+            for i, j in enumerate(nn):
+                aux[:, i] = _nonneg(values[:, layout.src[j]])
+                src[j] = values.shape[1] + i
+        native.write_csv(path, values, layout.names, layout.kinds, layout.vocabs, threads, src,
+                         layout.date_desc, layout.date_lut, aux=aux)
         return
     if layout.has_dates:
         raise RuntimeError("the Python CSV formatter has no date columns (native library not loaded)")
-    vals = values[:, layout.src]
+    vals = values[:, layout.src]          # (a copy: fancy indexing)
+    for j in nn:
+        vals[:, j] = _nonneg(vals[:, j])
     kinds_py = [KIND_FLOAT if k == KIND_NONNEG else k for k in layout.kinds]
     with open(path, "wb") as f:
         f.write(format_table_py(vals, layout.names, kinds_py, layout.vocabs,
