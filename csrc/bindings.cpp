@@ -103,6 +103,23 @@ int64_t reset_held() {
   return n;
 }
 
+// Batched clients (kernels/launch.h ClientBatch): the calling thread's launches from here on run K clients at
+// once -- client c's buffers `stride` bytes after client c-1's (one arena, identical layouts), its Philox seed
+// seed + c * seed_step; base = client 0's slab start (every pointer of a batched launch is checked to lie in
+// [base, base + stride)).  k = 1 restores plain launches.  Returns the previous k.
+int64_t set_client_batch(int64_t k, int64_t stride, int64_t seed_step, int64_t base) {
+  TORCH_CHECK(k >= 1 && k <= 65535, "set_client_batch: k");
+  TORCH_CHECK(k == 1 || (stride > 0 && stride % 256 == 0 && base != 0),
+              "set_client_batch: a batched context needs a 256-B aligned slab stride and a base");
+  fedtgan::ClientBatch& cb = fedtgan::client_batch();
+  const int64_t prev = cb.k;
+  cb.k = (int)k;
+  cb.stride = k > 1 ? stride : 0;
+  cb.seed_step = k > 1 ? (uint64_t)seed_step : 0;
+  cb.base = k > 1 ? reinterpret_cast<const char*>(base) : nullptr;
+  return prev;
+}
+
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
           const optional<Tensor>& bias, int64_t epi, const optional<Tensor>& ms, double slope, double p_drop,
           const optional<Tensor>& ws, int64_t splitk, int64_t seed, const optional<Tensor>& rng_ctr, int64_t stream,
@@ -1028,6 +1045,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("py_float(float x) -> str", &py_float);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
+  m.def("set_client_batch(int k, int stride, int seed_step, int base) -> int", &set_client_batch);
   m.def("check_status() -> int", &check_status);
   m.def("is_checked() -> bool", &is_checked);
 }

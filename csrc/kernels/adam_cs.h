@@ -7,6 +7,23 @@
 
 namespace fedtgan {
 
+// batched clients (launch.h ClientBatch): a client's copy of a column-sum job / of every job of an Adam launch
+__device__ __forceinline__ ColsumJob client_job(ColsumJob jb, int64_t o) {
+  jb.a = cptr(jb.a, o);
+  jb.out = cptr(jb.out, o);
+  jb.w = cptr(jb.w, o);
+  jb.dot_v = cptr(jb.dot_v, o);
+  jb.dot_e = cptr(jb.dot_e, o);
+  jb.dot_out = cptr(jb.dot_out, o);
+  jb.dot_w = cptr(jb.dot_w, o);
+  return jb;
+}
+inline void check_slab(const AdamColsum& cs) {
+  for (int k = 0; k < cs.n_jobs && k < 8; ++k)
+    check_slabs("adam column-sum job", cs.jobs[k].a, cs.jobs[k].out, cs.jobs[k].w, cs.jobs[k].dot_v, cs.jobs[k].dot_e,
+                cs.jobs[k].dot_out, cs.jobs[k].dot_w);
+}
+
 // One Adam element update, with explicit fmaf so every kernel that applies it (the float4 Adam, the
 // column-sum jobs, a fused GEMM's epilogue) rounds identically whatever the compiler contracts:
 //   gq = g + wd p ; m = b1 m + (1 - b1) gq ; v = b2 v + (1 - b2) gq^2 ; p -= sz m / (sqrt(v) / bc2s + eps)
@@ -40,7 +57,8 @@ template <int AUX>
 __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restrict__ p, const float* __restrict__ g,
                                              float* __restrict__ m, float* __restrict__ v,
                                              const float* __restrict__ step, int64_t n4, float lr, float b1, float b2,
-                                             float eps, float wd, uint64_t* rng_bump, const AdamColsum& cs) {
+                                             float eps, float wd, uint64_t* rng_bump, const AdamColsum& cs,
+                                             int64_t co = 0) {
   const float t = step[0];
   const float bc1 = 1.f - powf(b1, t);
   const float bc2s = sqrtf(1.f - powf(b2, t));
@@ -51,7 +69,9 @@ __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restric
     __shared__ float part[2][ACS_GROUPS][ACS_COLS + 1];
     int j = 0;
     while (j + 1 < cs.n_jobs && bid >= cs.blk_start[j + 1]) ++j;
-    const ColsumJob jb = cs.jobs[j];
+    // (co: batched clients -- this client's copy of the job; applied to the one job read here, never to the
+    // whole by-value AdamColsum, which would then live in scratch memory)
+    const ColsumJob jb = co ? client_job(cs.jobs[j], co) : cs.jobs[j];
     const int cb = bid - cs.blk_start[j];
     const int qd = threadIdx.x & 3, grp = threadIdx.x >> 2;
     const int c0 = cb * ACS_COLS + qd * 4;

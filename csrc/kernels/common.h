@@ -40,6 +40,12 @@ enum CheckCode : unsigned {
 #define FT_CHECKED 0
 #endif
 
+// batched clients (launch.h ClientBatch): client copy of a buffer, `off` bytes after client 0's
+template <class T>
+__device__ __forceinline__ T* cptr(T* p, int64_t off) {
+  return p ? (T*)((const char*)p + off) : p;
+}
+
 struct RngArgs {
   uint64_t seed;
   const uint64_t* ctr;  // device-resident step counter

@@ -16,12 +16,34 @@
 // Randomness: Philox streams (common.h) indexed by (seed, stream id, device step counter,
 // element); the step counter is bumped by the generator's Adam launch (last of a step).
 #include <algorithm>
+#include <stdexcept>
+#include <string>
 
 #include "common.h"
 #include "launch.h"
 #include "adam_cs.h"
 
 namespace fedtgan {
+
+// ---------------------------------------------------------------------------- batched clients (launch.h)
+ClientBatch& client_batch() {
+  static thread_local ClientBatch cb{1, 0, 0, nullptr};
+  return cb;
+}
+
+void check_slab(const void* p, const char* what) {
+  const ClientBatch& cb = client_batch();
+  if (cb.k <= 1 || p == nullptr) return;
+  const char* c = static_cast<const char*>(p);
+  if (c < cb.base || c >= cb.base + cb.stride)
+    throw std::runtime_error(std::string("batched launch: ") + what +
+                             " is not in client 0's arena slab (every buffer of a batched step must be)");
+}
+
+void require_unbatched(const char* what) {
+  if (client_batch().k > 1) throw std::runtime_error(std::string(what) + " has no batched-clients form");
+}
+
 
 #if FT_CHECKED
 __device__ unsigned g_check_ops = 0u;
@@ -101,6 +123,27 @@ __device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint4 k
 }
 
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
+  if (blockIdx.z) {   // batched clients: this client's buffers and seed
+    const int64_t o = (int64_t)blockIdx.z * a.cb.stride;
+    a.h = cptr(a.h, o);
+    a.h16 = cptr(a.h16, o);
+    a.xf = cptr(a.xf, o);
+    a.xr = cptr(a.xr, o);
+    a.cdf = cptr(a.cdf, o);
+    a.cond_off = cptr(a.cond_off, o);
+    a.cond_w = cptr(a.cond_w, o);
+    a.row_off = cptr(a.row_off, o);
+    a.row_cnt = cptr(a.row_cnt, o);
+    a.rows = cptr(a.rows, o);
+    a.data = cptr(a.data, o);
+    a.col = cptr(a.col, o);
+    a.opt = cptr(a.opt, o);
+    a.step_bump = cptr(a.step_bump, o);
+    a.step_bump2 = cptr(a.step_bump2, o);
+    a.metrics = cptr(a.metrics, o);
+    a.rng_ctr = cptr(a.rng_ctr, o);
+    a.seed += (uint64_t)blockIdx.z * a.cb.seed_step;
+  }
   const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (blockIdx.x == 0 && tid == 0) {
@@ -202,9 +245,19 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   for (int i = lane; i < a.Dd; i += 64) dst[i] = src[i];
 }
 
-void launch_sample(const SampleArgs& a, hipStream_t stream) {
+void launch_sample(const SampleArgs& a0, hipStream_t stream) {
+  SampleArgs a = a0;
+  a.cb = client_batch();
+  if (a.cb.k > 1) {
+    for (const void* p : {(const void*)a.h, (const void*)a.h16, (const void*)a.xf, (const void*)a.xr, (const void*)a.cdf,
+                          (const void*)a.cond_off, (const void*)a.cond_w, (const void*)a.row_off, (const void*)a.row_cnt,
+                          (const void*)a.rows, (const void*)a.data, (const void*)a.col, (const void*)a.opt,
+                          (const void*)a.step_bump, (const void*)a.step_bump2, (const void*)a.metrics,
+                          (const void*)a.rng_ctr})
+      check_slab(p, "sample operand");
+  }
   const int blocks = (a.B + SAMPLE_ROWS - 1) / SAMPLE_ROWS;
-  hipLaunchKernelGGL(sample_kernel, dim3(blocks), dim3(SAMPLE_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(sample_kernel, dim3(blocks, 1, a.cb.k), dim3(SAMPLE_THREADS), 0, stream, a);
 }
 
 // ============================================================================ activation
@@ -271,6 +324,22 @@ __device__ __forceinline__ ActSmem act_stage_tables(const SpanTables& sp, float*
   return t;
 }
 
+// batched clients: a client's copy of the span tables / the fused slerp's buffers
+__device__ __forceinline__ void client_off(SpanTables& sp, int64_t o) {
+  sp.start = cptr(sp.start, o);
+  sp.width = cptr(sp.width, o);
+  sp.kind = cptr(sp.kind, o);
+  sp.cond_idx = cptr(sp.cond_idx, o);
+  sp.packed = cptr(sp.packed, o);
+}
+__device__ __forceinline__ void client_off(SlerpFuse& sl, int64_t o) {
+  sl.real = cptr(sl.real, o);
+  sl.out = cptr(sl.out, o);
+}
+static void check_slab(const SpanTables& sp) {
+  check_slabs("span tables", sp.start, sp.width, sp.kind, sp.cond_idx, sp.packed);
+}
+
 // order-preserving float <-> uint map (for ds_max_u32 on floats); 0 is below every float
 __device__ __forceinline__ uint32_t f2ord(float f) {
   const uint32_t b = __float_as_uint(f);
@@ -294,8 +363,17 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
                                                                   float* __restrict__ out, int ldo, int rows,
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
                                                                   const uint64_t* ctr, uint32_t stream_id,
-                                                                  SlerpFuse sl) {
+                                                                  SlerpFuse sl, ClientBatch cb) {
   extern __shared__ float act_smem[];
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    logits = cptr(logits, co);
+    out = cptr(out, co);
+    ctr = cptr(ctr, co);
+    client_off(sp, co);
+    client_off(sl, co);
+    seed += (uint64_t)blockIdx.z * cb.seed_step;
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
   const int rc = min(r, rows - 1);
@@ -454,10 +532,19 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
                                                                       float* __restrict__ out, int ldo, int rows,
                                                                       SpanTables sp, float inv_tau, uint64_t seed,
                                                                       const uint64_t* ctr, uint32_t stream_id,
-                                                                      SlerpFuse sl) {
+                                                                      SlerpFuse sl, ClientBatch cb) {
   // LDS holds only the row image and the span statistics; the element -> span map (the first D
   // words of the packed table, shared by every row and L2-resident) is read next to the logits
   extern __shared__ float act_smem[];
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    logits = cptr(logits, co);
+    out = cptr(out, co);
+    ctr = cptr(ctr, co);
+    client_off(sp, co);
+    client_off(sl, co);
+    seed += (uint64_t)blockIdx.z * cb.seed_step;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = blockIdx.x;
   const int D = sp.dim, S = sp.n_span;
@@ -547,8 +634,20 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
                                                                         SpanTables sp, const int* __restrict__ col,
                                                                         const int* __restrict__ opt,
                                                                         float* __restrict__ dl, int ldg, int rows,
-                                                                        float inv_tau, float* loss, int loss_per_row) {
+                                                                        float inv_tau, float* loss, int loss_per_row,
+                                                                        ClientBatch cb) {
   extern __shared__ float act_smem[];
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    dact = cptr(dact, co);
+    act = cptr(act, co);
+    logits = cptr(logits, co);
+    col = cptr(col, co);
+    opt = cptr(opt, co);
+    dl = cptr(dl, co);
+    loss = cptr(loss, co);
+    client_off(sp, co);
+  }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = blockIdx.x;
   const int D = sp.dim, S = sp.n_span;
@@ -677,17 +776,23 @@ static void allow_big_lds(K kernel, size_t bytes) {
 void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows, SpanTables sp, float tau,
                      uint64_t seed, const uint64_t* ctr, uint32_t stream_id, SlerpFuse sl, hipStream_t stream) {
   if (rows == 0) return;
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) {
+    check_slabs("activate operand", logits, out, ctr, sl.real, sl.out);
+    check_slab(sp);
+  }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_fwd_smem_bytes(sp);
     allow_big_lds(activate_row_kernel, lds);
-    hipLaunchKernelGGL(activate_row_kernel, dim3(rows), dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out, ldo, rows,
-                       sp, 1.f / tau, seed, ctr, stream_id, sl);
+    hipLaunchKernelGGL(activate_row_kernel, dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out,
+                       ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);
     return;
   }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(activate_kernel, lds);
-  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl);
+  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, logits, ldl, out,
+                     ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);
 }
 
 // backward of the activation + fused conditional cross-entropy, one wave per row; the per-span
@@ -698,8 +803,19 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
                                                                     SpanTables sp, const int* __restrict__ col,
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
                                                                     int ldg, int rows, float inv_tau, float* loss,
-                                                                    int loss_per_row) {
+                                                                    int loss_per_row, ClientBatch cb) {
   extern __shared__ float act_smem[];
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    dact = cptr(dact, co);
+    act = cptr(act, co);
+    logits = cptr(logits, co);
+    col = cptr(col, co);
+    opt = cptr(opt, co);
+    dl = cptr(dl, co);
+    loss = cptr(loss, co);
+    client_off(sp, co);
+  }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
   const int rc = min(r, rows - 1);
@@ -822,18 +938,23 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
                        const int* col, const int* opt, float* dlogits, int ldg, int rows, float tau, float* loss,
                        int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) {
+    check_slabs("act_bwd_ce operand", dact, act, logits, col, opt, dlogits, loss);
+    check_slab(sp);
+  }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_smem_bytes(sp);
     allow_big_lds(act_bwd_ce_row_kernel, lds);
-    hipLaunchKernelGGL(act_bwd_ce_row_kernel, dim3(rows), dim3(ROW_WAVES * 64), lds, stream, dact, ldd, act, lda,
-                       logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row);
+    hipLaunchKernelGGL(act_bwd_ce_row_kernel, dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, dact, ldd, act,
+                       lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row, cb);
     return;
   }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
   allow_big_lds(act_bwd_ce_kernel, lds);
-  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + nw - 1) / nw), dim3(nw * 64), lds, stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows,
-                     1.f / tau, loss, loss_per_row);
+  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, dact, ldd, act,
+                     lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row, cb);
 }
 
 size_t activation_smem_bytes(const SpanTables& sp) {
@@ -844,7 +965,15 @@ size_t activation_smem_bytes(const SpanTables& sp) {
 // one wave per row
 __global__ __launch_bounds__(256) void slerp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
                                                     float* __restrict__ out, int rows, int cols, int ld, uint64_t seed,
-                                                    const uint64_t* ctr, uint32_t stream_id) {
+                                                    const uint64_t* ctr, uint32_t stream_id, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    real = cptr(real, co);
+    fake = cptr(fake, co);
+    out = cptr(out, co);
+    ctr = cptr(ctr, co);
+    seed += (uint64_t)blockIdx.z * cb.seed_step;
+  }
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r >= rows) return;
@@ -868,8 +997,10 @@ __global__ __launch_bounds__(256) void slerp_kernel(const float* __restrict__ re
 void launch_slerp(const float* real, const float* fake, float* out, int rows, int cols, int ld, uint64_t seed,
                   const uint64_t* ctr, uint32_t stream_id, hipStream_t stream) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(slerp_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, real, fake, out, rows, cols, ld, seed,
-                     ctr, stream_id);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("slerp operand", real, fake, out, ctr);
+  hipLaunchKernelGGL(slerp_kernel, dim3((rows + 3) / 4, 1, cb.k), dim3(256), 0, stream, real, fake, out, rows, cols, ld,
+                     seed, ctr, stream_id, cb);
 }
 
 // one workgroup per packed row.  The vector variant keeps the whole row in registers (up to
@@ -890,7 +1021,13 @@ __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, f
 
 __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                           int ldo, int rows, int cols, float lam, float* loss,
-                                                          int loss_per_row) {
+                                                          int loss_per_row, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    g = cptr(g, co);
+    out = cptr(out, co);
+    loss = cptr(loss, co);
+  }
   __shared__ float sh[8];
   const int r = blockIdx.x;
   const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
@@ -912,7 +1049,13 @@ __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restric
 
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                        int ldo, int rows, int cols, float lam, float* loss,
-                                                       int loss_per_row) {
+                                                       int loss_per_row, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    g = cptr(g, co);
+    out = cptr(out, co);
+    loss = cptr(loss, co);
+  }
   __shared__ float sh[8];
   const int r = blockIdx.x;
   const float* x = g + (size_t)r * ldg;
@@ -934,7 +1077,13 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
 // GP_V4 float4 per thread, each chunk's loads issued together
 __global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __restrict__ g, int ldg,
                                                                float* __restrict__ out, int ldo, int rows, int cols,
-                                                               float lam, float* loss, int loss_per_row) {
+                                                               float lam, float* loss, int loss_per_row, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    g = cptr(g, co);
+    out = cptr(out, co);
+    loss = cptr(loss, co);
+  }
   __shared__ float sh[8];
   const int r = blockIdx.x;
   const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
@@ -965,18 +1114,22 @@ __global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __re
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
                      int loss_per_row, hipStream_t stream) {
   if (rows == 0) return;
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("gp_scale operand", g, out, loss);
+  // (16-B alignment of client c's rows follows from client 0's: the slab stride is a multiple of 256 B)
   const bool al = cols % 4 == 0 && ldg % 4 == 0 && ldo % 4 == 0 && reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
                   reinterpret_cast<uintptr_t>(out) % 16 == 0;
   const bool v4 = al && cols <= GP_V4 * 256 * 4;
+  const dim3 grid(rows, 1, cb.k);
   if (al && !v4)
-    hipLaunchKernelGGL(gp_scale_v4_wide_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam,
-                       loss, loss_per_row);
+    hipLaunchKernelGGL(gp_scale_v4_wide_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                       loss_per_row, cb);
   else if (v4)
-    hipLaunchKernelGGL(gp_scale_v4_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
-                       loss_per_row);
+    hipLaunchKernelGGL(gp_scale_v4_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                       loss_per_row, cb);
   else
-    hipLaunchKernelGGL(gp_scale_kernel, dim3(rows), dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
-                       loss_per_row);
+    hipLaunchKernelGGL(gp_scale_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+                       loss_per_row, cb);
 }
 
 // one wave per row: y = d.v + e ; a = coef * v * ms ; loss += wloss * y
@@ -1010,6 +1163,7 @@ void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const flo
                    const float* coef, const float* wloss, float* y, float* a, int lda, int rows, int cols, float* loss,
                    hipStream_t stream) {
   if (rows == 0) return;
+  require_unbatched("d_head");
   hipLaunchKernelGGL(d_head_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, d, ldd, ms, ldms, v, e, coef, wloss, y,
                      a, lda, rows, cols, loss);
 }
@@ -1021,9 +1175,9 @@ struct ColsumBatch {
   int n_jobs;
 };
 
-__global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch bt) {
+__global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch bt, ClientBatch cb) {
   __shared__ float part[2][CS_GROUPS][CS_COLS + 1];
-  const ColsumJob jb = bt.jobs[blockIdx.y];
+  const ColsumJob jb = client_job(bt.jobs[blockIdx.y], (int64_t)blockIdx.z * cb.stride);
   const int c = blockIdx.x * CS_COLS + (threadIdx.x % CS_COLS);
   const int grp = threadIdx.x / CS_COLS;
   if ((int)(blockIdx.x * CS_COLS) >= jb.cols) return;
@@ -1069,8 +1223,13 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
   }
   bt.n_jobs = n_jobs;
   if (n_jobs == 0 || maxc == 0) return;
-  hipLaunchKernelGGL(colsum_kernel, dim3((maxc + CS_COLS - 1) / CS_COLS, n_jobs), dim3(CS_COLS * CS_GROUPS), 0, stream,
-                     bt);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1)
+    for (int i = 0; i < n_jobs; ++i)
+      check_slabs("colsum job", bt.jobs[i].a, bt.jobs[i].out, bt.jobs[i].w, bt.jobs[i].dot_v, bt.jobs[i].dot_e,
+                  bt.jobs[i].dot_out, bt.jobs[i].dot_w);
+  hipLaunchKernelGGL(colsum_kernel, dim3((maxc + CS_COLS - 1) / CS_COLS, n_jobs, cb.k), dim3(CS_COLS * CS_GROUPS), 0,
+                     stream, bt, cb);
 }
 
 // ============================================================================ batch norm + relu
@@ -1115,7 +1274,20 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
-    float momentum, float eps) {
+    float momentum, float eps, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    a = cptr(a, co);
+    gamma = cptr(gamma, co);
+    beta = cptr(beta, co);
+    out = cptr(out, co);
+    nhat = cptr(nhat, co);
+    mean = cptr(mean, co);
+    invstd = cptr(invstd, co);
+    rm = cptr(rm, co);
+    rv = cptr(rv, co);
+  }
+
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
@@ -1183,7 +1355,20 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
-    float momentum, float eps) {
+    float momentum, float eps, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    a = cptr(a, co);
+    gamma = cptr(gamma, co);
+    beta = cptr(beta, co);
+    out = cptr(out, co);
+    nhat = cptr(nhat, co);
+    mean = cptr(mean, co);
+    invstd = cptr(invstd, co);
+    rm = cptr(rm, co);
+    rv = cptr(rv, co);
+  }
+
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
@@ -1256,7 +1441,21 @@ __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ part, int n_tiles, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn,
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows,
-    int cols, int groups, float momentum, float eps) {
+    int cols, int groups, float momentum, float eps, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    a = cptr(a, co);
+    part = cptr(part, co);
+    gamma = cptr(gamma, co);
+    beta = cptr(beta, co);
+    out = cptr(out, co);
+    nhat = cptr(nhat, co);
+    mean = cptr(mean, co);
+    invstd = cptr(invstd, co);
+    rm = cptr(rm, co);
+    rv = cptr(rv, co);
+  }
+
   __shared__ float st[BNA_COLS][2][3];   // [col][batch] = (mean, invstd, biased var)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int c0 = blockIdx.x * BNA_COLS;
@@ -1329,9 +1528,11 @@ void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tile
                           const float* beta, float* out, int ldo, float* nhat, int ldn, float* mean, float* invstd,
                           float* rm, float* rv, int rows, int cols, int groups, float momentum, float eps,
                           hipStream_t stream) {
-  const dim3 grid((cols + BNA_COLS - 1) / BNA_COLS, (rows + BNA_ROWS - 1) / BNA_ROWS);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("bn_relu_apply operand", a, part, gamma, beta, out, nhat, mean, invstd, rm, rv);
+  const dim3 grid((cols + BNA_COLS - 1) / BNA_COLS, (rows + BNA_ROWS - 1) / BNA_ROWS, cb.k);
   hipLaunchKernelGGL(bn_relu_apply_kernel, grid, dim3(BNA_THREADS), 0, stream, a, lda, part, n_tiles, gamma, beta,
-                     out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps);
+                     out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb);
 }
 
 template <int COLS>
@@ -1339,10 +1540,12 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream) {
   constexpr int GROUPS = BN_THREADS / COLS;
-  const dim3 grid((cols + COLS - 1) / COLS), block(BN_THREADS);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("bn_relu_train operand", a, gamma, beta, out, nhat, mean, invstd, rm, rv);
+  const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
 #define BN_TRAIN_LAUNCH(R)                                                                                          \
   hipLaunchKernelGGL((bn_relu_train_kernel<COLS, R>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, \
-                     ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps)
+                     ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb)
   if (rows <= 4 * GROUPS) BN_TRAIN_LAUNCH(4);
   else if (rows <= 8 * GROUPS) BN_TRAIN_LAUNCH(8);
   else if (rows <= 16 * GROUPS) BN_TRAIN_LAUNCH(16);
@@ -1350,7 +1553,7 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
   else if (rows <= 64 * GROUPS) BN_TRAIN_LAUNCH(64);
   else
     hipLaunchKernelGGL((bn_relu_train_stream_kernel<COLS>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo,
-                       nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps);
+                       nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb);
 #undef BN_TRAIN_LAUNCH
 }
 
@@ -1372,7 +1575,20 @@ template <int COLS, int MAXR>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols) {
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    dr = cptr(dr, co);
+    r_ = cptr(r_, co);
+    nhat = cptr(nhat, co);
+    gamma = cptr(gamma, co);
+    invstd = cptr(invstd, co);
+    da = cptr(da, co);
+    dgamma = cptr(dgamma, co);
+    dbeta = cptr(dbeta, co);
+    dbias = cptr(dbias, co);
+  }
+
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[3 * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
@@ -1420,7 +1636,20 @@ template <int COLS>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_stream_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols) {
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    dr = cptr(dr, co);
+    r_ = cptr(r_, co);
+    nhat = cptr(nhat, co);
+    gamma = cptr(gamma, co);
+    invstd = cptr(invstd, co);
+    da = cptr(da, co);
+    dgamma = cptr(dgamma, co);
+    dbeta = cptr(dbeta, co);
+    dbias = cptr(dbias, co);
+  }
+
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[3 * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
@@ -1458,10 +1687,12 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream) {
   constexpr int GROUPS = BN_THREADS / COLS;
-  const dim3 grid((cols + COLS - 1) / COLS), block(BN_THREADS);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("bn_relu_bwd operand", dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias);
+  const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
 #define BN_BWD_LAUNCH(R)                                                                                          \
   hipLaunchKernelGGL((bn_relu_bwd_kernel<COLS, R>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, \
-                     invstd, da, ldda, dgamma, dbeta, dbias, rows, cols)
+                     invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, cb)
   if (rows <= 4 * GROUPS) BN_BWD_LAUNCH(4);
   else if (rows <= 8 * GROUPS) BN_BWD_LAUNCH(8);
   else if (rows <= 16 * GROUPS) BN_BWD_LAUNCH(16);
@@ -1469,7 +1700,7 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
   else if (rows <= 64 * GROUPS) BN_BWD_LAUNCH(64);
   else
     hipLaunchKernelGGL((bn_relu_bwd_stream_kernel<COLS>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma,
-                       invstd, da, ldda, dgamma, dbeta, dbias, rows, cols);
+                       invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, cb);
 #undef BN_BWD_LAUNCH
 }
 
@@ -1495,7 +1726,16 @@ template <int AUX>
 __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v,
                                                    const float* __restrict__ step, int64_t n4, float lr, float b1,
-                                                   float b2, float eps, float wd, uint64_t* rng_bump) {
+                                                   float b2, float eps, float wd, uint64_t* rng_bump, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    p = cptr(p, co);
+    g = cptr(g, co);
+    m = cptr(m, co);
+    v = cptr(v, co);
+    step = cptr(step, co);
+    rng_bump = cptr(rng_bump, co);
+  }
   const float t = step[0];
   const float bc1 = 1.f - powf(b1, t);
   const float bc2s = sqrtf(1.f - powf(b2, t));
@@ -1520,7 +1760,15 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
 }
 
 __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, const float* step, int64_t start,
-                                 int64_t n, float lr, float b1, float b2, float eps, float wd) {
+                                 int64_t n, float lr, float b1, float b2, float eps, float wd, ClientBatch cb) {
+  if (blockIdx.z) {
+    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+    p = cptr(p, co);
+    g = cptr(g, co);
+    m = cptr(m, co);
+    v = cptr(v, co);
+    step = cptr(step, co);
+  }
   const int64_t i = start + threadIdx.x;
   if (i >= n) return;
   const float t = step[0];
@@ -1544,8 +1792,18 @@ template <int AUX>
 __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       const float* __restrict__ step, int64_t n4, float lr, float b1,
-                                                      float b2, float eps, float wd, uint64_t* rng_bump, AdamColsum cs) {
-  adam_cs_body<AUX>((int)blockIdx.x, (int)gridDim.x, p, g, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs);
+                                                      float b2, float eps, float wd, uint64_t* rng_bump, AdamColsum cs,
+                                                      ClientBatch cb) {
+  const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  if (co) {
+    p = cptr(p, co);
+    g = cptr(g, co);
+    m = cptr(m, co);
+    v = cptr(v, co);
+    step = cptr(step, co);
+    rng_bump = cptr(rng_bump, co);
+  }
+  adam_cs_body<AUX>((int)blockIdx.x, (int)gridDim.x, p, g, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
 }
 
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
@@ -1558,16 +1816,21 @@ void launch_adam_colsum(float* p, const float* g, float* m, float* v, const floa
   const int64_t n4 = n / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
   const int grid = std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) {
+    check_slabs("adam operand", p, g, m, v, step, rng_ctr_bump);
+    check_slab(cs);
+  }
 #define FEDTGAN_ADAM_CS(AUX)                                                                                       \
-  hipLaunchKernelGGL(adam_cs_kernel<AUX>, dim3(grid), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, b2, eps, wd, \
-                     rng_ctr_bump, cs)
+  hipLaunchKernelGGL(adam_cs_kernel<AUX>, dim3(grid, 1, cb.k), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, b2, \
+                     eps, wd, rng_ctr_bump, cs, cb)
   if (g_adam_store == 2) FEDTGAN_ADAM_CS(2);
   else if (g_adam_store == 16) FEDTGAN_ADAM_CS(16);
   else FEDTGAN_ADAM_CS(0);
 #undef FEDTGAN_ADAM_CS
   if (n4 * 4 < n)
-    hipLaunchKernelGGL(adam_tail_kernel, dim3(1), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2, eps,
-                       wd);
+    hipLaunchKernelGGL(adam_tail_kernel, dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
+                       eps, wd, cb);
 }
 
 void launch_adam(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
@@ -1576,17 +1839,19 @@ void launch_adam(float* p, const float* g, float* m, float* v, const float* step
   // one float4 per thread where possible: a grid-stride loop over few workgroups keeps too few
   // loads in flight for HBM (19.5M-parameter wide-table D: 259 us at 1024 workgroups)
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slabs("adam operand", p, g, m, v, step, rng_ctr_bump);
 #define FEDTGAN_ADAM(AUX)                                                                                       \
-  hipLaunchKernelGGL(adam_kernel<AUX>, dim3(std::max(blocks, 1)), dim3(256), 0, stream, reinterpret_cast<float4*>(p), \
-                     reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v),   \
-                     step, n4, lr, b1, b2, eps, wd, rng_ctr_bump)
+  hipLaunchKernelGGL(adam_kernel<AUX>, dim3(std::max(blocks, 1), 1, cb.k), dim3(256), 0, stream,                 \
+                     reinterpret_cast<float4*>(p), reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), \
+                     reinterpret_cast<float4*>(v), step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cb)
   if (g_adam_store == 2) FEDTGAN_ADAM(2);
   else if (g_adam_store == 16) FEDTGAN_ADAM(16);
   else FEDTGAN_ADAM(0);
 #undef FEDTGAN_ADAM
   if (n4 * 4 < n)
-    hipLaunchKernelGGL(adam_tail_kernel, dim3(1), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2, eps,
-                       wd);
+    hipLaunchKernelGGL(adam_tail_kernel, dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
+                       eps, wd, cb);
 }
 
 // ============================================================================ generation decode
@@ -1764,6 +2029,7 @@ int g_decode_rows = 2;
 void launch_sample_decode(const DecodeArgs& a, hipStream_t stream) {
   const int64_t n = (int64_t)a.rows * a.n_cols;
   if (n == 0) return;
+  require_unbatched("sample_decode");
   if (g_decode_rows == 2 && a.quads && a.ecol) {
     const size_t lds = (size_t)DEC_WAVES * a.n_cols * sizeof(unsigned long long);
     hipLaunchKernelGGL(sample_decode_quad_kernel, dim3((unsigned)((a.rows + DEC_WAVES - 1) / DEC_WAVES)),
@@ -1807,13 +2073,19 @@ void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream) {
   int64_t total = 0;
   for (int j = 0; j < a.n_jobs; ++j) total += (int64_t)a.jobs[j].N * (a.jobs[j].kd + a.jobs[j].C);
   if (total == 0) return;
+  require_unbatched("gen_weight_prep");
   hipLaunchKernelGGL(gen_weight_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a);
 }
 
-__global__ void rng_bump_kernel(uint64_t* ctr) { ctr[0] += 1ull; }
+__global__ void rng_bump_kernel(uint64_t* ctr, ClientBatch cb) {
+  ctr = cptr(ctr, (int64_t)blockIdx.z * cb.stride);
+  ctr[0] += 1ull;
+}
 
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream) {
-  hipLaunchKernelGGL(rng_bump_kernel, dim3(1), dim3(1), 0, stream, ctr);
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) check_slab(ctr, "rng counter");
+  hipLaunchKernelGGL(rng_bump_kernel, dim3(1, 1, cb.k), dim3(1), 0, stream, ctr, cb);
 }
 
 }  // namespace fedtgan

@@ -878,6 +878,47 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
 }
 
+// batched clients (launch.h ClientBatch): client c's copy of every buffer of a GEMM and its Philox seed
+__device__ __forceinline__ void client_view(GemmArgs& g, int c) {
+  const int64_t o = (int64_t)c * g.cstride;
+  g.a = cptr(g.a, o);
+  g.b = cptr(g.b, o);
+  g.c = cptr(g.c, o);
+  g.bias = cptr(g.bias, o);
+  g.ms = cptr(g.ms, o);
+  g.head_coef = cptr(g.head_coef, o);
+  g.head_v = cptr(g.head_v, o);
+  g.head_a = cptr(g.head_a, o);
+  g.ws = cptr(g.ws, o);
+  g.bn_gamma = cptr(g.bn_gamma, o);
+  g.bn_beta = cptr(g.bn_beta, o);
+  g.bn_rm = cptr(g.bn_rm, o);
+  g.bn_rv = cptr(g.bn_rv, o);
+  g.rng_ctr = cptr(g.rng_ctr, o);
+  g.oh_w = cptr(g.oh_w, o);
+  g.oh_col = cptr(g.oh_col, o);
+  g.oh_opt = cptr(g.oh_opt, o);
+  g.oh_off = cptr(g.oh_off, o);
+  g.bn_part = cptr(g.bn_part, o);
+  g.tile_cnt = cptr(g.tile_cnt, o);
+  g.a16 = cptr(g.a16, o);
+  g.b16 = cptr(g.b16, o);
+  g.c16 = cptr(g.c16, o);
+  g.adam_p = cptr(g.adam_p, o);
+  g.adam_m = cptr(g.adam_m, o);
+  g.adam_v = cptr(g.adam_v, o);
+  g.adam_step = cptr(g.adam_step, o);
+  g.seed += (uint64_t)c * g.seed_step;
+}
+
+// host: every device pointer of a batched GEMM lies in client 0's slab
+static void check_slab(const GemmArgs& g) {
+  if (client_batch().k <= 1) return;
+  check_slabs("gemm operand", g.a, g.b, g.c, g.bias, g.ms, g.head_coef, g.head_v, g.head_a, g.ws, g.bn_gamma, g.bn_beta,
+              g.bn_rm, g.bn_rv, g.rng_ctr, g.oh_w, g.oh_col, g.oh_opt, g.oh_off, g.bn_part, g.tile_cnt, g.a16, g.b16,
+              g.c16, g.adam_p, g.adam_m, g.adam_v, g.adam_step);
+}
+
 // Every slab load of an output element is issued before the first is consumed (SMAX >= splits
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
 // LDS is sized per launch (gemm_smem_bytes): a GEMM whose K-slice is one burst uses one stage
@@ -885,8 +926,12 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
-                                           smem);
+  // grid.z = split-K slices x clients (client-major)
+  const int sk = (int)gridDim.z / g.nclient;
+  const int cl = (int)blockIdx.z / sk;
+  if (cl) client_view(g, cl);
+  gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk, gridDim.x, gridDim.y,
+                                           sk, smem);
 }
 
 // stage buffers a launch needs: two when a K-slice spans several bursts, else one -- unless the
@@ -913,6 +958,10 @@ template <class P1, class P2>
 __global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2, Grid3 grid1, Grid3 grid2) {
   constexpr int S1 = 2 * Cfg<false, P1::TM, P1::TM>::STAGE, S2 = 2 * Cfg<false, P2::TM, P2::TM>::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[S1 > S2 ? S1 : S2];
+  if (blockIdx.z) {
+    client_view(g1, blockIdx.z);
+    client_view(g2, blockIdx.z);
+  }
   const int n1 = grid1.x * grid1.y * grid1.z;
   int b = blockIdx.x;
   if (b < n1) {
@@ -959,6 +1008,7 @@ __device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
+  if (blockIdx.z) client_view(g, blockIdx.z);
   const size_t total = (size_t)g.M * g.N;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
@@ -980,6 +1030,10 @@ template <int SMAX>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
   __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
   __shared__ float part[4][CH_COLS];
+  if (blockIdx.z) {
+    client_view(g, blockIdx.z);
+    client_view(t, blockIdx.z);
+  }
   const int m = blockIdx.x, s = blockIdx.y;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
@@ -1030,13 +1084,23 @@ __global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, flo
                                                        float b2, float eps, float wd, uint64_t* rng_bump,
                                                        AdamColsum cs) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, TM, TM>::STAGE];
+  const int64_t co = (int64_t)blockIdx.z * g.cstride;
+  if (co) {   // batched clients: the GEMM's buffers (its Adam pointers included) and the Adam operands
+    client_view(g, blockIdx.z);
+    p = cptr(p, co);
+    gr = cptr(gr, co);
+    m = cptr(m, co);
+    v = cptr(v, co);
+    step = cptr(step, co);
+    rng_bump = cptr(rng_bump, co);
+  }
   const int nt = gd.x * gd.y * gd.z;
   const int b = blockIdx.x;
   if (b < nt) {
     gemm_tile<true, false, false, VEC, TM, TM, false, true>(g, b % gd.x, (b / gd.x) % gd.y, b / (gd.x * gd.y), gd.x,
                                                              gd.y, gd.z, smem);
   } else {
-    adam_cs_body<AUX>(b - nt, (int)gridDim.x - nt, p, gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs);
+    adam_cs_body<AUX>(b - nt, (int)gridDim.x - nt, p, gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
   }
 }
 
@@ -1044,6 +1108,10 @@ int gemm_kc(int f32) { return f32 ? Cfg<true, 64, 64>::KC : Cfg<false, 64, 64>::
 
 // tile grid, split count, K chunk and per-launch flags of one GEMM
 static dim3 gemm_prepare(GemmArgs& g) {
+  const ClientBatch& cb = client_batch();
+  g.nclient = cb.k > 1 ? cb.k : 1;
+  g.cstride = cb.k > 1 ? cb.stride : 0;
+  g.seed_step = cb.k > 1 ? cb.seed_step : 0;
   const int KC = gemm_kc(g.f32);
   const int T = g.tile == 32 ? 32 : (g.tile == 128 ? 128 : 64);   // square output tile
   g.tile = T;
@@ -1069,8 +1137,9 @@ static dim3 gemm_prepare(GemmArgs& g) {
   return dim3(tn, tm, g.splitk);
 }
 
-static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
+static void gemm_dispatch(const GemmArgs& g, dim3 grid_, hipStream_t stream) {
   const dim3 block(NT);
+  const dim3 grid(grid_.x, grid_.y, grid_.z * g.nclient);   // split-K slices x clients
   const int T = g.tile;
   const size_t lds = gemm_smem_bytes(g);
   if (g.bin) {   // bf16 operands: C = A B^T only (checked on the host)
@@ -1112,9 +1181,12 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid, hipStream_t stream) {
 static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
   if (g.chain) {     // the chained tail GEMM rides on this GEMM's reduction launch (or follows it)
     GemmArgs h = g;
-    const GemmArgs t = *g.chain;
+    GemmArgs t = *g.chain;
     h.chain = nullptr;
-    const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS), block(256);
+    t.cstride = g.cstride;      // (the tail was never prepared: it shares the head's client layout)
+    t.seed_step = g.seed_step;
+    t.nclient = g.nclient;
+    const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS, g.nclient), block(256);
     if (g.splitk <= 1 || g.red_inl) hipLaunchKernelGGL(chain_epilogue_kernel<0>, grid, block, 0, stream, h, t);
     else if (g.splitk <= 8) hipLaunchKernelGGL(chain_epilogue_kernel<8>, grid, block, 0, stream, h, t);
     else if (g.splitk <= 16) hipLaunchKernelGGL(chain_epilogue_kernel<16>, grid, block, 0, stream, h, t);
@@ -1125,14 +1197,17 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
   if (g.splitk <= 1 || g.red_inl) return;
   const size_t total = (size_t)g.M * g.N;
   int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
-  if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, dim3(blocks), dim3(256), 0, stream, g);
-  else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, dim3(blocks), dim3(256), 0, stream, g);
-  else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, dim3(blocks), dim3(256), 0, stream, g);
-  else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, dim3(blocks), dim3(256), 0, stream, g);
+  const dim3 grid(blocks, 1, g.nclient);
+  if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, grid, dim3(256), 0, stream, g);
+  else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, grid, dim3(256), 0, stream, g);
+  else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, grid, dim3(256), 0, stream, g);
+  else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, grid, dim3(256), 0, stream, g);
 }
 
 void launch_gemm(GemmArgs g, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0) return;
+  check_slab(g);
+  if (g.chain) check_slab(*g.chain);
   const dim3 grid = gemm_prepare(g);
   gemm_dispatch(g, grid, stream);
   gemm_epilogue_launch(g, stream);
@@ -1143,7 +1218,7 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
 // two launches.
 template <bool V1, bool V2>
 static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3 b, hipStream_t stream) {
-  const dim3 grid(a.x * a.y * a.z + b.x * b.y * b.z), block(NT);
+  const dim3 grid(a.x * a.y * a.z + b.x * b.y * b.z, 1, g1.nclient), block(NT);
 #define FEDTGAN_PAIR(T1, TA2, TB2)                                                                              \
   hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>>), grid, block, \
                      0, stream, g1, g2, a, b)
@@ -1164,6 +1239,10 @@ static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3
 void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
   if (g1.M <= 0 || g1.N <= 0) return launch_gemm(g2, stream);
   if (g2.M <= 0 || g2.N <= 0) return launch_gemm(g1, stream);
+  check_slab(g1);
+  check_slab(g2);
+  if (g1.chain) check_slab(*g1.chain);
+  if (g2.chain) check_slab(*g2.chain);
   const dim3 d1 = gemm_prepare(g1), d2 = gemm_prepare(g2);
   const Grid3 a{(int)d1.x, (int)d1.y, (int)d1.z}, b{(int)d2.x, (int)d2.y, (int)d2.z};
   bool fused = false;
@@ -1185,6 +1264,11 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
                       float lr, float b1, float b2, float eps, float wd, uint64_t* rng_ctr_bump,
                       const AdamColsum& cs_in, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0 || g.f32 || g.bin || g.c16 || !g.ta || g.tb || n % 4 != 0) return false;
+  check_slab(g);
+  if (client_batch().k > 1) {
+    check_slabs("adam operand", p, gr, m, v, step, rng_ctr_bump);
+    check_slab(cs_in);
+  }
   const dim3 d = gemm_prepare(g);
   if (g.splitk != 1 || (g.tile != 32 && g.tile != 64)) return false;
   g.adam_p = p + (g.c - gr);
@@ -1205,8 +1289,8 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
   const Grid3 gd{(int)d.x, (int)d.y, (int)d.z};
   const int grid = gd.x * gd.y * gd.z + std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
 #define FEDTGAN_GEMM_ADAM(V, T, AUX)                                                                               \
-  hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX>), dim3(grid), dim3(NT), 0, stream, g, gd, p, gr, m, v, step, n4, lr, \
-                     b1, b2, eps, wd, rng_ctr_bump, cs)
+  hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX>), dim3(grid, 1, g.nclient), dim3(NT), 0, stream, g, gd, p, gr, m, v,  \
+                     step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs)
 #define FEDTGAN_GEMM_ADAM_T(V, T)                                 \
   if (g_adam_store == 2) FEDTGAN_GEMM_ADAM(V, T, 2);              \
   else if (g_adam_store == 16) FEDTGAN_GEMM_ADAM(V, T, 16);       \

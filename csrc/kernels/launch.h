@@ -9,6 +9,29 @@ enum Epilogue : int { EPI_NONE = 0, EPI_LRELU_DROPOUT = 1, EPI_MASK = 2, EPI_REL
 
 struct RngArgs;
 
+// Batched clients (fed_tgan_amd/models/batched.py): K federated clients' training steps in ONE launch
+// per kernel.  Every buffer a kernel touches lives in one device arena, client c's copy exactly `stride`
+// bytes after client c-1's (identical layouts), so client c = blockIdx.z (the GEMM folds it with its
+// split-K index) offsets every pointer by c * stride and its Philox seed by c * seed_step.  k = 1 (the
+// default) is the plain single-client launch.  The host context is per thread (set by the bindings
+// around a batched engine's launches); in a batched launch every pointer must lie in client 0's slab
+// [base, base + stride), which the launchers verify (check_slab).
+struct ClientBatch {
+  int k;
+  int64_t stride;
+  uint64_t seed_step;
+  const char* base;
+};
+ClientBatch& client_batch();
+// host: throws std::runtime_error when a batched launch is handed a pointer outside client 0's slab
+void check_slab(const void* p, const char* what);
+// host: throws when the launch has no batched form
+void require_unbatched(const char* what);
+template <class... P>
+inline void check_slabs(const char* what, P... ps) {
+  (check_slab((const void*)ps, what), ...);
+}
+
 struct GemmArgs {
   const float* a;
   const float* b;
@@ -88,6 +111,10 @@ struct GemmArgs {
   // is final, the tail C2 = epi2(C B2^T + bias2) (the tail's own GemmArgs: op(A2) = this C, row-local,
   // K2 = N <= 1024) is computed in this GEMM's reduction launch, as fp32 dot products
   const struct GemmArgs* chain;
+  // batched clients (ClientBatch; set by the launchers): nclient = grid.z / splitk
+  int64_t cstride;
+  uint64_t seed_step;
+  int nclient;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -128,6 +155,7 @@ struct SampleArgs {
   uint64_t seed;
   const uint64_t* rng_ctr;
   uint32_t rng_stream;
+  ClientBatch cb;           // set by launch_sample
 };
 
 void launch_sample(const SampleArgs& a, hipStream_t stream);

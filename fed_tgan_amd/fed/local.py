@@ -34,6 +34,10 @@ class LocalGroup:
         self.slots: List[Any] = [None] * k
         self.result: Any = None
         self.failed = threading.Event()
+        # the batched multi-client engine of this process' clients (models/batched.py), if they use one:
+        # thread 0 then issues every client's training steps, the FedAvg and the generation
+        self.batch = None
+        self.lock = threading.Lock()
 
     def wait(self):
         if self.failed.is_set():
@@ -107,7 +111,17 @@ class ThreadComm(Comm):
         pass
 
     def weighted_all_reduce(self, flat, weight: float):
-        """sum_i w_i * flat_i: every rank posts (buffer, weight); rank 0 accumulates on the device."""
+        """sum_i w_i * flat_i: every rank posts (buffer, weight); rank 0 accumulates on the device.
+        Batched clients (the buffers live in one arena): thread 0 reduces over the arena on its stream,
+        the stream every client's training ran on -- no device synchronisation, no copies."""
+        b = self.g.batch
+        if b is not None and flat.is_cuda and b.owns(flat):
+            self.g.slots[self.rank] = float(weight)
+            self.g.wait()
+            if self.rank == 0:
+                b.weighted_average(list(self.g.slots))
+            self.g.wait()
+            return flat
         if flat.is_cuda:
             device_sync(flat.device)
         self.g.slots[self.rank] = (flat, float(weight))

@@ -111,6 +111,10 @@ class FedConfig:
     phase_timer: str = "events"
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
+    # several clients on one GPU (in-process emulation): "auto" runs their training steps as ONE batched
+    # launch sequence (models/batched.py) when they allow it (HIP backend, equal row counts, no fault
+    # injection); "off" keeps one engine, stream and step graph per client thread
+    batched_clients: str = "auto"
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -287,7 +291,13 @@ class FedRuntime:
         self.gen_cond = CondTables(lay, cnt.numpy())
         # ---- engine + F. initial weights
         torch.manual_seed(cfg.seed + self.rank)
-        self.engine = CTGANEngine(lay, cfg.engine, self.device, backend=cfg.backend, seed=cfg.seed * 7919 + self.rank)
+        batch = self._batch_group(lay)
+        if batch is not None:
+            self.engine = batch.engine_for(c.client_index, lay, cfg.engine, cfg.seed * 7919 + self.rank,
+                                           backend=cfg.backend)
+        else:
+            self.engine = CTGANEngine(lay, cfg.engine, self.device, backend=cfg.backend,
+                                      seed=cfg.seed * 7919 + self.rank)
         if getattr(self, "thread_local_capture", False):
             self.engine.capture_mode = "thread_local"
         if self.is_client:
@@ -302,6 +312,31 @@ class FedRuntime:
         c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
+
+    def _batch_group(self, lay):
+        """The batched multi-client engine's arena when this process' clients run as one (threads of an
+        in-process emulation on a GPU; see FedConfig.batched_clients), else None."""
+        cfg, c = self.cfg, self.comm
+        g = getattr(c, "g", None)
+        self.batched = False
+        if cfg.batched_clients == "off" or g is None or type(c).__name__ != "ThreadComm" or not self.is_client:
+            return None
+        ok = (self.device.type == "cuda" and cfg.backend in ("auto", "hip") and len(set(self.rows)) == 1 and
+              cfg.drop_client_prob <= 0 and c.client_ranks == list(range(c.world_size)) and c.n_clients > 1 and
+              cfg.mode == "fedavg")
+        if not ok:
+            if cfg.batched_clients == "on":
+                raise RuntimeError("batched_clients='on' needs a GPU, the HIP backend, equal client row counts, "
+                                   "every rank a client and no fault injection")
+            return None
+        from ..models.arena import Arena
+        from ..models.batched import BatchedClients
+        with g.lock:
+            if g.batch is None:
+                g.batch = BatchedClients.empty(c.n_clients, self.device,
+                                               Arena.estimate_slab_bytes(lay, cfg.engine, max(self.rows)))
+        self.batched = True
+        return g.batch
 
     def _initial_weights(self):
         """Step F: the clients keep their own random init (reference) or adopt the first client's;
@@ -372,7 +407,10 @@ class FedRuntime:
         differ and the whole table comes from the federator's model alone."""
         c = self.comm
         colocated = self.federator in c.client_ranks
-        samplers = c.client_ranks if (colocated and aggregated) else [self.federator]
+        # (batched clients: the federator's engine generates the whole table -- the other clients' threads
+        # issue no GPU work at all)
+        samplers = c.client_ranks if (colocated and aggregated and not getattr(self, "batched", False)) \
+            else [self.federator]
         share = None
         per = [self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0)
                for i in range(len(samplers))]
@@ -451,7 +489,15 @@ class FedRuntime:
         self._round_start[epoch] = t0
         alive = round_alive_mask(self.cfg, epoch, c.n_clients)
         with self.timer.phase("train", self.device):
-            if self.is_client and alive[c.client_index]:
+            if getattr(self, "batched", False):
+                # every client's epoch in one batched launch sequence, issued by client 0's thread
+                c.barrier()
+                if c.client_index == 0:
+                    self.engine.batch.train_epoch(self.cfg.use_graph)
+                    if self.gradflow is not None:
+                        self.gradflow.update(self.engine)
+                c.barrier()
+            elif self.is_client and alive[c.client_index]:
                 self.engine.train_epoch(self.cfg.use_graph)
                 if self.gradflow is not None:
                     self.gradflow.update(self.engine)
@@ -587,6 +633,9 @@ class FedRuntime:
 
     def save_checkpoint(self, epoch: int):
         e = self.engine
+        if getattr(self, "batched", False):
+            from ..utils.devsync import device_sync
+            device_sync(self.device)      # the state was written by client 0's stream
         state = {"epoch": epoch, "flat": e.flat.cpu(), "mG": e.mG.cpu(), "vG": e.vG.cpu(), "mD": e.mD.cpu(),
                  "vD": e.vD.cpu(), "stepG": e.stepG.cpu(), "stepD": e.stepD.cpu(), "bn_batches": e.bn_batches,
                  "round_times": self.epoch_stamps(), "cpu_rng": torch.get_rng_state(),

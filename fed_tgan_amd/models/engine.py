@@ -44,6 +44,7 @@ import numpy as np
 import torch
 
 from ..features.transformer import SpanLayout
+from .arena import TorchAlloc
 from .ctgan import Discriminator, Generator
 from .samplers import CondTables, RowIndex
 
@@ -54,9 +55,12 @@ def _ceil4(n: int) -> int:
     return (int(n) + 3) // 4 * 4
 
 
-def _padded_rows(rows: int, cols: int, device) -> torch.Tensor:
-    """[rows, cols] view of a zeroed [rows, ceil4(cols)] buffer (16-B aligned row starts)."""
-    return torch.zeros(rows, _ceil4(cols), dtype=torch.float32, device=device)[:, :cols]
+def _padded_rows(rows: int, cols: int, mem) -> torch.Tensor:
+    """[rows, cols] view of a zeroed [rows, ceil4(cols)] buffer (16-B aligned row starts); ``mem`` is an
+    allocator (models/arena.py) or a device."""
+    if not hasattr(mem, "zeros"):
+        mem = TorchAlloc(mem)
+    return mem.zeros(rows, _ceil4(cols), dtype=torch.float32)[:, :cols]
 
 
 def _ext(t: torch.Tensor, cols: int) -> torch.Tensor:
@@ -114,7 +118,7 @@ class EngineConfig:
     chain_d1: bool = True
 
 
-def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16"):
+def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
     if backend == "auto":
         backend = "hip" if device.type == "cuda" else "torch"
     if backend == "torch":
@@ -124,18 +128,21 @@ def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = 
         if device.type != "cuda":
             raise ValueError("the hip backend needs a GPU device")
         from ..ops.hip import HipOps
-        return HipOps(device, seed, precision)
+        return HipOps(device, seed, precision, mem=mem)
     raise ValueError(backend)
 
 
 class CTGANEngine:
     def __init__(self, layout: SpanLayout, cfg: EngineConfig | None = None, device="cpu", backend: str = "auto",
-                 seed: int | None = None):
+                 seed: int | None = None, mem=None):
         self.cfg = cfg = cfg or EngineConfig()
         self.layout = layout
         self.device = torch.device(device)
+        # every buffer a training step touches comes from ``mem`` (models/arena.py): plain torch memory, or a
+        # client slab of the batched multi-client engine (models/batched.py)
+        self.mem = mem or TorchAlloc(self.device)
         self.seed = int(seed if seed is not None else torch.initial_seed() % (2 ** 31))
-        self.ops = get_ops(backend, self.device, self.seed, cfg.precision)
+        self.ops = get_ops(backend, self.device, self.seed, cfg.precision, mem=self.mem)
         B, P = cfg.batch_size, cfg.pack
         if B % P:
             raise ValueError("batch_size must be a multiple of pack")
@@ -159,7 +166,7 @@ class CTGANEngine:
         self.spans = [(int(s), int(w), int(k)) for s, w, k in zip(layout.start, layout.width, layout.kind)]
         self.cond_spans = [(int(s), int(w)) for s, w in zip(layout.cond_start, layout.cond_width)]
         self.use_onehot = bool(cfg.onehot) and self.C > 0
-        self._cond_off = torch.as_tensor(np.asarray(layout.cond_offset, dtype=np.int32), device=self.device)
+        self._cond_off = self.mem.tensor(np.asarray(layout.cond_offset, dtype=np.int32))
         self._build_params()
         self._build_buffers()
         # side streams ("lanes") for independent work inside a step; the captured graph keeps the
@@ -174,6 +181,7 @@ class CTGANEngine:
         self.graphs: Dict[int, object] = {}    # steps per graph -> captured hipGraph
         self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
+        self.batch = None         # models/batched.py BatchedClients when this engine issues K clients' steps
 
     # ================================================================= parameters
     def _build_params(self):
@@ -196,7 +204,7 @@ class CTGANEngine:
         spec.sort(key=lambda t: order[t[2]])
         self.param_spec = spec
         self.wt_names, store, sizes, offsets, total = self._layout(bool(self.cfg.g_wt))
-        self.flat = torch.zeros(total, dtype=torch.float32, device=self.device)
+        self.flat = self.mem.zeros(total)
         self.p: Dict[str, torch.Tensor] = {}
         self.group_range = {}
         align = 16
@@ -211,20 +219,20 @@ class CTGANEngine:
         self.nG, self.nD = gB - gA, dB - dA
         self.flatG = self.flat[gA:gB]
         self.flatD = self.flat[dA:dB]
-        self.gradG = torch.zeros(self.nG, dtype=torch.float32, device=self.device)
-        self.gradD = torch.zeros(self.nD, dtype=torch.float32, device=self.device)
+        self.gradG = self.mem.zeros(self.nG)
+        self.gradD = self.mem.zeros(self.nD)
         self.g: Dict[str, torch.Tensor] = {}
         for (name, shape, grp), n, o, st in zip(spec, sizes, offsets, store):
             if grp == "S":
                 continue
             base = o - (gA if grp == "G" else dA)
             self.g[name] = view(self.gradG if grp == "G" else self.gradD, base, n, shape, st, name, self.wt_names)
-        self.mG = torch.zeros_like(self.gradG)
-        self.vG = torch.zeros_like(self.gradG)
-        self.mD = torch.zeros_like(self.gradD)
-        self.vD = torch.zeros_like(self.gradD)
-        self.stepG = torch.zeros(1, dtype=torch.float32, device=self.device)
-        self.stepD = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.mG = self.mem.zeros(self.nG)
+        self.vG = self.mem.zeros(self.nG)
+        self.mD = self.mem.zeros(self.nD)
+        self.vD = self.mem.zeros(self.nD)
+        self.stepG = self.mem.zeros(1)
+        self.stepD = self.mem.zeros(1)
         self.reset_parameters()
 
     def _layout(self, g_wt: bool):
@@ -358,9 +366,9 @@ class CTGANEngine:
 
     # ================================================================= buffers
     def _build_buffers(self):
-        dev, f32 = self.device, torch.float32
+        dev, f32 = self.mem, torch.float32
         B, nP = self.B, self.nP
-        z = lambda *s: torch.zeros(*s, dtype=f32, device=dev)  # noqa: E731
+        z = lambda *s: self.mem.zeros(*s, dtype=f32)  # noqa: E731
         # generator forward buffers hold two batches: rows [0, B) the D phase, [B, 2B) the G phase.
         # The paired prepare runs both through ONE M = 2B GEMM chain (BN statistics per batch);
         # the per-phase paths use the G-phase rows, which are also what the G backward reads.
@@ -400,11 +408,11 @@ class CTGANEngine:
         inv = 1.0 / nP
         # packed-row slices of the stacked D batch: interpolates, then real, then fake
         self.rows_i, self.rows_fr = slice(0, nP), slice(nP, 3 * nP)
-        self.coef3 = torch.cat([torch.ones(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).to(dev, f32)
-        self.wloss3 = torch.cat([torch.zeros(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).to(dev, f32)
-        self.coefg = torch.full((nP,), -inv, dtype=f32, device=dev)
-        self.col2 = torch.zeros(2 * B, dtype=torch.int32, device=dev)
-        self.opt2 = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+        self.coef3 = self.mem.tensor(torch.cat([torch.ones(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).float())
+        self.wloss3 = self.mem.tensor(torch.cat([torch.zeros(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).float())
+        self.coefg = self.mem.tensor(torch.full((nP,), -inv, dtype=f32))
+        self.col2 = self.mem.zeros(2 * B, dtype=torch.int32)
+        self.opt2 = self.mem.zeros(2 * B, dtype=torch.int32)
         self.col = self.col2[B:]
         self.opt = self.opt2[B:]
         self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
@@ -420,24 +428,25 @@ class CTGANEngine:
         lay = self.layout
         dev = self.device
         dev_enc = hasattr(encoded, "opt") and hasattr(encoded, "rows")
+        mk = self.mem.tensor
         if dev_enc:
             cond = cond or CondTables(lay, encoded.counts)
             rt = encoded.rows
-            t = {"data": encoded.data.to(dev), "row_offset": rt["row_offset"].to(dev),
-                 "row_count": rt["row_count"].to(dev), "rows": rt["rows"].to(dev)}
+            t = {"data": mk(encoded.data), "row_offset": mk(rt["row_offset"]), "row_count": mk(rt["row_count"]),
+                 "rows": mk(rt["rows"])}
         else:
             rows = rows or RowIndex(encoded, lay)
             cond = cond or CondTables.from_encoded(encoded, lay)
-            t = {"data": torch.as_tensor(np.ascontiguousarray(encoded, dtype=np.float32), device=dev),
-                 "row_offset": torch.as_tensor(rows.offset, dtype=torch.int64, device=dev),
-                 "row_count": torch.as_tensor(rows.count, dtype=torch.int64, device=dev),
-                 "rows": torch.as_tensor(rows.rows, dtype=torch.int64, device=dev)}
+            t = {"data": mk(np.ascontiguousarray(encoded, dtype=np.float32)),
+                 "row_offset": mk(np.asarray(rows.offset), dtype=torch.int64),
+                 "row_count": mk(np.asarray(rows.count), dtype=torch.int64),
+                 "rows": mk(np.asarray(rows.rows), dtype=torch.int64)}
         t.update({
-            "cdf_log": torch.as_tensor(cond.cdf_log, dtype=torch.float32, device=dev),
-            "cdf_emp": torch.as_tensor(cond.cdf_emp, dtype=torch.float32, device=dev),
-            "cond_offset": torch.as_tensor(lay.cond_offset, dtype=torch.int32, device=dev),
-            "cond_width": torch.as_tensor(lay.cond_width, dtype=torch.int32, device=dev),
-            "cond_start": torch.as_tensor(lay.cond_start, dtype=torch.int32, device=dev),
+            "cdf_log": mk(np.asarray(cond.cdf_log), dtype=torch.float32),
+            "cdf_emp": mk(np.asarray(cond.cdf_emp), dtype=torch.float32),
+            "cond_offset": mk(np.asarray(lay.cond_offset), dtype=torch.int32),
+            "cond_width": mk(np.asarray(lay.cond_width), dtype=torch.int32),
+            "cond_start": mk(np.asarray(lay.cond_start), dtype=torch.int32),
         })
         self.n_rows = len(encoded)
         self.tables = t
@@ -860,17 +869,21 @@ class CTGANEngine:
             return self._capture_locked(steps)
 
     def _capture_locked(self, steps: int = 1):
-        # warm up on a side stream (allocator / lazy init), then capture one step
+        # warm up on a side stream (allocator / lazy init), then capture one step.  The state snapshot is
+        # enqueued BEFORE the side stream forks from the current one, so the warm-up step cannot overtake
+        # the copies (it could, racing them, when the fork came first).  (A batched engine's warm-up step
+        # trains every client: all of their states are restored.)
+        state = self.batch.state_tensors() if self.batch is not None else \
+            [self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD]
+        snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        snap = self.flat.clone(), self.mG.clone(), self.vG.clone(), self.mD.clone(), self.vD.clone(), \
-            self.stepG.clone(), self.stepD.clone()
         with torch.cuda.stream(s):
             self._one_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         # restore state so the warm-up step does not count
-        for dst, src in zip((self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD), snap):
+        for dst, src in zip(state, snap):
             dst.copy_(src)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=self.capture_mode):

@@ -23,7 +23,7 @@ from . import native
 EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 4
 
 
-def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
+def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
     """(output tile, split-K factor) for the burst GEMM (one K-burst = ``kc`` values per row).
 
     Measured on MI355X (profiles/gemm_split_sweep_r1.txt): a split costs an epilogue launch
@@ -37,10 +37,13 @@ def _plan(M: int, N: int, K: int, kc: int = 128) -> tuple:
         deeper where that would leave more than ~8 bursts per split (wide tables: D0's K is
         137,800 -- 83 serial bursts at 13 splits); at least 2 bursts per split, fp32 slabs
         capped at ~6 MB.  (Every Intrusion shape keeps its measured split.)
+    clients: a batched multi-client launch (models/batched.py) runs every tile once per client, so the
+    grid-filling thresholds count clients x tiles (8 clients' 40 tiles need far less split-K).
     """
-    t128 = -(-M // 128) * -(-N // 128)
-    t64 = -(-M // 64) * -(-N // 64)
-    t32 = -(-M // 32) * -(-N // 32)
+    c = max(1, int(clients))
+    t128 = -(-M // 128) * -(-N // 128) * c
+    t64 = -(-M // 64) * -(-N // 64) * c
+    t32 = -(-M // 32) * -(-N // 32) * c
     bursts = -(-K // kc)
     if t128 >= 256 and K >= 256:
         return 128, 1
@@ -83,15 +86,24 @@ class HipOps:
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
     gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
 
-    def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16"):
+    def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
         self.L = native.require()
         if precision not in ("bf16", "fp32"):
             raise ValueError(f"precision must be bf16 or fp32, got {precision!r}")
         self.f32 = precision == "fp32"
         self.device = device
+        # every operand a training step's launches touch comes from ``mem`` (models/arena.py): for the
+        # batched multi-client engine that is a client slab, and the lazily sized workspaces below are then
+        # created in every slab at once
+        if mem is None:
+            from ..models.arena import TorchAlloc
+            mem = TorchAlloc(device)
+        self.mem = mem
         self.seed = int(seed) & ((1 << 62) - 1)
-        self.ctr = torch.zeros(1, dtype=torch.int64, device=device)
+        self.ctr = mem.zeros(1, dtype=torch.int64)
         self.split_override = None   # int: force the split-K factor (tuning / microbenchmarks)
+        self.batch_k = 1             # clients of the batched launches being issued (set_client_batch)
+        self.batch_plan = True       # plan tiles / split-K over clients x tiles in a batched launch (A/B knob)
         self.tile_override = None    # 32 | 64: force the output tile (tuning / microbenchmarks)
         self.lane = 0          # set by the engine while it issues work on a side stream
         self._ws: Dict[Tuple[int, bool], torch.Tensor] = {}
@@ -103,7 +115,7 @@ class HipOps:
         self.splitk_inlaunch = False
         self._spans: Dict[Tuple, Tuple[torch.Tensor, ...]] = {}
         self._dec: Dict[int, Tuple] = {}
-        self._dummy_i32 = torch.zeros(1, dtype=torch.int32, device=device)
+        self._dummy_i32 = mem.zeros(1, dtype=torch.int32)
         # BatchNorm(train) from the GEMM's per-tile partial statistics (gemm epilogue + bn_relu_apply)
         # instead of a separate full reduction over the batch (bn_relu_train).  A/B knob, default off:
         # measured slower in the step (224.6 -> 231.4 us; bn_relu_apply 11.3 us vs bn_relu_train 7.8 us,
@@ -112,6 +124,15 @@ class HipOps:
         self._bnp: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ helpers
+    def set_client_batch(self, k: int, stride: int = 0, seed_step: int = 0, base: int = 0) -> int:
+        """This thread's launches from here on run K clients at once (csrc/kernels/launch.h ClientBatch);
+        k = 1 restores plain launches.  Returns the previous k."""
+        self.batch_k = int(k)
+        return int(self.L.set_client_batch(int(k), int(stride), int(seed_step), int(base)))
+
+    def _plan_clients(self) -> int:
+        return self.batch_k if self.batch_plan else 1
+
     def reset_held(self) -> int:
         """Drop every GEMM this thread holds for pairing / a chain / the Adam launch (see gemm's
         ``group``), unlaunched; returns how many there were."""
@@ -140,7 +161,7 @@ class HipOps:
         if ws is None or ws.numel() < n:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K workspace must be sized before graph capture")
-            ws = torch.zeros(max(1 << 20, int(n * 1.25)), dtype=torch.float32, device=self.device)
+            ws = self.mem.zeros(max(1 << 20, int(n * 1.25)), dtype=torch.float32)
             self._ws[key] = ws
         return ws
 
@@ -152,7 +173,7 @@ class HipOps:
         if t is None or t.numel() < n:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("split-K tile counters must be sized before graph capture")
-            t = torch.zeros(max(n, 4096), dtype=torch.int32, device=self.device)
+            t = self.mem.zeros(max(n, 4096), dtype=torch.int32)
             self._cnt[key] = t
         return t
 
@@ -162,7 +183,7 @@ class HipOps:
         if t is None or t.numel() < n:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("BN partials buffer must be sized before graph capture")
-            t = torch.zeros(max(n, 1 << 16), dtype=torch.float32, device=self.device)
+            t = self.mem.zeros(max(n, 1 << 16), dtype=torch.float32)
             self._bnp[self.lane] = t
         return t
 
@@ -186,7 +207,7 @@ class HipOps:
             # the LDS image the activation kernels stage: [elem | kind | start | width | cidx], padded to 4
             packed = elem + kd + st + wd + cidx
             packed += [0] * (-len(packed) % 4)
-            mk = lambda v: torch.tensor(v, dtype=torch.int32, device=self.device)  # noqa: E731
+            mk = lambda v: self.mem.tensor(np.asarray(v, dtype=np.int32))  # noqa: E731
             t = (mk(st), mk(wd), mk(kd), mk(cidx), mk(packed))
             self._spans[key] = t
         return t
@@ -225,7 +246,7 @@ class HipOps:
         K = a.shape[0] if ta else a.shape[1]
         N = b.shape[0] if tb else b.shape[1]
         kc = 64 if self.f32 else 128
-        tile_p, sk = _plan(M, N, K, kc)
+        tile_p, sk = _plan(M, N, K, kc, self._plan_clients())
         tile = self.tile_override or tile or tile_p
         sk = _effective_splits(K, self.split_override or sk, kc)
         if c.dtype == torch.bfloat16:
@@ -250,7 +271,7 @@ class HipOps:
         if training:
             M, N, K = x.shape[0], W.shape[0], x.shape[1]
             kc = 64 if self.f32 else 128
-            tile, sk = _plan(M, N, K, kc)
+            tile, sk = _plan(M, N, K, kc, self._plan_clients())
             tile = self.tile_override or tile
             sk = _effective_splits(K, self.split_override or sk, kc)
             if self.bn_fused and tile in (32, 64) and sk == 1 and -(-M // tile) <= 64:
@@ -363,7 +384,7 @@ class HipOps:
     def gemm_is_split(self, M: int, N: int, K: int) -> bool:
         """Does a GEMM of this shape get a split-K reduction launch (the launch a chain tail rides on)?"""
         kc = 64 if self.f32 else 128
-        _, sk = _plan(M, N, K, kc)
+        _, sk = _plan(M, N, K, kc, self._plan_clients())
         return _effective_splits(K, self.split_override or sk, kc) > 1 and not self.splitk_inlaunch
 
     def adam(self, p, g, m, v, step, lr, b1, b2, eps, wd, last_in_step=False, jobs=None):

@@ -168,3 +168,30 @@ def test_hier_two_processes_two_clients_each(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     _check_outputs(tmp_path, 2, 3001)
     assert len(list((tmp_path / "data" / "raw").glob("Intrusion_train_client*.csv"))) == 4
+
+
+def test_gpu_emulated_clients_batched(tmp_path):
+    """Three emulated clients with equal row counts run as ONE batched engine (models/batched.py): client 0's
+    thread issues every client's steps, the FedAvg reduces over the arena, every client ends each round
+    holding the same aggregate, and the federator writes every epoch table."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    rt = run_local_emulation(_cfg(tmp_path, epochs=3), 3, backend="hip", device=DEV)
+    assert rt.batched and rt.engine.batch is not None
+    b = rt.engine.batch
+    torch.cuda.synchronize()
+    flats = [e.flat for e in b.engines]
+    assert all(torch.equal(f, flats[0]) for f in flats[1:])
+    assert bool(torch.isfinite(flats[0]).all())
+    assert all(e.bn_batches == b.engines[0].bn_batches for e in b.engines)
+    _check_outputs(tmp_path, 3, 3000)
+
+
+def test_gpu_emulated_clients_batched_off_and_unequal_rows(tmp_path):
+    """batched_clients='off', and clients with different row counts, keep the per-thread engines."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    rt = run_local_emulation(_cfg(tmp_path, epochs=1, batched_clients="off"), 2, backend="hip", device=DEV)
+    assert not rt.batched and rt.engine.batch is None
+    rt = run_local_emulation(_cfg(tmp_path / "u", epochs=1, shard_mode="dirichlet"), 2, backend="hip", device=DEV)
+    assert len(set(rt.rows)) > 1 and not rt.batched

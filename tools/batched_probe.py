@@ -1,0 +1,111 @@
+"""Epoch time of K clients on one GPU: the batched engine (one launch per kernel for all K clients)
+against one plain engine, and against K plain engines on K streams (the thread emulation's layout).
+
+    python tools/batched_probe.py [--rows 40000] [--ks 1 2 4 8] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=40000)
+    ap.add_argument("--ks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--streams", action="store_true", help="also K plain engines on K streams")
+    ap.add_argument("--plan", default="on", choices=["on", "off", "both"],
+                    help="HipOps.batch_plan: split-K / tile planning over clients x tiles (on) or per client (off)")
+    ap.add_argument("--profile-k", type=int, default=0, help="only run the batched engine with this K (profiling)")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from fed_tgan_amd.data.schema import intrusion_spec
+    from fed_tgan_amd.data.synthetic import generate
+    from fed_tgan_amd.data.table import TablePreprocessor
+    from fed_tgan_amd.features.transformer import VGMTransformer
+    from fed_tgan_amd.fed.stats import merge_categorical_metas
+    from fed_tgan_amd.models.batched import BatchedClients
+    from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+    dev = torch.device("cuda:0")
+    spec = intrusion_spec()
+    df = generate(spec, args.rows, seed=0)
+    tp = TablePreprocessor(df, "Intrusion", spec.problem_type, spec.target_column, spec.categorical_list,
+                           spec.nonnegative_list)
+    meta, vocabs, _ = merge_categorical_metas([tp.local_meta()])
+    enc = tp.encode(vocabs)
+    cat = tp.categorical_indices()
+    tr = VGMTransformer().fit(enc, cat, (), seed=0, backend="torch", device=dev)
+    tr.refit(enc, meta, vocabs, cat, (), tr.bank, tr.components)
+    X = tr.transform(enc, np.random.default_rng(0))
+    rng = np.random.default_rng(1)
+    cfg = EngineConfig()
+
+    def timed(fn, reps):
+        fn()                       # capture / warm-up
+        torch.cuda.synchronize()
+        best = 1e9
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return best
+
+    if args.profile_k:
+        bc = BatchedClients(tr.layout, cfg, dev, [100 + c for c in range(args.profile_k)], n_rows=len(X))
+        bc.engines[0].ops.batch_plan = args.plan != "off"
+        for c, e in enumerate(bc.engines):
+            e.set_training_data(X if c == 0 else X[rng.permutation(len(X))])
+        for _ in range(args.reps):
+            bc.train_epoch()
+        torch.cuda.synchronize()
+        return
+    plain = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=0)
+    plain.set_training_data(X)
+    t1 = timed(plain.train_epoch, args.reps)
+    steps = plain.steps_per_epoch
+    print(json.dumps({"mode": "plain", "k": 1, "epoch_ms": round(t1 * 1e3, 3),
+                      "step_us": round(t1 / steps * 1e6, 1)}), flush=True)
+    plans = {"on": [True], "off": [False], "both": [False, True]}[args.plan]
+    for k in args.ks:
+        for plan in plans:
+            bc = BatchedClients(tr.layout, cfg, dev, [100 + c for c in range(k)], n_rows=len(X))
+            bc.engines[0].ops.batch_plan = plan
+            for c, e in enumerate(bc.engines):
+                e.set_training_data(X if c == 0 else X[rng.permutation(len(X))])
+            tk = timed(bc.train_epoch, args.reps)
+            tagg = timed(lambda: bc.weighted_average([1.0 / k] * k), args.reps)
+            print(json.dumps({"mode": "batched", "k": k, "batch_plan": plan, "epoch_ms": round(tk * 1e3, 3),
+                              "step_us": round(tk / steps * 1e6, 1), "vs_one_client": round(tk / t1, 3),
+                              "fedavg_us": round(tagg * 1e6, 1)}), flush=True)
+            del bc
+        if args.streams and k > 1:
+            engines, streams = [], []
+            for c in range(k):
+                e = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=200 + c)
+                e.set_training_data(X)
+                e.capture_mode = "thread_local"
+                engines.append(e)
+                streams.append(torch.cuda.Stream(dev))
+
+            def run_streams():
+                for e, s in zip(engines, streams):
+                    s.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(s):
+                        e.train_epoch()
+                for s in streams:
+                    torch.cuda.current_stream(dev).wait_stream(s)
+            ts = timed(run_streams, args.reps)
+            print(json.dumps({"mode": "streams", "k": k, "epoch_ms": round(ts * 1e3, 3),
+                              "vs_one_client": round(ts / t1, 3)}), flush=True)
+            del engines
+
+
+if __name__ == "__main__":
+    main()

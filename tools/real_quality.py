@@ -56,7 +56,7 @@ def make_split(out: str, n_clients: int = 2, seed: int = 2024, bootstrap_rows: i
 
 
 def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, clients: int, gmm: str,
-              csv_epochs=None):
+              csv_epochs=None, batched: str = "auto"):
     import torch
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.fed.local import run_local_emulation
@@ -64,12 +64,14 @@ def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, c
     from fed_tgan_amd.models.engine import EngineConfig
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = FedConfig(spec=intrusion_spec(), epochs=epochs, datapath=datapath, out_dir=out, n_sample=40000,
-                    gmm_backend=gmm, seed=seed, engine=EngineConfig(precision=precision), verbose=False)
+                    gmm_backend=gmm, seed=seed, engine=EngineConfig(precision=precision), verbose=False,
+                    batched_clients=batched)
     if csv_epochs is not None:      # long runs: only the scored epochs' tables are written
         cfg.csv_epochs = sorted(set(csv_epochs))
     t0 = time.time()
     rt = run_local_emulation(cfg, clients, backend="auto", device=dev)
     return {"rows": rt.rows, "steps": rt.steps, "weights": [float(w) for w in rt.weights],
+            "batched": bool(getattr(rt, "batched", False)),
             "wall_s": time.time() - t0, "round_s": [float(x) for x in rt.round_times]}
 
 
@@ -111,6 +113,8 @@ def main():
                     help="resample every client's rows (with replacement) to this many: 20000 gives the "
                          "reference's ~40 steps per client per epoch")
     ap.add_argument("--only-scored-csv", action="store_true", help="write only the scored epochs' CSVs")
+    ap.add_argument("--batched", default="auto", choices=["auto", "on", "off"],
+                    help="FedConfig.batched_clients: the clients' steps as one batched engine, or one per thread")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     train_path, hold_path, datapath = make_split(args.out, args.clients, bootstrap_rows=args.bootstrap_rows)
@@ -120,7 +124,7 @@ def main():
         for seed in args.seeds:
             rd = os.path.join(args.out, f"run_{prec}_s{seed}")
             info = train_run(rd, datapath, prec, seed, args.epochs, args.clients, args.gmm,
-                             eval_epochs if args.only_scored_csv else None)
+                             eval_epochs if args.only_scored_csv else None, args.batched)
             sims = similarity(train_path, rd, eval_epochs)
             rec = {"precision": prec, "seed": seed, **info, "eval_epochs": eval_epochs, "avg_jsd": [s[0] for s in sims],
                    "avg_wd": [s[1] for s in sims]}
@@ -139,6 +143,8 @@ def main():
     for prec in args.precisions:
         rs = [r for r in runs if r["precision"] == prec]
         summary[prec] = {"avg_jsd_mean": np.mean([r["avg_jsd"] for r in rs], axis=0).round(4).tolist(),
+                         "avg_jsd_sem": (np.std([r["avg_jsd"] for r in rs], axis=0, ddof=1) /
+                                         np.sqrt(len(rs))).round(4).tolist() if len(rs) > 1 else None,
                          "avg_wd_mean": np.mean([r["avg_wd"] for r in rs], axis=0).round(4).tolist(),
                          "f1_gap_mean": float(np.mean([r["utility_final"]["f1_gap"] for r in rs])),
                          "eval_epochs": eval_epochs, "bootstrap_rows": args.bootstrap_rows,
