@@ -336,6 +336,7 @@ class FedRuntime:
                 g.batch = BatchedClients.empty(c.n_clients, self.device,
                                                Arena.estimate_slab_bytes(lay, cfg.engine, max(self.rows)))
         self.batched = True
+        self.batch_clients = g.batch       # (strong reference: the engine only holds a weak one)
         return g.batch
 
     def _initial_weights(self):
@@ -493,7 +494,7 @@ class FedRuntime:
                 # every client's epoch in one batched launch sequence, issued by client 0's thread
                 c.barrier()
                 if c.client_index == 0:
-                    self.engine.batch.train_epoch(self.cfg.use_graph)
+                    self.batch_clients.train_epoch(self.cfg.use_graph)
                     if self.gradflow is not None:
                         self.gradflow.update(self.engine)
                 c.barrier()

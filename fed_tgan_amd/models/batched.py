@@ -17,6 +17,7 @@ row count on every client (identical buffer shapes), consecutive engine seeds.
 """
 from __future__ import annotations
 
+import weakref
 from typing import List, Sequence
 
 import numpy as np
@@ -41,7 +42,9 @@ class BatchedClients:
         e0 = self.engines[0]
         if e0.ops.name != "hip":
             raise ValueError("batched clients need the HIP backend")
-        e0.batch = self
+        # (a weak back-reference: a strong one would make a cycle whose collection -- at an arbitrary moment,
+        # e.g. while another engine captures a graph -- destroys this group's step graphs mid-capture)
+        e0.batch = weakref.proxy(self)
         self._frozen = False
 
     @classmethod
@@ -60,7 +63,7 @@ class BatchedClients:
         e = CTGANEngine(layout, cfg, self.device, backend=backend, seed=seed, mem=self.arena.slab(c))
         self.engines[c] = e
         if c == 0:
-            e.batch = self
+            e.batch = weakref.proxy(self)
         return e
 
     # ------------------------------------------------------------------ state

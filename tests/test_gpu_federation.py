@@ -178,7 +178,7 @@ def test_gpu_emulated_clients_batched(tmp_path):
     native.require()
     rt = run_local_emulation(_cfg(tmp_path, epochs=3), 3, backend="hip", device=DEV)
     assert rt.batched and rt.engine.batch is not None
-    b = rt.engine.batch
+    b = rt.batch_clients
     torch.cuda.synchronize()
     flats = [e.flat for e in b.engines]
     assert all(torch.equal(f, flats[0]) for f in flats[1:])

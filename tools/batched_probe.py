@@ -4,6 +4,7 @@ against one plain engine, and against K plain engines on K streams (the thread e
     python tools/batched_probe.py [--rows 40000] [--ks 1 2 4 8] [--reps 5]
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -22,6 +23,11 @@ def main():
     ap.add_argument("--plan", default="on", choices=["on", "off", "both"],
                     help="HipOps.batch_plan: split-K / tile planning over clients x tiles (on) or per client (off)")
     ap.add_argument("--profile-k", type=int, default=0, help="only run the batched engine with this K (profiling)")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override (repeatable), e.g. --engine chain_d1=0")
+    ap.add_argument("--skip-plain", action="store_true")
+    ap.add_argument("--groups", type=int, nargs="*", default=[],
+                    help="also K clients as G batched groups of K/G clients on G streams (one entry per G)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -45,6 +51,10 @@ def main():
     X = tr.transform(enc, np.random.default_rng(0))
     rng = np.random.default_rng(1)
     cfg = EngineConfig()
+    for kv in args.engine:
+        key, val = kv.split("=", 1)
+        cur = getattr(cfg, key)
+        setattr(cfg, key, (val.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(val))
 
     def timed(fn, reps):
         fn()                       # capture / warm-up
@@ -68,9 +78,9 @@ def main():
         return
     plain = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=0)
     plain.set_training_data(X)
-    t1 = timed(plain.train_epoch, args.reps)
     steps = plain.steps_per_epoch
-    print(json.dumps({"mode": "plain", "k": 1, "epoch_ms": round(t1 * 1e3, 3),
+    t1 = timed(plain.train_epoch, args.reps) if not args.skip_plain else float("nan")
+    print(json.dumps({"mode": "plain", "k": 1, "epoch_ms": round(t1 * 1e3, 3), "engine": args.engine,
                       "step_us": round(t1 / steps * 1e6, 1)}), flush=True)
     plans = {"on": [True], "off": [False], "both": [False, True]}[args.plan]
     for k in args.ks:
@@ -81,10 +91,39 @@ def main():
                 e.set_training_data(X if c == 0 else X[rng.permutation(len(X))])
             tk = timed(bc.train_epoch, args.reps)
             tagg = timed(lambda: bc.weighted_average([1.0 / k] * k), args.reps)
-            print(json.dumps({"mode": "batched", "k": k, "batch_plan": plan, "epoch_ms": round(tk * 1e3, 3),
+            print(json.dumps({"mode": "batched", "k": k, "batch_plan": plan, "engine": args.engine,
+                              "epoch_ms": round(tk * 1e3, 3),
                               "step_us": round(tk / steps * 1e6, 1), "vs_one_client": round(tk / t1, 3),
                               "fedavg_us": round(tagg * 1e6, 1)}), flush=True)
             del bc
+            gc.collect()
+            torch.cuda.synchronize()
+        for G in args.groups:
+            if k % G or G <= 1:
+                continue
+            m = k // G
+            groups, streams = [], []
+            for j in range(G):
+                bc = BatchedClients(tr.layout, cfg, dev, [300 + 10 * j + c for c in range(m)], n_rows=len(X))
+                for e in bc.engines:
+                    e.set_training_data(X[rng.permutation(len(X))])
+                    e.capture_mode = "thread_local"
+                groups.append(bc)
+                streams.append(torch.cuda.Stream(dev))
+
+            def run_groups():
+                for bc, s in zip(groups, streams):
+                    s.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(s):
+                        bc.train_epoch()
+                for s in streams:
+                    torch.cuda.current_stream(dev).wait_stream(s)
+            tg = timed(run_groups, args.reps)
+            print(json.dumps({"mode": f"{G} groups x {m}", "k": k, "engine": args.engine, "epoch_ms": round(tg * 1e3, 3),
+                              "vs_one_client": round(tg / t1, 3)}), flush=True)
+            del groups
+            gc.collect()
+            torch.cuda.synchronize()
         if args.streams and k > 1:
             engines, streams = [], []
             for c in range(k):
@@ -105,6 +144,8 @@ def main():
             print(json.dumps({"mode": "streams", "k": k, "epoch_ms": round(ts * 1e3, 3),
                               "vs_one_client": round(ts / t1, 3)}), flush=True)
             del engines
+            gc.collect()
+            torch.cuda.synchronize()
 
 
 if __name__ == "__main__":

@@ -56,7 +56,7 @@ def make_split(out: str, n_clients: int = 2, seed: int = 2024, bootstrap_rows: i
 
 
 def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, clients: int, gmm: str,
-              csv_epochs=None, batched: str = "auto"):
+              csv_epochs=None, batched: str = "auto", init: str = "independent"):
     import torch
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.fed.local import run_local_emulation
@@ -65,7 +65,7 @@ def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, c
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = FedConfig(spec=intrusion_spec(), epochs=epochs, datapath=datapath, out_dir=out, n_sample=40000,
                     gmm_backend=gmm, seed=seed, engine=EngineConfig(precision=precision), verbose=False,
-                    batched_clients=batched)
+                    batched_clients=batched, init=init)
     if csv_epochs is not None:      # long runs: only the scored epochs' tables are written
         cfg.csv_epochs = sorted(set(csv_epochs))
     t0 = time.time()
@@ -113,6 +113,8 @@ def main():
                     help="resample every client's rows (with replacement) to this many: 20000 gives the "
                          "reference's ~40 steps per client per epoch")
     ap.add_argument("--only-scored-csv", action="store_true", help="write only the scored epochs' CSVs")
+    ap.add_argument("--init", default="independent", choices=["independent", "broadcast"])
+    ap.add_argument("--no-utility", action="store_true", help="skip the ML-utility evaluation of the last epoch")
     ap.add_argument("--batched", default="auto", choices=["auto", "on", "off"],
                     help="FedConfig.batched_clients: the clients' steps as one batched engine, or one per thread")
     args = ap.parse_args()
@@ -124,7 +126,7 @@ def main():
         for seed in args.seeds:
             rd = os.path.join(args.out, f"run_{prec}_s{seed}")
             info = train_run(rd, datapath, prec, seed, args.epochs, args.clients, args.gmm,
-                             eval_epochs if args.only_scored_csv else None, args.batched)
+                             eval_epochs if args.only_scored_csv else None, args.batched, args.init)
             sims = similarity(train_path, rd, eval_epochs)
             rec = {"precision": prec, "seed": seed, **info, "eval_epochs": eval_epochs, "avg_jsd": [s[0] for s in sims],
                    "avg_wd": [s[1] for s in sims]}
@@ -134,8 +136,11 @@ def main():
     last = args.epochs - 1
     fakes = [os.path.join(args.out, f"run_{r['precision']}_s{r['seed']}", "Intrusion_result",
                           f"Intrusion_synthesis_epoch_{last}.csv") for r in runs]
-    with ProcessPoolExecutor(max_workers=args.utility_workers) as ex:
-        utils = list(ex.map(utility, [train_path] * len(fakes), [hold_path] * len(fakes), fakes))
+    if args.no_utility:
+        utils = [{"diff": None, "f1_gap": float("nan")} for _ in fakes]
+    else:
+        with ProcessPoolExecutor(max_workers=args.utility_workers) as ex:
+            utils = list(ex.map(utility, [train_path] * len(fakes), [hold_path] * len(fakes), fakes))
     for r, u in zip(runs, utils):
         r["utility_final"] = u
         print(json.dumps({"precision": r["precision"], "seed": r["seed"], "f1_gap": u["f1_gap"]}), flush=True)
@@ -147,7 +152,10 @@ def main():
                                          np.sqrt(len(rs))).round(4).tolist() if len(rs) > 1 else None,
                          "avg_wd_mean": np.mean([r["avg_wd"] for r in rs], axis=0).round(4).tolist(),
                          "f1_gap_mean": float(np.mean([r["utility_final"]["f1_gap"] for r in rs])),
+                         "avg_wd_sem": (np.std([r["avg_wd"] for r in rs], axis=0, ddof=1) /
+                                        np.sqrt(len(rs))).round(4).tolist() if len(rs) > 1 else None,
                          "eval_epochs": eval_epochs, "bootstrap_rows": args.bootstrap_rows,
+                         "gmm": args.gmm, "init": args.init, "batched": args.batched,
                          "seeds": [r["seed"] for r in rs]}
     with open(os.path.join(args.out, "real_quality.json"), "w") as f:
         json.dump({"protocol": __doc__, "runs": runs, "summary": summary}, f, indent=1)

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--json", default=None, help="append the JSON lines to this file")
     ap.add_argument("--one-stream", action="store_true", help="emulated clients share one HIP stream")
+    ap.add_argument("--batched", default="auto", choices=["auto", "on", "off"],
+                    help="emulated clients as one batched engine (FedConfig.batched_clients) or one engine per thread")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override for A/B runs, e.g. --engine g_wt=1")
     args = ap.parse_args()
@@ -65,7 +67,7 @@ def main():
                     dirichlet_alpha=args.alpha, out_dir=out, n_sample=args.n_sample, backend=args.backend,
                     gmm_backend="torch", aggregation=args.aggregation, seed=args.seed,
                     engine=_engine_cfg(EngineConfig(precision=args.precision), args.engine), verbose=True,
-                    client_streams=not args.one_stream)
+                    client_streams=not args.one_stream, batched_clients=args.batched)
     t0 = time.time()
     if args.clients == 1:
         rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=dev), dev)
@@ -92,6 +94,7 @@ def main():
         lines.append(rec)
         print(json.dumps(rec), flush=True)
     summ = {"spec": spec.name, "clients": k, "shard": args.shard, "precision": args.precision,
+            "batched": bool(getattr(rt, "batched", False)),
             "rows_per_client": args.rows, "epochs": args.epochs, "weights": [round(float(w), 4) for w in rt.weights],
             "mean_sec_per_epoch_after_first": round(sum(rt.round_times[1:]) / max(len(rt.round_times) - 1, 1), 4),
             "wall_s_incl_init": round(wall, 2), "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
