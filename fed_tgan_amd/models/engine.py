@@ -545,8 +545,11 @@ class CTGANEngine:
         inp = Xs[rows]
         L = len(self.ddims)
         # two hidden layers: D1 (150 or 50 x 256 x 256) computed row by row in D0's split-K reduction launch
+        # (not in a batched multi-client step: the row-by-row chain re-reads D1's weights per row, which pays for
+        # a few dozen rows on an idle chip but not for K clients' rows -- profiles/batched_r3.md)
         chain = L == 2 and self.cfg.chain_d1 and hasattr(o, "gemm_is_split") and self.ddims[0] % 16 == 0 and \
-            self.ddims[0] <= 1024 and o.gemm_is_split(inp.shape[0], self.ddims[0], inp.shape[1])
+            self.ddims[0] <= 1024 and o.gemm_is_split(inp.shape[0], self.ddims[0], inp.shape[1]) and \
+            getattr(o, "batch_k", 1) == 1
         for i in range(L):
             head = None
             if coef is not None and i == L - 1:
@@ -655,7 +658,8 @@ class CTGANEngine:
         # two hidden layers: R1 rides on R0's split-K reduction launch, and dW1 (then the last D GEMM)
         # is held for the D Adam launch (gemm_adam_kernel)
         fuse_d = pair and L == 2 and self.cfg.fuse_d_adam and getattr(o, "gemm_adam", False) and \
-            self.ddims[0] % 16 == 0 and self.ddims[0] <= 1024 and o.gemm_is_split(self.nP, self.ddims[0], self.K1)
+            self.ddims[0] % 16 == 0 and self.ddims[0] <= 1024 and o.gemm_is_split(self.nP, self.ddims[0], self.K1) and \
+            getattr(o, "batch_k", 1) == 1
         for i in range(L):
             last_fused = fuse_d and i == L - 1
             with self._lane(1 + i % 2):

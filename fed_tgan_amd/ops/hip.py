@@ -45,7 +45,7 @@ def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
     t64 = -(-M // 64) * -(-N // 64) * c
     t32 = -(-M // 32) * -(-N // 32) * c
     bursts = -(-K // kc)
-    if t128 >= 256 and K >= 256:
+    if t128 >= 256 and K >= 256 and M >= 128:    # (a 128-row tile over < 128 rows idles its MFMA rows)
         return 128, 1
     if t64 >= 256:
         return 64, 1

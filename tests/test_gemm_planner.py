@@ -10,3 +10,14 @@ def test_split_planner_keeps_bursts_per_split_bounded():
         n = _effective_splits(K, sk, 128)
         assert tile == 32 and 1 < n <= GEMM_MAX_SPLITS
         assert -(-K // n) <= 128 * 27       # was 83 bursts per split for D0 of the wide table
+
+
+def test_planner_counts_clients_of_a_batched_launch():
+    """A batched multi-client launch fills the chip with clients x tiles: less split-K for the same shape,
+    and no 128-row tiles over fewer than 128 rows."""
+    from fed_tgan_amd.ops.hip import _plan
+    t1, s1 = _plan(150, 256, 5860)
+    t8, s8 = _plan(150, 256, 5860, clients=8)
+    assert t1 == t8 == 32 and s8 < s1
+    assert _plan(50, 5860, 256, clients=8)[0] != 128
+    assert _plan(40000, 256, 658)[0] == 128
