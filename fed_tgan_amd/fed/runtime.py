@@ -113,8 +113,12 @@ class FedConfig:
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "auto" runs their training steps as ONE batched
     # launch sequence (models/batched.py) when they allow it (HIP backend, equal row counts, no fault
-    # injection); "off" keeps one engine, stream and step graph per client thread
+    # injection) and there are at most batched_max_auto of them; "on" always when allowed; "off" keeps one
+    # engine, stream and step graph per client thread.  Measured round times, 40k-row Intrusion clients
+    # (profiles/batched_r3.md): 2 clients 23.9 ms batched vs 27.2 ms threads, 4 clients 35.3 vs 35.7,
+    # 8 clients 58.4 vs 48.8 -- the batched kernels are throughput-bound at 8 clients' work
     batched_clients: str = "auto"
+    batched_max_auto: int = 4
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -324,6 +328,8 @@ class FedRuntime:
         ok = (self.device.type == "cuda" and cfg.backend in ("auto", "hip") and len(set(self.rows)) == 1 and
               cfg.drop_client_prob <= 0 and c.client_ranks == list(range(c.world_size)) and c.n_clients > 1 and
               cfg.mode == "fedavg")
+        if ok and cfg.batched_clients == "auto" and c.n_clients > cfg.batched_max_auto:
+            return None
         if not ok:
             if cfg.batched_clients == "on":
                 raise RuntimeError("batched_clients='on' needs a GPU, the HIP backend, equal client row counts, "
