@@ -250,6 +250,7 @@ def run_rank(args) -> None:
                        "data_plane": comm.data_backend if comm.dist_active else "none"},
             "avg_jsd": avg_jsd, "avg_wd": avg_wd, "epochs_trained": cfg.epochs,
             "phase_s": {k: round(v / max(args.steps, 1), 6) for k, v in rt.timer.totals.items()},
+            "init_s": {k: round(v, 3) for k, v in rt.init_times.items()},    # cumulative, untimed
         }
         if consistency is not None:
             rec["consistency"] = consistency

@@ -110,6 +110,22 @@ class TablePreprocessor:
             df, categorical = split_dates(df, self.date_columns, categorical)
         self.categorical_list = categorical
         self.df = df
+        self._cat_cache: Dict[str, tuple] = {}
+
+    def _cat_strings(self, c: str):
+        """Column ``c`` as ``(codes, labels)`` with ``labels[codes]`` == ``df[c].astype(str)``.
+
+        Factorises the raw column once and stringifies only its distinct values (a few dozen) instead
+        of every row; ``labels`` are in first-appearance order, like the hash pass of ``value_counts``.
+        Cached: ``local_meta`` and ``encode`` both need it."""
+        hit = self._cat_cache.get(c)
+        if hit is None:
+            codes, uniq = pd.factorize(self.df[c], use_na_sentinel=False)
+            strs = pd.Index(uniq).astype(str)
+            remap, labels = pd.factorize(strs)          # distinct raw values that print the same merge
+            hit = (remap[codes], np.asarray(labels, dtype=object))
+            self._cat_cache[c] = hit
+        return hit
 
     # ------------------------------------------------------------------ meta
     def local_meta(self) -> dict:
@@ -117,7 +133,9 @@ class TablePreprocessor:
         for pos, c in enumerate(self.df.columns):
             entry: dict = {"column_name": c}
             if c in self.categorical_list:
-                counts = self.df[c].astype(str).value_counts()
+                codes, labels = self._cat_strings(c)
+                n = np.bincount(codes, minlength=len(labels))
+                counts = pd.Series(n, index=pd.Index(labels, dtype=object)).sort_values(ascending=False)
                 entry["type"] = CATEGORICAL
                 entry["size"] = int(len(counts))
                 entry["i2s"] = {str(k): int(v) for k, v in counts.items()}
@@ -146,7 +164,8 @@ class TablePreprocessor:
         cursor = 0
         for j, c in enumerate(self.df.columns):
             if c in self.categorical_list:
-                out[:, j] = vocabs[cursor].transform(self.df[c].astype(str).to_numpy())
+                codes, labels = self._cat_strings(c)
+                out[:, j] = vocabs[cursor].transform(labels)[codes]
                 cursor += 1
             else:
                 out[:, j] = pd.to_numeric(self.df[c]).to_numpy(dtype=np.float64)

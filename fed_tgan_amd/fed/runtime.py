@@ -253,6 +253,7 @@ class FedRuntime:
         self.cat_idx = cat_idx
         if self.is_fed:
             self._write_meta_artifacts()
+        self.init_times = {"meta": time.time() - t0}
         _log(cfg, self.rank, f"[init] categorical merge done ({time.time() - t0:.2f}s)")
         # ---- B. local VGMs -> global VGM
         info = None
@@ -272,6 +273,7 @@ class FedRuntime:
         self.bank = VGMBank.from_dict(gbank)
         self.components = np.asarray(comps, dtype=bool)
         self.e_hat = np.asarray(e_hat)
+        self.init_times["vgm"] = time.time() - t0
         _log(cfg, self.rank, f"[init] global VGM fitted ({time.time() - t0:.2f}s)")
         # ---- C. refit + encode
         self.transformer = VGMTransformer().refit(self.encoded, merged, self.vocabs, cat_idx, (), self.bank,
@@ -279,6 +281,7 @@ class FedRuntime:
         lay = self.transformer.layout
         if self.is_client:
             self.train_matrix = self._encode_training_table()
+        self.init_times["encode"] = time.time() - t0
         # ---- D. weights
         if cfg.aggregation == "uniform":
             self.weights = uniform_weights(c.n_clients)
@@ -312,8 +315,10 @@ class FedRuntime:
         if cfg.resume:
             self.load_checkpoint()
         self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
+        self.init_times["engine"] = time.time() - t0
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
         c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
+        self.init_times["total"] = time.time() - t0     # cumulative seconds at the end of each stage
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
 
@@ -379,6 +384,14 @@ class FedRuntime:
         mdir = os.path.join(self.cfg.out_dir, "models")
         os.makedirs(mdir, exist_ok=True)
         dump_meta_json(self.global_meta, os.path.join(mdir, f"{self.name}.json"))
+
+    def write_label_encoders(self):
+        """``models/label_encoders_{name}.pickle`` (`Server/dtds/distributed.py:679-684`).
+
+        Written after training, not during initialisation: building sklearn ``LabelEncoder`` objects
+        imports scikit-learn (0.5-0.9 s), which sat on the critical path of every run's start."""
+        mdir = os.path.join(self.cfg.out_dir, "models")
+        os.makedirs(mdir, exist_ok=True)
         les = [{"column_name": v.column_name, "label_encoder": v.to_sklearn()} for v in self.vocabs]
         with open(os.path.join(mdir, f"label_encoders_{self.name}.pickle"), "wb") as f:
             pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
@@ -585,6 +598,7 @@ class FedRuntime:
             self.gradflow.save_csv(os.path.join(d, "grad_flow.csv"))
             self.gradflow.plot(d)
         if self.is_fed:
+            self.write_label_encoders()
             self.write_timestamps()
             if cfg.dump_real:
                 self.merge_real_shards()
