@@ -117,6 +117,37 @@ class VGMBank:
         return np.concatenate(out) if out else np.zeros(0)
 
 
+def sample_pool(banks: Sequence[VGMBank], n_per_client: Sequence[int], rng: np.random.Generator, device,
+                seed: int):
+    """Every client's VGM sampled into one pooled tensor on ``device``: [n_cont, sum(n_per_client)],
+    client i's ``n_per_client[i]`` draws of column j in columns ``off[i]:off[i+1]`` of row j, grouped
+    by component like ``sklearn``'s ``sample`` / :meth:`VGMBank.sample_column`.
+
+    Component counts are multinomial draws on the host (``n_cont x K x 10`` numbers); the normals are
+    drawn on the device from a generator seeded with ``seed``.  Returns (pool, offsets)."""
+    import torch
+    n_cont = banks[0].n
+    nk = banks[0].k
+    off = np.concatenate([[0], np.cumsum(n_per_client)]).astype(np.int64)
+    counts = np.zeros((n_cont, len(banks), nk), dtype=np.int64)
+    for j in range(n_cont):
+        for i, b in enumerate(banks):
+            counts[j, i] = rng.multinomial(int(n_per_client[i]), b.weights[j])
+    mean = np.stack([b.means for b in banks], axis=1)                      # [n_cont, K, nk]
+    std = np.sqrt(np.stack([b.covariances for b in banks], axis=1))
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    seg = torch.arange(n_cont * len(banks) * nk, device=dev)
+    idx = torch.repeat_interleave(seg, torch.as_tensor(counts.reshape(-1), device=dev),
+                                  output_size=int(n_cont * off[-1]))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(int(seed))
+    z = torch.randn(int(n_cont * off[-1]), generator=gen, dtype=torch.float64, device=dev)
+    m = torch.as_tensor(mean.reshape(-1), device=dev)
+    sd = torch.as_tensor(std.reshape(-1), device=dev)
+    pool = (m[idx] + sd[idx] * z).view(n_cont, int(off[-1]))
+    return pool, off.tolist()
+
+
 def bank_from_sklearn(models: Sequence) -> VGMBank:
     return VGMBank(
         wc_a=np.stack([m.weight_concentration_[0] for m in models]),
@@ -143,8 +174,9 @@ def fit_vgm_sklearn(columns: List[np.ndarray], n_clusters: int = N_CLUSTERS, see
     return bank_from_sklearn(models)
 
 
-def fit_vgm(columns: List[np.ndarray], backend: str = "sklearn", n_clusters: int = N_CLUSTERS,
+def fit_vgm(columns, backend: str = "sklearn", n_clusters: int = N_CLUSTERS,
             seed: int | None = None, device=None) -> VGMBank:
+    """columns: a list of 1-D samples, one per column, or (torch backend) a [n_cols, n] tensor."""
     if len(columns) == 0:
         z = np.zeros((0, n_clusters))
         return VGMBank(z, z, z, z, z, z)

@@ -43,14 +43,19 @@ TOL = 1e-3
 MAX_ITER = 100
 
 
-def _pad(columns: Sequence[np.ndarray], device, dtype):
+def _pad(columns, device, dtype):
+    """Columns -> zero-padded [n_cols, n] values and 0/1 weights on ``device`` (one host->device copy
+    each); a [n_cols, n] tensor is taken as already padded, every entry live."""
+    if isinstance(columns, torch.Tensor):
+        X = columns.to(device=device, dtype=dtype)
+        return X, torch.ones_like(X)
     n = max(len(c) for c in columns)
-    X = torch.zeros(len(columns), n, dtype=dtype, device=device)
-    W = torch.zeros(len(columns), n, dtype=dtype, device=device)
+    Xh = np.zeros((len(columns), n), dtype=np.float64)
+    Wh = np.zeros((len(columns), n), dtype=np.float64)
     for j, c in enumerate(columns):
-        X[j, :len(c)] = torch.as_tensor(np.asarray(c, dtype=np.float64), dtype=dtype, device=device)
-        W[j, :len(c)] = 1.0
-    return X, W
+        Xh[j, :len(c)] = np.asarray(c, dtype=np.float64)
+        Wh[j, :len(c)] = 1.0
+    return (torch.from_numpy(Xh).to(device=device, dtype=dtype), torch.from_numpy(Wh).to(device=device, dtype=dtype))
 
 
 def _kmeans_seed(X: torch.Tensor, W: torch.Tensor, k: int, gen: torch.Generator) -> torch.Tensor:
@@ -206,7 +211,7 @@ def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: fl
                    dof=o[:, 4], covariances=o[:, 5])
 
 
-def fit_vgm_torch(columns: Sequence[np.ndarray], n_clusters: int = 10, seed: int | None = None, device=None,
+def fit_vgm_torch(columns, n_clusters: int = 10, seed: int | None = None, device=None,
                   max_iter: int = MAX_ITER, tol: float = TOL, use_hip: bool | None = None,
                   init_centers=None, fused: bool = True) -> VGMBank:
     """init_centers: optional [n_cols, K] k-means centres (original units) to start from instead of

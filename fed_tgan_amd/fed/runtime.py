@@ -34,6 +34,7 @@ import dataclasses
 import json
 import os
 import pickle
+import threading
 import time
 from typing import Dict, List, Optional
 
@@ -47,14 +48,15 @@ from ..data.schema import DatasetSpec
 from ..data.synthetic import generate, shard
 from ..data.table import TablePreprocessor, dump_meta_json
 from ..data.vocab import CategoryVocab
-from ..features.gmm import VGMBank, fit_vgm
+from ..features.gmm import VGMBank, fit_vgm, sample_pool
 from ..features.transformer import VGMTransformer
 from ..models.engine import CTGANEngine, EngineConfig
 from ..models.samplers import CondTables
 from ..parallel.comm import Comm
 from ..utils.metrics import MetricsLog, PhaseTimer
 from ..utils.devsync import PendingHost, stream_sync
-from .stats import aggregation_weights, continuous_client_distances, merge_categorical_metas, uniform_weights
+from .stats import (aggregation_weights, continuous_client_distances, continuous_client_distances_device,
+                    merge_categorical_metas, uniform_weights)
 
 
 @dataclasses.dataclass
@@ -126,6 +128,13 @@ def _log(cfg: FedConfig, rank: int, *msg):
         print(*msg, flush=True)
 
 
+def _warm_device(device):
+    x = torch.arange(64, device=device, dtype=torch.int64).flip(0)
+    torch.where(x > 3, torch.argsort(x.view(8, 8), dim=0, stable=True).view(-1), x)
+    torch.sort(x.double()).values.cumsum(0)
+    torch.cuda.synchronize(device)
+
+
 def federate_gmm(banks: List[VGMBank], rows: List[int], cfg: FedConfig, device) -> tuple:
     """Federator side of ``uniform_continuous_gmm`` (`Server/dtds/distributed.py:689-765`).
 
@@ -139,6 +148,12 @@ def federate_gmm(banks: List[VGMBank], rows: List[int], cfg: FedConfig, device) 
         n_total = cfg.gmm_pool_cap
     share = [float(r) / float(np.sum(rows)) for r in rows]
     n_cont = banks[0].n
+    if cfg.gmm_backend == "torch" and n_cont:
+        # the pool stays on the device: sampled there, W1 distances and the global fit read it in place
+        pool, off = sample_pool(banks, [int(n_total * sh) for sh in share], rng, device, cfg.seed + 4242)
+        e_hat = continuous_client_distances_device(pool, off)
+        gb = fit_vgm(pool, backend="torch", seed=cfg.seed, device=device)
+        return gb.to_dict(), gb.components().tolist(), e_hat
     pooled, per_client = [], [[] for _ in banks]
     for j in range(n_cont):
         parts = [b.sample_column(j, int(n_total * share[i]), rng) for i, b in enumerate(banks)]
@@ -232,6 +247,12 @@ class FedRuntime:
         cfg, c = self.cfg, self.comm
         spec = cfg.spec
         t0 = time.time()
+        warm = None
+        if self.device.type == "cuda":
+            # HIP context creation and the first loads of torch's sort / select code objects take
+            # ~0.3 s; they overlap the pandas work of stage A on a side thread
+            warm = threading.Thread(target=_warm_device, args=(self.device,), daemon=True)
+            warm.start()
         # ---- A. categorical meta
         self.table = None
         if self.is_client:
@@ -253,6 +274,8 @@ class FedRuntime:
         self.cat_idx = cat_idx
         if self.is_fed:
             self._write_meta_artifacts()
+        if warm is not None:
+            warm.join()
         self.init_times = {"meta": time.time() - t0}
         _log(cfg, self.rank, f"[init] categorical merge done ({time.time() - t0:.2f}s)")
         # ---- B. local VGMs -> global VGM
@@ -297,7 +320,12 @@ class FedRuntime:
         c.all_reduce_cpu(cnt)
         self.gen_cond = CondTables(lay, cnt.numpy())
         # ---- engine + F. initial weights
-        torch.manual_seed(cfg.seed + self.rank)
+        # this process' generators only: torch.manual_seed seeds every visible GPU, and counting them
+        # initialises the SMI library (0.1 s)
+        torch.random.default_generator.manual_seed(cfg.seed + self.rank)
+        if self.device.type == "cuda":
+            with torch.cuda.device(self.device):
+                torch.cuda.manual_seed(cfg.seed + self.rank)
         batch = self._batch_group(lay)
         if batch is not None:
             self.engine = batch.engine_for(c.client_index, lay, cfg.engine, cfg.seed * 7919 + self.rank,

@@ -58,6 +58,33 @@ def wasserstein_1d(u: np.ndarray, v: np.ndarray) -> float:
     return float(np.sum(np.abs(cu - cv) * deltas))
 
 
+def wasserstein_1d_rows(u, v, u_sorted: bool = False):
+    """Row-wise W1 on the device: ``u`` [R, N], ``v`` [R, M] torch tensors (one empirical
+    distribution per row, unit weights) -> [R] float64.  The same CDF-difference integral as
+    :func:`wasserstein_1d`, batched over rows (sort + merged grid + two ``searchsorted``)."""
+    import torch
+    u = u.double() if u_sorted else torch.sort(u.double(), dim=1).values
+    v = torch.sort(v.double(), dim=1).values
+    allv = torch.sort(torch.cat([u, v], dim=1), dim=1).values
+    grid = allv[:, :-1].contiguous()
+    cu = torch.searchsorted(u, grid, right=True).double() / u.shape[1]
+    cv = torch.searchsorted(v, grid, right=True).double() / v.shape[1]
+    return ((cu - cv).abs() * torch.diff(allv, dim=1)).sum(1)
+
+
+def continuous_client_distances_device(pooled, offsets: Sequence[int]) -> np.ndarray:
+    """:func:`continuous_client_distances` for a device pool: ``pooled`` [n_cont, N] holds client i's
+    samples in columns ``offsets[i]:offsets[i+1]`` of every row."""
+    import torch
+    k = len(offsets) - 1
+    if pooled.shape[0] == 0:
+        return np.zeros((k, 0))
+    us = torch.sort(pooled, dim=1).values
+    e = torch.stack([wasserstein_1d_rows(us, pooled[:, offsets[i]:offsets[i + 1]], u_sorted=True)
+                     for i in range(k)])
+    return normalise_over_clients(e.cpu().numpy(), zero_fill_uniform=False)
+
+
 def normalise_over_clients(dist: np.ndarray, zero_fill_uniform: bool) -> np.ndarray:
     """dist: [K, n_cols]. Divide each column by its sum over clients."""
     out = dist.astype(np.float64).copy()

@@ -24,6 +24,59 @@ def test_w1_matches_scipy():
         assert wasserstein_1d(u, v) == pytest.approx(wasserstein_distance(u, v), rel=1e-10)
 
 
+def _device_pool_case(dev):
+    import torch
+    from fed_tgan_amd.fed.stats import continuous_client_distances, continuous_client_distances_device
+    rng = np.random.default_rng(2)
+    parts = [[rng.normal(i, 1 + j, size=n) for j in range(3)] for i, n in enumerate((500, 1300, 40))]
+    pooled = [np.concatenate([p[j] for p in parts]) for j in range(3)]
+    off = np.concatenate([[0], np.cumsum([len(p[0]) for p in parts])]).tolist()
+    want = continuous_client_distances(pooled, parts)
+    got = continuous_client_distances_device(torch.as_tensor(np.stack(pooled), device=dev), off)
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12)
+
+
+def test_w1_rows_and_device_distances_match_numpy():
+    """The batched device W1 (sort + merged grid, fed/stats.py) = the numpy/SciPy one per row."""
+    import torch
+    from fed_tgan_amd.fed.stats import wasserstein_1d_rows
+    rng = np.random.default_rng(3)
+    u, v = rng.normal(size=(4, 900)), rng.gamma(2.0, size=(4, 333))
+    got = wasserstein_1d_rows(torch.as_tensor(u), torch.as_tensor(v)).numpy()
+    np.testing.assert_allclose(got, [wasserstein_distance(a, b) for a, b in zip(u, v)], rtol=1e-10)
+    _device_pool_case("cpu")
+
+
+@pytest.mark.gpu
+def test_device_distances_on_gpu():
+    _device_pool_case("cuda:0")
+
+
+def test_sample_pool_layout_and_moments():
+    """sample_pool: client i's draws of column j sit in columns off[i]:off[i+1] of row j, with that
+    client's mixture moments."""
+    from fed_tgan_amd.features.gmm import VGMBank, sample_pool
+    k = 10
+
+    def bank(mu):
+        a = np.full((2, k), 1.0)
+        w = np.zeros((2, k))
+        w[:, :2] = [[5.0, 1e-9], [2.0, 2.0]]
+        means = np.zeros((2, k))
+        means[:, 0], means[:, 1] = mu, mu + 4
+        return VGMBank(w + 1e-12, a, a, means, a + 5, np.full((2, k), 0.25))
+    banks = [bank(0.0), bank(10.0)]
+    pool, off = sample_pool(banks, [20000, 5000], np.random.default_rng(0), "cpu", seed=1)
+    assert tuple(pool.shape) == (2, 25000) and off == [0, 20000, 25000]
+    p = pool.numpy()
+    for i, b in enumerate(banks):
+        for j in range(2):
+            x = p[j, off[i]:off[i + 1]]
+            w = b.weights[j]
+            mean = float(np.sum(w * b.means[j]))
+            assert abs(x.mean() - mean) < 0.05, (i, j)
+
+
 def _meta(counts):
     return {"columns": [{"column_name": "c", "type": "categorical", "i2s": counts},
                         {"column_name": "x", "type": "continous"}]}
