@@ -564,6 +564,77 @@ void bn_relu_apply(const Tensor& a, const Tensor& part, int64_t n_tiles, const T
                                 (int)groups, (float)momentum, (float)eps, cur_stream());
 }
 
+// Linear -> BatchNorm(train) -> ReLU, one launch (kernels/bn_fused.hip).  x: the dense input columns
+// [groups * rpg, K]; W: [N, K] (any strides); one-hot block as for gemm (oh_w [N, C], or [C, N] with
+// oh_trans); stat: >= groups * 2 * N floats; cnt: >= ceil(N / 16) zeroed int32 counters.
+void linear_bn_relu_colown(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, const Tensor& gamma,
+                           const Tensor& beta, const Tensor& out, const Tensor& nhat, const Tensor& mean,
+                           const Tensor& invstd, const Tensor& rm, const Tensor& rv, double momentum, double eps,
+                           int64_t groups, const optional<Tensor>& oh_w, const optional<Tensor>& oh_col,
+                           const optional<Tensor>& oh_opt, const optional<Tensor>& oh_off, bool oh_trans,
+                           const Tensor& stat, const Tensor& cnt) {
+  check_f32_2d(x, "x");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.dim() == 2, "colown: w must be a 2-D fp32 GPU tensor");
+  check_f32_2d(out, "out");
+  check_f32_2d(nhat, "nhat");
+  const int64_t rows = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(groups == 1 || groups == 2, "colown: 1 or 2 batches");
+  TORCH_CHECK(rows >= 2 && rows % groups == 0, "colown: rows must split evenly");
+  TORCH_CHECK(K >= 1 && w.size(1) == K, "colown: w is ", w.sizes(), ", x has K = ", K);
+  TORCH_CHECK(out.size(0) == rows && out.size(1) == N && nhat.size(0) == rows && nhat.size(1) == N, "colown: out / nhat");
+  TORCH_CHECK(gamma.numel() == N && beta.numel() == N && rm.numel() == N && rv.numel() == N && gamma.is_contiguous() &&
+                  beta.is_contiguous() && rm.is_contiguous() && rv.is_contiguous(), "colown: BN vectors");
+  TORCH_CHECK(mean.is_contiguous() && invstd.is_contiguous() && mean.numel() == groups * N &&
+                  invstd.numel() == groups * N, "colown: mean/invstd must be contiguous [groups, cols]");
+  const int64_t rpg = rows / groups;
+  TORCH_CHECK(fedtgan::colown_smem_bytes((int)K, (int)rpg) <= 64 * 1024, "colown: batch x K too large for LDS");
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.is_contiguous() && stat.numel() >= groups * 2 * N,
+              "colown: stat");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous() && cnt.numel() >= (N + 15) / 16,
+              "colown: cnt");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "colown: bias");
+  fedtgan::ColOwnArgs g{};
+  g.x = cfp(x);
+  g.ldx = (int)ld_of(x);
+  g.w = w.data_ptr<float>();
+  g.w_sn = w.stride(0);
+  g.w_sk = w.stride(1);
+  g.bias = optp<float>(bias);
+  if (oh_w.has_value() && oh_w->defined()) {
+    TORCH_CHECK(oh_col.has_value() && oh_opt.has_value() && oh_off.has_value(), "colown: one-hot needs col/opt/off");
+    TORCH_CHECK(oh_col->numel() == rows && oh_opt->numel() == rows && oh_col->scalar_type() == at::kInt &&
+                    oh_opt->scalar_type() == at::kInt && oh_off->scalar_type() == at::kInt, "colown: one-hot indices");
+    TORCH_CHECK(oh_w->scalar_type() == at::kFloat && oh_w->dim() == 2 && oh_w->size(oh_trans ? 1 : 0) == N,
+                "colown: one-hot block");
+    g.oh_w = oh_w->data_ptr<float>();
+    g.oh_sn = oh_trans ? oh_w->stride(1) : oh_w->stride(0);
+    g.oh_sc = oh_trans ? oh_w->stride(0) : oh_w->stride(1);
+    g.oh_col = oh_col->data_ptr<int>();
+    g.oh_opt = oh_opt->data_ptr<int>();
+    g.oh_off = oh_off->data_ptr<int>();
+  }
+  g.gamma = cfp(gamma);
+  g.beta = cfp(beta);
+  g.out = fp(out);
+  g.ldo = (int)ld_of(out);
+  g.nhat = fp(nhat);
+  g.ldn = (int)ld_of(nhat);
+  g.mean = fp(mean);
+  g.invstd = fp(invstd);
+  g.rm = fp(rm);
+  g.rv = fp(rv);
+  g.stat = fp(stat);
+  g.cnt = reinterpret_cast<unsigned*>(cnt.data_ptr<int>());
+  g.rpg = (int)rpg;
+  g.groups = (int)groups;
+  g.K = (int)K;
+  g.N = (int)N;
+  g.momentum = (float)momentum;
+  g.eps = (float)eps;
+  const bool vec = (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && g.ldx % 4 == 0;
+  fedtgan::launch_linear_bn_relu_colown(g, vec, cur_stream());
+}
+
 void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Tensor& gamma, const Tensor& invstd,
                  const Tensor& da, const Tensor& dgamma, const Tensor& dbeta, const optional<Tensor>& dbias) {
   check_f32_2d(dr, "dr");
@@ -1008,6 +1079,11 @@ TORCH_LIBRARY(fedtgan, m) {
       "colsum_ex(Tensor[] srcs, Tensor?[] outs, Tensor?[] w, Tensor?[] dot_v, Tensor?[] dot_e, Tensor?[] dot_out, "
       "Tensor?[] dot_w) -> ()");
   m.def(
+      "linear_bn_relu_colown(Tensor x, Tensor w, Tensor? bias, Tensor gamma, Tensor beta, Tensor(a!) out, "
+      "Tensor(b!) nhat, Tensor(c!) mean, Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, "
+      "int groups, Tensor? oh_w, Tensor? oh_col, Tensor? oh_opt, Tensor? oh_off, bool oh_trans, Tensor(g!) stat, "
+      "Tensor(h!) cnt) -> ()");
+  m.def(
       "bn_relu_train(Tensor a, Tensor gamma, Tensor beta, Tensor(a!) out, Tensor(b!) nhat, Tensor(c!) mean, "
       "Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
   m.def(
@@ -1064,6 +1140,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("bn_relu_train", &bn_relu_train);
   m.impl("bn_relu_bwd", &bn_relu_bwd);
   m.impl("bn_relu_apply", &bn_relu_apply);
+  m.impl("linear_bn_relu_colown", &linear_bn_relu_colown);
   m.impl("adam", &adam);
   m.impl("adam_cs", &adam_cs);
   m.impl("sample_decode", &sample_decode);

@@ -253,6 +253,41 @@ void launch_bn_relu_train(const float* a, int lda, const float* gamma, const flo
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream);
 
+// Linear -> BatchNorm(train) -> ReLU in one launch by column ownership (kernels/bn_fused.hip): a
+// workgroup owns 16 output columns of one batch.  x [groups * rpg, K] (unit column stride),
+// W(n, k) = w[n * w_sn + k * w_sk]; the optional one-hot block adds oh_w[n * oh_sn + j * oh_sc] with
+// j = oh_off[oh_col[r]] + oh_opt[r]; stat [groups][2][N] and cnt [ceil(N / 16)] (zero between launches)
+// carry the batch statistics to the running-stat update when groups == 2.
+struct ColOwnArgs {
+  const float* x;
+  int ldx;
+  const float* w;
+  int64_t w_sn, w_sk;
+  const float* bias;
+  const float* oh_w;
+  int64_t oh_sn, oh_sc;
+  const int* oh_col;
+  const int* oh_opt;
+  const int* oh_off;
+  const float* gamma;
+  const float* beta;
+  float* out;
+  int ldo;
+  float* nhat;
+  int ldn;
+  float* mean;
+  float* invstd;
+  float* rm;
+  float* rv;
+  float* stat;
+  unsigned* cnt;
+  int rpg, groups, K, N;
+  float momentum, eps;
+  int64_t cstride;   // set by the launcher (batched clients)
+};
+size_t colown_smem_bytes(int K, int rpg);
+void launch_linear_bn_relu_colown(ColOwnArgs g, bool vec, hipStream_t stream);
+
 // BatchNorm(train) + ReLU from the GEMM's per-tile partial statistics (kernels/ctgan_ops.hip)
 void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tiles, const float* gamma,
                           const float* beta, float* out, int ldo, float* nhat, int ldn, float* mean, float* invstd,

@@ -31,7 +31,6 @@ Data are centred per column first (prior mean 0), and the means shifted back at 
 from __future__ import annotations
 
 import math
-from typing import Sequence
 
 import numpy as np
 import torch

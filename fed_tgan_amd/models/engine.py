@@ -116,6 +116,9 @@ class EngineConfig:
     # HIP, two hidden D layers: the second layer's forward is computed row by row in the first layer's
     # split-K reduction launch (chain_epilogue_kernel)
     chain_d1: bool = True
+    # HIP, bf16: each generator layer's Linear -> BatchNorm(train) -> ReLU as ONE launch, a workgroup
+    # owning 16 output columns of one batch (kernels/bn_fused.hip) instead of a tile GEMM + BN launch
+    bn_colown: bool = False
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -143,6 +146,8 @@ class CTGANEngine:
         self.mem = mem or TorchAlloc(self.device)
         self.seed = int(seed if seed is not None else torch.initial_seed() % (2 ** 31))
         self.ops = get_ops(backend, self.device, self.seed, cfg.precision, mem=self.mem)
+        if hasattr(self.ops, "bn_colown"):
+            self.ops.bn_colown = bool(cfg.bn_colown)
         B, P = cfg.batch_size, cfg.pack
         if B % P:
             raise ValueError("batch_size must be a multiple of pack")

@@ -122,6 +122,10 @@ class HipOps:
         # profiles/README.md "negative results")
         self.bn_fused = False
         self._bnp: Dict[int, torch.Tensor] = {}
+        # Linear -> BatchNorm(train) -> ReLU as one launch by column ownership (kernels/bn_fused.hip);
+        # bf16 only.  Set from EngineConfig.bn_colown.
+        self.bn_colown = False
+        self._colown: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
 
     # ------------------------------------------------------------------ helpers
     def set_client_batch(self, k: int, stride: int = 0, seed_step: int = 0, base: int = 0) -> int:
@@ -186,6 +190,27 @@ class HipOps:
             t = self.mem.zeros(max(n, 1 << 16), dtype=torch.float32)
             self._bnp[self.lane] = t
         return t
+
+    def _colown_bufs(self, n: int):
+        """(stat, cnt) of the current lane for linear_bn_relu_colown: the batch-statistics hand-off and
+        the per-column-block arrival counters (zero between launches; sized before graph capture)."""
+        t = self._colown.get(self.lane)
+        if t is None or t[0].numel() < 4 * n:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("colown buffers must be sized before graph capture")
+            m = max(n, 1024)
+            t = (self.mem.zeros(4 * m, dtype=torch.float32), self.mem.zeros(-(-m // 16), dtype=torch.int32))
+            self._colown[self.lane] = t
+        return t
+
+    def _colown_ok(self, x, W, nhat, groups) -> bool:
+        if not (self.bn_colown and not self.f32 and nhat is not None and groups in (1, 2)):
+            return False
+        rows, K = x.shape
+        if rows % groups or rows // groups < 2 or x.stride(1) != 1:
+            return False
+        kp = -(-K // 32) * 32 + 8
+        return 16 * kp * 2 + (rows // groups * 20 + 1028) * 4 <= 64 * 1024
 
     def _span_tables(self, spans, cond_spans=None):
         key = (tuple(spans), tuple(cond_spans or ()))
@@ -268,6 +293,13 @@ class HipOps:
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):
         """groups = 2: the rows are two batches (BN statistics per batch, running stats updated
         batch after batch); mean / invstd are then [2, cols].  onehot: see gemm."""
+        if training and self._colown_ok(x, W, nhat, groups):
+            stat, cnt = self._colown_bufs(W.shape[0])
+            oh = onehot or (None, None, None, None)
+            self.L.linear_bn_relu_colown(x, W, b, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum),
+                                         float(eps), int(groups), oh[0], oh[1], oh[2], oh[3],
+                                         bool(onehot is not None and len(onehot) > 4 and onehot[4]), stat, cnt)
+            return
         if training:
             M, N, K = x.shape[0], W.shape[0], x.shape[1]
             kc = 64 if self.f32 else 128

@@ -1,0 +1,136 @@
+"""Linear -> BatchNorm(train) -> ReLU in one launch by column ownership (kernels/bn_fused.hip,
+EngineConfig.bn_colown) against the plain-PyTorch fp32 math of the same op (bf16-rounded GEMM operands,
+as every bf16 training GEMM stages them) and against the two-launch tile GEMM + BN path."""
+import numpy as np
+import pytest
+import torch
+
+from fed_tgan_amd.data.demo import small_table
+from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(torch.float32)
+
+
+def _case(rows, K, N, C, seed, transposed_w=False):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    r = lambda *s: torch.randn(*s, generator=g).to(DEV)  # noqa: E731
+    H = torch.zeros(rows, K + 8, device=DEV)
+    H[:, 4:4 + K] = r(rows, K) * 1.5 + 0.3
+    x = H[:, 4:4 + K]                                   # a strided view, 16-B aligned rows
+    W = (r(K, N).t() if transposed_w else r(N, K)) * 0.1
+    Wc = r(N, C) * 0.5
+    col = torch.randint(0, 3, (rows,), generator=g, dtype=torch.int32).to(DEV)
+    off = torch.tensor([0, 4, 9], dtype=torch.int32, device=DEV)
+    opt = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int32).to(DEV)
+    return x, W, r(N) * 0.2, torch.rand(N, generator=g).to(DEV) + 0.5, r(N) * 0.3, Wc, col, opt, off
+
+
+def _reference(x, W, b, gamma, beta, Wc, col, opt, off, groups, rm, rv, mom=0.1, eps=1e-5):
+    a = _bf(x) @ _bf(W).t() + b
+    if Wc is not None:
+        a = a + Wc[:, (off[col.long()] + opt).long()].t()
+    rpg = x.shape[0] // groups
+    outs, nh, means, invs = [], [], [], []
+    rm, rv = rm.clone(), rv.clone()
+    for h in range(groups):
+        ab = a[h * rpg:(h + 1) * rpg]
+        mu, var = ab.mean(0), ab.var(0, unbiased=False)
+        n = (ab - mu) * torch.rsqrt(var + eps)
+        nh.append(n)
+        outs.append(torch.relu(n * gamma + beta))
+        means.append(mu)
+        invs.append(torch.rsqrt(var + eps))
+        rm = (1 - mom) * rm + mom * mu
+        rv = (1 - mom) * rv + mom * var * rpg / (rpg - 1)
+    return torch.cat(outs), torch.cat(nh), torch.stack(means), torch.stack(invs), rm, rv
+
+
+@pytest.mark.parametrize("rows,groups,K,N,onehot,wt", [(1000, 2, 384, 256, True, False), (1000, 2, 128, 256, True, True),
+                                                       (500, 1, 300, 200, False, False), (66, 2, 37, 40, True, False)])
+def test_colown_matches_fp32_reference(rows, groups, K, N, onehot, wt):
+    from fed_tgan_amd.ops import native
+    from fed_tgan_amd.ops.hip import HipOps
+    native.require()
+    ops = HipOps(DEV, seed=7)
+    ops.bn_colown = True
+    x, W, b, gamma, beta, Wc, col, opt, off = _case(rows, K, N, 12, seed=rows + K, transposed_w=wt)
+    rm0, rv0 = torch.randn(N, device=DEV) * 0.1, torch.rand(N, device=DEV) + 0.5
+    out, nhat = torch.zeros(rows, N + 3, device=DEV)[:, :N], torch.zeros(rows, N, device=DEV)
+    mean, inv = torch.zeros(groups, N, device=DEV), torch.zeros(groups, N, device=DEV)
+    rm, rv = rm0.clone(), rv0.clone()
+    oh = (Wc, col, opt, off) if onehot else None
+    assert ops._colown_ok(x, W, nhat, groups)
+    for _ in range(2):   # a second launch: the arrival counters were re-zeroed by the first
+        rm.copy_(rm0)
+        rv.copy_(rv0)
+        ops.linear_bn_relu(x, W, b, gamma, beta, out, None, nhat, mean, inv, rm, rv, True, 0.1, 1e-5, groups=groups,
+                           onehot=oh)
+    torch.cuda.synchronize()
+    want = _reference(x, W, b, gamma, beta, Wc if onehot else None, col, opt, off, groups, rm0, rv0)
+    for name, got, ref in zip(("out", "nhat", "mean", "invstd", "rm", "rv"), (out, nhat, mean, inv, rm, rv), want):
+        torch.testing.assert_close(got, ref, rtol=2e-4, atol=2e-4, msg=name)
+    stat, cnt = ops._colown_bufs(N)
+    assert int(cnt.abs().sum()) == 0
+
+
+def test_colown_engine_matches_two_launch_path():
+    """The paired generator pass with bn_colown: same H / BN statistics / running stats as the tile
+    GEMM + BN kernels (within fp32 re-association), and captured training steps stay finite."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    res = []
+    for colown in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, bn_colown=colown), DEV, backend="hip", seed=3)
+        eng.set_training_data(X)
+        eng._prepare_paired()
+        torch.cuda.synchronize()
+        res.append((eng.H2.clone(), eng.bn_mean2[1].clone(), eng.bn_invstd2[1].clone(), eng.p["G.1.rv"].clone(),
+                    eng.nhat2[0].clone()))
+    for name, a, b in zip(("H2", "mean", "invstd", "rv", "nhat"), *res):
+        torch.testing.assert_close(b, a, rtol=1e-3, atol=1e-3, msg=name)
+    eng.train_steps(11, use_graph=True)
+    torch.cuda.synchronize()
+    assert np.isfinite(eng.losses()).all() and bool(torch.isfinite(eng.flat).all())
+    B = eng.B
+    a = eng.H2[:, eng.off[1]:eng.off[0]]
+    assert bool((a >= 0).all())
+    # BN of the D-phase batch: the normalised values have zero mean / unit variance per column
+    n0 = eng.nhat2[0][:B]
+    assert float(n0.mean(0).abs().max()) < 1e-4 and float((n0.var(0, unbiased=False) - 1).abs().max()) < 1e-2
+
+
+def test_colown_batched_clients_bit_identical():
+    """Batched clients (client = blockIdx.z) run the column-ownership kernel per client: identical to
+    single-client engines with the same seeds."""
+    from fed_tgan_amd.models.batched import BatchedClients
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table(2000, 0)
+    cfg = EngineConfig(batch_size=500, bn_colown=True)
+    seeds = [11, 12]
+    bc = BatchedClients(tr.layout, cfg, DEV, seeds, n_rows=len(X))
+    bc.engines[0].ops.batch_plan = False
+    rng = np.random.default_rng(3)
+    data = [X, X[rng.permutation(len(X))]]
+    for e, Xc in zip(bc.engines, data):
+        e.set_training_data(Xc)
+    plain = []
+    for s, e, Xc in zip(seeds, bc.engines, data):
+        p = CTGANEngine(tr.layout, cfg, DEV, backend="hip", seed=s)
+        p.flat.copy_(e.flat)
+        p.set_training_data(Xc)
+        plain.append(p)
+    bc.train_steps(9)
+    for p in plain:
+        p.train_steps(9)
+    torch.cuda.synchronize()
+    for e, p in zip(bc.engines, plain):
+        for name in ("flat", "mG", "vG"):
+            assert torch.equal(getattr(e, name), getattr(p, name)), name

@@ -134,6 +134,26 @@ def bn_ab(eng, dev):
             print(f"bn_fused={int(fused)}: full step {per_call(eng._one_step, dev, n=5, reps=20):8.2f} us", flush=True)
 
 
+def colown_ab(eng, dev):
+    """Generator Linear -> BN(train) -> ReLU: tile GEMM + BN kernel (two launches) vs one launch by column
+    ownership (EngineConfig.bn_colown) -- each paired layer alone, then the full captured step."""
+    def layer(i):
+        a, b_ = eng.off[i], eng.off[i + 1]
+        x, W, oh = eng._g_in(eng.H2, a, eng.p[f"G.{i}.W"], (eng.col2, eng.opt2, eng.cfg.onehot_trans))
+        return lambda: eng.ops.linear_bn_relu(
+            x, W, eng.p[f"G.{i}.b"], eng.p[f"G.{i}.gamma"], eng.p[f"G.{i}.beta"], eng.H2[:, b_:a], eng.abuf2[i],
+            eng.nhat2[i], eng.bn_mean2[i], eng.bn_invstd2[i], eng.p[f"G.{i}.rm"], eng.p[f"G.{i}.rv"], True,
+            eng.cfg.bn_momentum, eng.cfg.bn_eps, groups=2, onehot=oh)
+    eng._prepare_paired()
+    for rep in range(3):
+        for on in (False, True):
+            eng.ops.bn_colown = on
+            row = [per_call(layer(i), dev) for i in range(len(eng.gdims))]
+            t_step = per_call(eng._one_step, dev, n=5, reps=20)
+            print(f"bn_colown={int(on)}: " + "  ".join(f"G{i} paired {v:6.2f} us" for i, v in enumerate(row)) +
+                  f"   full step {t_step:8.2f} us", flush=True)
+
+
 def dw0_tile_ab(eng, dev):
     """D0 weight-gradient GEMM (paired with R0): planner tile vs 128x128 (fewer, fatter workgroups)."""
     for rep in range(3):
@@ -242,6 +262,7 @@ def main():
     ap.add_argument("--pair-sweep", action="store_true", help="independent GEMM pairs: two launches / one")
     ap.add_argument("--onehot-ab", action="store_true", help="step + generation: dense c block vs one-hot gather")
     ap.add_argument("--bn-ab", action="store_true", help="step: BN from GEMM partials vs full-reduction BN kernel")
+    ap.add_argument("--colown-ab", action="store_true", help="step: G layers as tile GEMM + BN vs one colown launch")
     ap.add_argument("--dw0-ab", action="store_true", help="step: D0 weight-gradient tile 64 vs 128")
     ap.add_argument("--inlaunch-ab", action="store_true", help="split-K: epilogue launch vs in-launch reduction")
     ap.add_argument("--gwt-ab", action="store_true", help="step + generation: generator weights [out, in] vs input-major")
@@ -271,6 +292,8 @@ def main():
         return onehot_ab(eng, tr, X, dev)
     if args.bn_ab:
         return bn_ab(eng, dev)
+    if args.colown_ab:
+        return colown_ab(eng, dev)
     if args.dw0_ab:
         return dw0_tile_ab(eng, dev)
     if args.inlaunch_ab:

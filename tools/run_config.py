@@ -98,7 +98,8 @@ def main():
             "rows_per_client": args.rows, "epochs": args.epochs, "weights": [round(float(w), 4) for w in rt.weights],
             "mean_sec_per_epoch_after_first": round(sum(rt.round_times[1:]) / max(len(rt.round_times) - 1, 1), 4),
             "wall_s_incl_init": round(wall, 2),
-            "init_s": {k: round(v, 3) for k, v in getattr(rt, "init_times", {}).items()}, "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
+            "init_s": {k: round(v, 3) for k, v in getattr(rt, "init_times", {}).items()},
+            "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
     if args.engine:
         summ["engine_overrides"] = args.engine
     print(json.dumps(summ), flush=True)
