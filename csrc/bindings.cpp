@@ -992,6 +992,12 @@ std::string py_float(double x) { return fedtgan::format_py_float(x); }
 
 // kernel variant knobs for measured sweeps (tools/microbench.py); returns the previous value
 int64_t set_tuning(const std::string& key, int64_t value) {
+  if (key == "colown_dbg") {   // phase-cost probe of linear_bn_relu_colown (results are wrong while set)
+    TORCH_CHECK(value >= 0 && value <= 7, "colown_dbg: bit mask 0..7");
+    const int64_t prev = fedtgan::g_colown_dbg;
+    fedtgan::g_colown_dbg = (int)value;
+    return prev;
+  }
   if (key == "bn_cols") {
     TORCH_CHECK(value == 4 || value == 8 || value == 16, "bn_cols must be 4, 8 or 16");
     const int64_t prev = fedtgan::g_bn_cols;

@@ -5,8 +5,9 @@
 // needs the whole batch's statistics before any row can be normalised, so the GEMM output makes a
 // round trip through memory and a second launch reduces it again.  Here one workgroup owns 16 output
 // columns of ONE batch (all of that batch's rows):
-//   1. the workgroup stages its 16 weight rows into LDS as bf16 once;
-//   2. its 8 waves walk the batch's 16-row blocks: A fragments straight from global memory (fp32,
+//   1. half the workgroup stages its 16 weight rows into LDS as bf16 once, the other half resolves every
+//      row's one-hot column (the two dependent index loads) into LDS;
+//   2. its 16 waves walk the batch's 16-row blocks: A fragments straight from global memory (fp32,
 //      rounded to bf16 in registers -- the same operand rounding as the tile GEMM), B fragments from
 //      LDS, v_mfma_f32_16x16x32_bf16 with fp32 accumulation; + bias + the one-hot block's gathered
 //      weight; the pre-BN values stay in LDS ([rows][16] fp32), never in HBM;
@@ -28,7 +29,7 @@ typedef __attribute__((ext_vector_type(8))) short co_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float co_f32x4;
 typedef __attribute__((ext_vector_type(4))) unsigned co_u32x4;
 
-constexpr int CO_THREADS = 512, CO_WAVES = CO_THREADS / 64, CO_COLS = 16;
+constexpr int CO_THREADS = 1024, CO_WAVES = CO_THREADS / 64, CO_COLS = 16;
 constexpr int CO_LDY = 20;   // LDS row stride of the pre-BN block (floats): the 4 row groups of a
                              // wave's accumulator store land on distinct banks
 
@@ -72,30 +73,72 @@ __global__ __launch_bounds__(CO_THREADS) void linear_bn_relu_colown_kernel(ColOw
   const int KP = (K + 31) / 32 * 32 + 8;   // LDS row stride of the weight slice (bf16)
   uint16_t* ws = reinterpret_cast<uint16_t*>(co_smem);
   float* ys = reinterpret_cast<float*>(co_smem + (size_t)CO_COLS * KP * 2);
-  float* red = ys + (size_t)rpg * CO_LDY;             // [32][16] partial sums, then [2][16] stats
+  float* red = ys + (size_t)rpg * CO_LDY;             // [CO_THREADS / 16][16] partial sums
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int c0 = blockIdx.x * CO_COLS, b = blockIdx.y;
   const int rbase = b * rpg;                          // first row of this batch
 
-  // 1. weight slice W[c0 .. c0+15][0 .. K) -> LDS bf16 (zero-padded to KP, zero rows past N)
-  for (int e = t; e < CO_COLS * (KP / 2); e += CO_THREADS) {
-    const int n = e / (KP / 2), k = 2 * (e % (KP / 2));
-    const bool okn = c0 + n < N;
-    const float* wr = w + (size_t)min(c0 + n, N - 1) * g.w_sn;
-    const float v0 = (okn && k < K) ? wr[(size_t)k * g.w_sk] : 0.f;
-    const float v1 = (okn && k + 1 < K) ? wr[(size_t)(k + 1) * g.w_sk] : 0.f;
-    *reinterpret_cast<uint32_t*>(&ws[n * KP + k]) = pack_bf16x2(v0, v1);
+  int* gidx = reinterpret_cast<int*>(red + 2 * CO_THREADS + 4);   // [rpg] one-hot column of each row
+
+  // 1. in parallel: the first half of the workgroup resolves every row's one-hot column (two dependent
+  //    loads) into LDS, the second half stages the weight slice W[c0 .. c0+15][0 .. K) into LDS as bf16
+  //    (zero-padded to KP, zero rows past N; consecutive threads read consecutive memory: along k for
+  //    [out, in] rows, along n for input-major storage)
+  constexpr int HALF = CO_THREADS / 2;
+  if (g.dbg & 2) {
+    // (probe: no staging)
+  } else if (t < HALF) {
+    if (oh_w)
+      for (int r = t; r < rpg; r += HALF) gidx[r] = oh_off[oh_col[rbase + r]] + oh_opt[rbase + r];
+  } else {
+    // SU elements per thread in flight: every load of a pass is issued before the first LDS store
+    // (a load -> convert -> store loop would pay one memory round trip per element)
+    constexpr int SU = 16;
+    const int total = CO_COLS * KP;
+    const bool im = g.w_sn == 1;
+    for (int e0 = t - HALF; e0 < total; e0 += SU * HALF) {
+      float v[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int e = e0 + u * HALF;
+        const int n = im ? e % CO_COLS : e / KP, k = im ? e / CO_COLS : e % KP;
+        const bool ok = e < total && c0 + n < N && k < K;
+        v[u] = ok ? w[(size_t)min(c0 + n, N - 1) * g.w_sn + (size_t)min(k, K - 1) * g.w_sk] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int e = e0 + u * HALF;
+        const int n = im ? e % CO_COLS : e / KP, k = im ? e / CO_COLS : e % KP;
+        if (e < total) ws[n * KP + k] = f2bf(v[u]);
+      }
+    }
   }
   __syncthreads();
 
-  // 2. 16-row blocks of this batch, round-robin over the waves
+  // 2. 16-row blocks of this batch, round-robin over the waves; a block's A loads and its rows' one-hot
+  //    gathers are issued together (one memory round trip per K chunk)
   const int nrb = (rpg + 15) / 16;
   const int n_l = lane & 15, kq = 8 * (lane >> 4);
   const int n_g = min(c0 + n_l, N - 1);
   const float bv = bias ? bias[n_g] : 0.f;
   for (int rb = wv; rb < nrb; rb += CO_WAVES) {
+    if (g.dbg & 1) {   // (probe: no GEMM)
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * rb + 4 * (lane >> 4) + i;
+        if (r < rpg) ys[r * CO_LDY + n_l] = bv + (float)r;
+      }
+      continue;
+    }
     const int lr = min(16 * rb + n_l, rpg - 1);       // this lane's A row (fragment row = lane & 15)
     const float* xr = x + (size_t)(rbase + lr) * g.ldx;
+    float gv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (oh_w) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = min(16 * rb + 4 * (lane >> 4) + i, rpg - 1);
+        gv[i] = oh_w[(size_t)n_g * g.oh_sn + (size_t)gidx[r] * g.oh_sc];
+      }
+    }
     co_f32x4 acc{0.f, 0.f, 0.f, 0.f};
     constexpr int KU = 8;   // k-steps of 32 whose loads are issued together
     for (int k0 = 0; k0 < K; k0 += 32 * KU) {
@@ -117,26 +160,20 @@ __global__ __launch_bounds__(CO_THREADS) void linear_bn_relu_colown_kernel(ColOw
     for (int i = 0; i < 4; ++i) {
       const int r = 16 * rb + 4 * (lane >> 4) + i;
       if (r < rpg) {
-        float v = acc[i] + bv;
-        if (oh_w) {
-          const int R = rbase + r;
-          const int idx = oh_off[oh_col[R]] + oh_opt[R];
-          v += oh_w[(size_t)n_g * g.oh_sn + (size_t)idx * g.oh_sc];
-        }
-        ys[r * CO_LDY + n_l] = v;
+        ys[r * CO_LDY + n_l] = acc[i] + bv + gv[i];
       }
     }
   }
   __syncthreads();
 
   // 3. batch statistics of the 16 columns, two passes over the LDS block
-  const int col = t & 15, part = t >> 4;   // 32 row slices per column
+  const int col = t & 15, part = t >> 4;   // CO_THREADS / 16 row slices per column
   float s = 0.f;
   for (int r = part; r < rpg; r += CO_THREADS / CO_COLS) s += ys[r * CO_LDY + col];
   red[part * CO_COLS + col] = s;
   __syncthreads();
   float mu = 0.f;
-#pragma unroll 8
+#pragma unroll 16
   for (int p = 0; p < CO_THREADS / CO_COLS; ++p) mu += red[p * CO_COLS + col];
   mu /= (float)rpg;
   __syncthreads();
@@ -148,7 +185,7 @@ __global__ __launch_bounds__(CO_THREADS) void linear_bn_relu_colown_kernel(ColOw
   red[part * CO_COLS + col] = q;
   __syncthreads();
   float m2 = 0.f;
-#pragma unroll 8
+#pragma unroll 16
   for (int p = 0; p < CO_THREADS / CO_COLS; ++p) m2 += red[p * CO_COLS + col];
   const float var = m2 / (float)rpg;   // biased batch variance
   const float is = rsqrtf(var + g.eps);
@@ -204,7 +241,7 @@ __global__ __launch_bounds__(CO_THREADS) void linear_bn_relu_colown_kernel(ColOw
   }
 
   // 4. normalise: consecutive threads write consecutive columns of a row (the thread's column is fixed)
-  if (!okc) return;
+  if (!okc || (g.dbg & 4)) return;
   const float gm = cptr(g.gamma, co)[c], bt = cptr(g.beta, co)[c];
   for (int r = part; r < rpg; r += CO_THREADS / CO_COLS) {
     const float nv = (ys[r * CO_LDY + col] - mu) * is;
@@ -217,11 +254,14 @@ __global__ __launch_bounds__(CO_THREADS) void linear_bn_relu_colown_kernel(ColOw
 
 size_t colown_smem_bytes(int K, int rpg) {
   const int KP = (K + 31) / 32 * 32 + 8;
-  return (size_t)CO_COLS * KP * 2 + ((size_t)rpg * CO_LDY + 2 * CO_THREADS + 4) * 4;
+  return (size_t)CO_COLS * KP * 2 + ((size_t)rpg * CO_LDY + 2 * CO_THREADS + 4 + rpg) * 4;
 }
+
+int g_colown_dbg = 0;
 
 void launch_linear_bn_relu_colown(ColOwnArgs g, bool vec, hipStream_t stream) {
   const ClientBatch& cb = client_batch();
+  g.dbg = g_colown_dbg;
   g.cstride = cb.k > 1 ? cb.stride : 0;
   if (cb.k > 1) {
     check_slabs("linear_bn_relu_colown operand", g.x, g.w, g.bias, g.oh_w, g.oh_col, g.oh_opt, g.oh_off, g.gamma,

@@ -284,7 +284,9 @@ struct ColOwnArgs {
   int rpg, groups, K, N;
   float momentum, eps;
   int64_t cstride;   // set by the launcher (batched clients)
+  int dbg;           // phase-cost probe (set_tuning("colown_dbg")): 1 no GEMM, 2 no staging, 4 no stores
 };
+extern int g_colown_dbg;
 size_t colown_smem_bytes(int K, int rpg);
 void launch_linear_bn_relu_colown(ColOwnArgs g, bool vec, hipStream_t stream);
 

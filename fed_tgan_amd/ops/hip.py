@@ -210,7 +210,7 @@ class HipOps:
         if rows % groups or rows // groups < 2 or x.stride(1) != 1:
             return False
         kp = -(-K // 32) * 32 + 8
-        return 16 * kp * 2 + (rows // groups * 20 + 1028) * 4 <= 64 * 1024
+        return 16 * kp * 2 + (rows // groups * 21 + 2052) * 4 <= 64 * 1024
 
     def _span_tables(self, spans, cond_spans=None):
         key = (tuple(spans), tuple(cond_spans or ()))

@@ -1,6 +1,8 @@
 """Linear -> BatchNorm(train) -> ReLU in one launch by column ownership (kernels/bn_fused.hip,
 EngineConfig.bn_colown) against the plain-PyTorch fp32 math of the same op (bf16-rounded GEMM operands,
 as every bf16 training GEMM stages them) and against the two-launch tile GEMM + BN path."""
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -25,8 +27,9 @@ def _case(rows, K, N, C, seed, transposed_w=False):
     W = (r(K, N).t() if transposed_w else r(N, K)) * 0.1
     Wc = r(N, C) * 0.5
     col = torch.randint(0, 3, (rows,), generator=g, dtype=torch.int32).to(DEV)
-    off = torch.tensor([0, 4, 9], dtype=torch.int32, device=DEV)
+    off = torch.tensor([0, 4, 8], dtype=torch.int32, device=DEV)   # C = 12 one-hot columns
     opt = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int32).to(DEV)
+    assert int((off[col.long()] + opt).max()) < C      # every gather stays inside the block
     return x, W, r(N) * 0.2, torch.rand(N, generator=g).to(DEV) + 0.5, r(N) * 0.3, Wc, col, opt, off
 
 
@@ -123,7 +126,8 @@ def test_colown_batched_clients_bit_identical():
         e.set_training_data(Xc)
     plain = []
     for s, e, Xc in zip(seeds, bc.engines, data):
-        p = CTGANEngine(tr.layout, cfg, DEV, backend="hip", seed=s)
+        p = CTGANEngine(tr.layout, dataclasses.replace(cfg, chain_d1=False, fuse_d_adam=False), DEV, backend="hip",
+                        seed=s)   # the batched step's launch structure (see test_batched._twin_cfg)
         p.flat.copy_(e.flat)
         p.set_training_data(Xc)
         plain.append(p)

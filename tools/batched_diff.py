@@ -6,6 +6,7 @@ engines with the same seeds / weights / data, and prints the first buffers that 
     python tools/batched_diff.py [--k 2] [--precision bf16]
 """
 import argparse
+import dataclasses
 import os
 import sys
 
@@ -17,6 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=2)
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override (repeatable), e.g. --engine bn_colown=1")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -26,16 +29,23 @@ def main():
     dev = torch.device("cuda:0")
     _, _, _, _, _, _, tr, X = small_table(2000, 0)
     cfg = EngineConfig(batch_size=500, precision=args.precision)
+    for kv in args.engine:
+        key, val = kv.split("=", 1)
+        cur = getattr(cfg, key)
+        setattr(cfg, key, (val.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(val))
     k = args.k
     seeds = [1000 + c for c in range(k)]
     rng = np.random.default_rng(7)
     data = [X if c == 0 else X[rng.permutation(len(X))] for c in range(k)]
     bc = BatchedClients(tr.layout, cfg, dev, seeds, n_rows=len(X))
+    bc.engines[0].ops.batch_plan = False      # per-client split-K planning: bit-identical sums
     for e, Xc in zip(bc.engines, data):
         e.set_training_data(Xc)
     plain = []
     for s, e, Xc in zip(seeds, bc.engines, data):
-        p = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=s)
+        # (the batched step neither chains D1 nor fuses D1's weight gradient into the Adam launch)
+        p = CTGANEngine(tr.layout, dataclasses.replace(cfg, chain_d1=False, fuse_d_adam=False), dev, backend="hip",
+                        seed=s)
         p.flat.copy_(e.flat)
         p.set_training_data(Xc)
         plain.append(p)

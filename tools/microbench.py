@@ -145,6 +145,15 @@ def colown_ab(eng, dev):
             eng.nhat2[i], eng.bn_mean2[i], eng.bn_invstd2[i], eng.p[f"G.{i}.rm"], eng.p[f"G.{i}.rv"], True,
             eng.cfg.bn_momentum, eng.cfg.bn_eps, groups=2, onehot=oh)
     eng._prepare_paired()
+    if os.environ.get("COLOWN_DBG"):
+        # phase costs of the one-launch kernel (results wrong while a bit is set): 1 no GEMM, 2 no
+        # staging, 4 no output stores
+        eng.ops.bn_colown = True
+        for dbg in (0, 1, 2, 4, 7):
+            torch.ops.fedtgan.set_tuning("colown_dbg", dbg)
+            row = [per_call(layer(i), dev) for i in range(len(eng.gdims))]
+            print(f"colown_dbg={dbg}: " + "  ".join(f"G{i} paired {v:6.2f} us" for i, v in enumerate(row)), flush=True)
+        torch.ops.fedtgan.set_tuning("colown_dbg", 0)
     for rep in range(3):
         for on in (False, True):
             eng.ops.bn_colown = on
