@@ -56,6 +56,8 @@ def build_parser() -> argparse.ArgumentParser:
                          "last epoch CSV has n_sample rows (reported as 'consistency'); default on for N > 1")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override for A/B measurements, e.g. --engine onehot=0")
+    ap.add_argument("--fed", action="append", default=[], metavar="KEY=VALUE",
+                    help="FedConfig override for A/B measurements, e.g. --fed csv_threads=8")
     ap.add_argument("--phase-timer", default="events", choices=["events", "sync"],
                     help="phase timers: HIP events (no host sync) or stream-synchronised wall time")
     ap.add_argument("--force-dist", action="store_true",
@@ -193,6 +195,10 @@ def run_rank(args) -> None:
     cfg = FedConfig(spec=spec, epochs=args.warmup + args.steps, synthetic_rows=args.rows, out_dir=out,
                     n_sample=args.n_sample, backend=args.backend, gmm_backend=args.gmm, seed=0,
                     verbose=not args.quiet, async_csv=not args.sync_csv, engine=ecfg, phase_timer=args.phase_timer)
+    for kv in args.fed:
+        k, v = kv.split("=", 1)
+        cur = getattr(cfg, k)
+        setattr(cfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
     rt = FedRuntime(cfg, comm, device)
     rt.initialize()
     for ep in range(args.warmup):

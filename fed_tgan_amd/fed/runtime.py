@@ -111,6 +111,8 @@ class FedConfig:
     # phase timers on a GPU: "events" (HIP event pairs, no host sync) or "sync" (stream-synchronised wall
     # time at every phase boundary, the round-2 behaviour)
     phase_timer: str = "events"
+    # wait on the host for the local epoch's kernels before issuing the aggregation / sampling work
+    train_sync: bool = False
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "auto" runs their training steps as ONE batched
@@ -549,6 +551,8 @@ class FedRuntime:
                 self.engine.train_epoch(self.cfg.use_graph)
                 if self.gradflow is not None:
                     self.gradflow.update(self.engine)
+            if self.cfg.train_sync and self.device.type == "cuda":
+                stream_sync(self.device)
         self._epoch_done = epoch + 1
         with self.timer.phase("aggregate", self.device):
             # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
