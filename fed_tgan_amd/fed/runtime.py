@@ -111,8 +111,11 @@ class FedConfig:
     # phase timers on a GPU: "events" (HIP event pairs, no host sync) or "sync" (stream-synchronised wall
     # time at every phase boundary, the round-2 behaviour)
     phase_timer: str = "events"
-    # wait on the host for the local epoch's kernels before issuing the aggregation / sampling work
-    train_sync: bool = False
+    # wait on the host for the local epoch's kernels before issuing the aggregation / sampling work.
+    # Measured (bench.py, 1 GPU, 20 rounds): 18.5 ms/round with the wait, 20.4-20.6 ms without it -- issuing
+    # the generation graph, the pinned D2H copy and the CSV hand-off while the 80-step epoch still runs
+    # stretches the epoch's kernels by ~2 ms (profiles/bench_train_sync_r3.txt)
+    train_sync: bool = True
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "auto" runs their training steps as ONE batched

@@ -38,14 +38,16 @@ def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
         137,800 -- 83 serial bursts at 13 splits); at least 2 bursts per split, fp32 slabs
         capped at ~6 MB.  (Every Intrusion shape keeps its measured split.)
     clients: a batched multi-client launch (models/batched.py) runs every tile once per client, so the
-    grid-filling thresholds count clients x tiles (8 clients' 40 tiles need far less split-K).
+    grid-filling thresholds count clients x tiles (8 clients' 40 tiles need far less split-K).  D0's weight
+    gradient at 8 clients (256 x 6200 x 150, 784 128-tiles) takes 128x128 tiles: the 8-client step
+    709 -> 677 us against 64x64 (profiles/batched_r3.md).
     """
     c = max(1, int(clients))
     t128 = -(-M // 128) * -(-N // 128) * c
     t64 = -(-M // 64) * -(-N // 64) * c
     t32 = -(-M // 32) * -(-N // 32) * c
     bursts = -(-K // kc)
-    if t128 >= 256 and K >= 256 and M >= 128:    # (a 128-row tile over < 128 rows idles its MFMA rows)
+    if t128 >= 256 and K >= 128 and M >= 128:    # (a 128-row tile over < 128 rows idles its MFMA rows)
         return 128, 1
     if t64 >= 256:
         return 64, 1

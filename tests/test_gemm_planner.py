@@ -21,3 +21,6 @@ def test_planner_counts_clients_of_a_batched_launch():
     assert t1 == t8 == 32 and s8 < s1
     assert _plan(50, 5860, 256, clients=8)[0] != 128
     assert _plan(40000, 256, 658)[0] == 128
+    # D0's weight gradient (K = the 150 stacked rows): 64-tiles for one client, 128-tiles for 8
+    assert _plan(256, 6200, 150) == (64, 1)
+    assert _plan(256, 6200, 150, clients=8) == (128, 1)

@@ -56,7 +56,7 @@ def make_split(out: str, n_clients: int = 2, seed: int = 2024, bootstrap_rows: i
 
 
 def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, clients: int, gmm: str,
-              csv_epochs=None, batched: str = "auto", init: str = "independent"):
+              csv_epochs=None, batched: str = "auto", init: str = "independent", host_encode: bool = False):
     import torch
     from fed_tgan_amd.data.schema import intrusion_spec
     from fed_tgan_amd.fed.local import run_local_emulation
@@ -65,7 +65,7 @@ def train_run(out: str, datapath: str, precision: str, seed: int, epochs: int, c
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     cfg = FedConfig(spec=intrusion_spec(), epochs=epochs, datapath=datapath, out_dir=out, n_sample=40000,
                     gmm_backend=gmm, seed=seed, engine=EngineConfig(precision=precision), verbose=False,
-                    batched_clients=batched, init=init)
+                    batched_clients=batched, init=init, device_encode=not host_encode)
     if csv_epochs is not None:      # long runs: only the scored epochs' tables are written
         cfg.csv_epochs = sorted(set(csv_epochs))
     t0 = time.time()
@@ -117,6 +117,8 @@ def main():
     ap.add_argument("--no-utility", action="store_true", help="skip the ML-utility evaluation of the last epoch")
     ap.add_argument("--batched", default="auto", choices=["auto", "on", "off"],
                     help="FedConfig.batched_clients: the clients' steps as one batched engine, or one per thread")
+    ap.add_argument("--host-encode", action="store_true",
+                    help="FedConfig.device_encode off: VGM-encode the rows on the host (numpy) instead of the HIP kernel")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     train_path, hold_path, datapath = make_split(args.out, args.clients, bootstrap_rows=args.bootstrap_rows)
@@ -126,7 +128,8 @@ def main():
         for seed in args.seeds:
             rd = os.path.join(args.out, f"run_{prec}_s{seed}")
             info = train_run(rd, datapath, prec, seed, args.epochs, args.clients, args.gmm,
-                             eval_epochs if args.only_scored_csv else None, args.batched, args.init)
+                             eval_epochs if args.only_scored_csv else None, args.batched, args.init,
+                             args.host_encode)
             sims = similarity(train_path, rd, eval_epochs)
             rec = {"precision": prec, "seed": seed, **info, "eval_epochs": eval_epochs, "avg_jsd": [s[0] for s in sims],
                    "avg_wd": [s[1] for s in sims]}
@@ -156,6 +159,7 @@ def main():
                                         np.sqrt(len(rs))).round(4).tolist() if len(rs) > 1 else None,
                          "eval_epochs": eval_epochs, "bootstrap_rows": args.bootstrap_rows,
                          "gmm": args.gmm, "init": args.init, "batched": args.batched,
+                         "host_encode": args.host_encode,
                          "seeds": [r["seed"] for r in rs]}
     with open(os.path.join(args.out, "real_quality.json"), "w") as f:
         json.dump({"protocol": __doc__, "runs": runs, "summary": summary}, f, indent=1)
