@@ -116,6 +116,13 @@ class EngineConfig:
     # HIP, two hidden D layers: the second layer's forward is computed row by row in the first layer's
     # split-K reduction launch (chain_epilogue_kernel)
     chain_d1: bool = True
+    # HIP, where fuse_d_adam does not apply (the batched multi-client step): D0's weight gradient -- the
+    # largest gradient, 256 x 10 Din -- is held for the D Adam launch instead of sharing a launch with R0, so
+    # it is never written and re-read through HBM (gemm_adam_kernel's tiles update it in place).  A/B knob,
+    # default off: measured slower (8 clients 675 -> 773 us per step, 4 clients 412 -> 437 us: the 64-tile
+    # Adam epilogue's per-element p / m / v traffic and R0 losing its pair partner cost more than the
+    # 51 MB gradient round trip saves; profiles/batched_r3.md)
+    fuse_d0_adam: bool = False
     # HIP, bf16: each generator layer's Linear -> BatchNorm(train) -> ReLU as ONE launch, a workgroup
     # owning 16 output columns of one batch (kernels/bn_fused.hip) instead of a tile GEMM + BN launch
     bn_colown: bool = False
@@ -665,12 +672,19 @@ class CTGANEngine:
         fuse_d = pair and L == 2 and self.cfg.fuse_d_adam and getattr(o, "gemm_adam", False) and \
             self.ddims[0] % 16 == 0 and self.ddims[0] <= 1024 and o.gemm_is_split(self.nP, self.ddims[0], self.K1) and \
             getattr(o, "batch_k", 1) == 1
+        # otherwise D0's weight gradient may be the GEMM held for the Adam launch (its operands, A0 and X, are
+        # final here: the R chain below writes only dl[*][I])
+        d0_fused = pair and not fuse_d and self.cfg.fuse_d0_adam and getattr(o, "gemm_adam", False)
         for i in range(L):
             last_fused = fuse_d and i == L - 1
             with self._lane(1 + i % 2):
                 kw = {"tile": self.cfg.dw0_tile} if (i == 0 and self.cfg.dw0_tile and self.ops.name == "hip") else {}
-                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=3 if last_fused else (1 if pair else 0),
-                       **kw)
+                if i == 0 and d0_fused:
+                    kw = {"tile": 64 if self.cfg.dw0_tile not in (32, 64) else self.cfg.dw0_tile}   # gemm_adam tiles
+                    grp = 3
+                else:
+                    grp = 3 if last_fused else (1 if pair else 0)
+                o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=grp, **kw)
             if last_fused:
                 break              # R_{L-1} was computed with R_{L-2}
             rk = {}
@@ -679,7 +693,7 @@ class CTGANEngine:
                        ms=self.ms[i + 1][I], group=4)
                 rk = {"chain": True}
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
-                   group=2 if pair else 0, **rk)
+                   group=2 if (pair and not (i == 0 and d0_fused)) else 0, **rk)
             inp = self.dl[i][I]
             prev = self.dl[i]
         # (the column sums are folded into the Adam launch: those workgroups update the bias / head
