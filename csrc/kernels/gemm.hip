@@ -923,15 +923,22 @@ static void check_slab(const GemmArgs& g) {
 // clamped, always-valid addresses): one memory round trip instead of ceil(splits / 4).
 // LDS is sized per launch (gemm_smem_bytes): a GEMM whose K-slice is one burst uses one stage
 // buffer, so a 64x64-tile launch over a short K fits 4 workgroups per CU instead of 2.
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false>
+// BATCH: a batched multi-client launch (grid.z = split-K slices x clients, client-major).  The one-client
+// instantiation carries no client prologue at all: even a never-taken client branch costs the step's latency-
+// bound GEMMs measurably (the dW0 || R0 pair 17.6 -> 21.6 us, the step 215.5 -> 223 us; profiles/README.md).
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool BATCH = false>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // grid.z = split-K slices x clients (client-major)
-  const int sk = (int)gridDim.z / g.nclient;
-  const int cl = (int)blockIdx.z / sk;
-  if (cl) client_view(g, cl);
-  gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk, gridDim.x, gridDim.y,
-                                           sk, smem);
+  if constexpr (BATCH) {
+    const int sk = (int)gridDim.z / g.nclient;
+    const int cl = (int)blockIdx.z / sk;
+    if (cl) client_view(g, cl);
+    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk, gridDim.x,
+                                             gridDim.y, sk, smem);
+  } else {
+    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
+                                             smem);
+  }
 }
 
 // stage buffers a launch needs: two when a K-slice spans several bursts, else one -- unless the
@@ -954,13 +961,15 @@ struct Grid3 {
   int x, y, z;
 };
 
-template <class P1, class P2>
+template <class P1, class P2, bool BATCH = false>
 __global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2, Grid3 grid1, Grid3 grid2) {
   constexpr int S1 = 2 * Cfg<false, P1::TM, P1::TM>::STAGE, S2 = 2 * Cfg<false, P2::TM, P2::TM>::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[S1 > S2 ? S1 : S2];
-  if (blockIdx.z) {
-    client_view(g1, blockIdx.z);
-    client_view(g2, blockIdx.z);
+  if constexpr (BATCH) {
+    if (blockIdx.z) {
+      client_view(g1, blockIdx.z);
+      client_view(g2, blockIdx.z);
+    }
   }
   const int n1 = grid1.x * grid1.y * grid1.z;
   int b = blockIdx.x;
@@ -1078,21 +1087,24 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
 // flat-buffer Adam with its folded column sums (adam_cs_body), skipping the GEMM's range.  The step's
 // last two launches (the generator's first-layer weight gradient, then the generator's Adam) become
 // one: none of the other Adam work waits for that gradient.
-template <bool VEC, int TM, int AUX>
+template <bool VEC, int TM, int AUX, bool BATCH = false>
 __global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, float* p, const float* gr, float* m,
                                                        float* v, const float* step, int64_t n4, float lr, float b1,
                                                        float b2, float eps, float wd, uint64_t* rng_bump,
                                                        AdamColsum cs) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, TM, TM>::STAGE];
-  const int64_t co = (int64_t)blockIdx.z * g.cstride;
-  if (co) {   // batched clients: the GEMM's buffers (its Adam pointers included) and the Adam operands
-    client_view(g, blockIdx.z);
-    p = cptr(p, co);
-    gr = cptr(gr, co);
-    m = cptr(m, co);
-    v = cptr(v, co);
-    step = cptr(step, co);
-    rng_bump = cptr(rng_bump, co);
+  int64_t co = 0;
+  if constexpr (BATCH) {
+    co = (int64_t)blockIdx.z * g.cstride;
+    if (co) {   // batched clients: the GEMM's buffers (its Adam pointers included) and the Adam operands
+      client_view(g, blockIdx.z);
+      p = cptr(p, co);
+      gr = cptr(gr, co);
+      m = cptr(m, co);
+      v = cptr(v, co);
+      step = cptr(step, co);
+      rng_bump = cptr(rng_bump, co);
+    }
   }
   const int nt = gd.x * gd.y * gd.z;
   const int b = blockIdx.x;
@@ -1137,23 +1149,21 @@ static dim3 gemm_prepare(GemmArgs& g) {
   return dim3(tn, tm, g.splitk);
 }
 
-static void gemm_dispatch(const GemmArgs& g, dim3 grid_, hipStream_t stream) {
-  const dim3 block(NT);
-  const dim3 grid(grid_.x, grid_.y, grid_.z * g.nclient);   // split-K slices x clients
+template <bool BATCH>
+static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds, hipStream_t stream) {
   const int T = g.tile;
-  const size_t lds = gemm_smem_bytes(g);
   if (g.bin) {   // bf16 operands: C = A B^T only (checked on the host)
-    if (T == 32) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 32, 32, true>), grid, block, lds, stream, g);
-    else if (T == 128) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 128, 128, true>), grid, block, lds, stream, g);
-    else hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 64, 64, true>), grid, block, lds, stream, g);
+    if (T == 32) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 32, 32, true, BATCH>), grid, block, lds, stream, g);
+    else if (T == 128) hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 128, 128, true, BATCH>), grid, block, lds, stream, g);
+    else hipLaunchKernelGGL((gemm_kernel<false, true, false, true, 64, 64, true, BATCH>), grid, block, lds, stream, g);
     return;
   }
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT>), grid, block, lds, stream, g);       \
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT>), grid, block, lds, stream, g); \
-  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT>), grid, block, lds, stream, g);   \
-  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT>), grid, block, lds, stream, g);
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g); \
+  else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);   \
+  else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);
 #define FEDTGAN_GEMM_TILES(F, V)       \
   if (T == 32) {                       \
     FEDTGAN_GEMM_LAYOUTS(F, V, 32)     \
@@ -1176,6 +1186,12 @@ static void gemm_dispatch(const GemmArgs& g, dim3 grid_, hipStream_t stream) {
 #undef FEDTGAN_GEMM_TILES
 #undef FEDTGAN_GEMM_LAYOUTS
 #undef FEDTGAN_GEMM_DISPATCH
+}
+
+static void gemm_dispatch(const GemmArgs& g, dim3 grid_, hipStream_t stream) {
+  const dim3 grid(grid_.x, grid_.y, grid_.z * g.nclient);   // split-K slices x clients
+  if (g.nclient > 1) gemm_dispatch_t<true>(g, grid, dim3(NT), gemm_smem_bytes(g), stream);
+  else gemm_dispatch_t<false>(g, grid, dim3(NT), gemm_smem_bytes(g), stream);
 }
 
 static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
@@ -1220,8 +1236,14 @@ template <bool V1, bool V2>
 static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3 b, hipStream_t stream) {
   const dim3 grid(a.x * a.y * a.z + b.x * b.y * b.z, 1, g1.nclient), block(NT);
 #define FEDTGAN_PAIR(T1, TA2, TB2)                                                                              \
-  hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>>), grid, block, \
-                     0, stream, g1, g2, a, b)
+  do {                                                                                                          \
+    if (g1.nclient > 1)                                                                                         \
+      hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>, true>),   \
+                         grid, block, 0, stream, g1, g2, a, b);                                                  \
+    else                                                                                                        \
+      hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>, false>),  \
+                         grid, block, 0, stream, g1, g2, a, b);                                                  \
+  } while (0)
   if (!(g1.ta && !g1.tb) || g2.ta || g2.tile != 32) return false;
   if (g1.tile == 64) {
     if (g2.tb) FEDTGAN_PAIR(64, false, true); else FEDTGAN_PAIR(64, false, false);
@@ -1288,9 +1310,15 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
   const Grid3 gd{(int)d.x, (int)d.y, (int)d.z};
   const int grid = gd.x * gd.y * gd.z + std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
-#define FEDTGAN_GEMM_ADAM(V, T, AUX)                                                                               \
-  hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX>), dim3(grid, 1, g.nclient), dim3(NT), 0, stream, g, gd, p, gr, m, v,  \
-                     step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs)
+#define FEDTGAN_GEMM_ADAM(V, T, AUX)                                                                                  \
+  do {                                                                                                                   \
+    if (g.nclient > 1)                                                                                                   \
+      hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX, true>), dim3(grid, 1, g.nclient), dim3(NT), 0, stream, g, gd, p,   \
+                         gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs);                                     \
+    else                                                                                                                 \
+      hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX, false>), dim3(grid, 1, 1), dim3(NT), 0, stream, g, gd, p, gr, m,   \
+                         v, step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs);                                            \
+  } while (0)
 #define FEDTGAN_GEMM_ADAM_T(V, T)                                 \
   if (g_adam_store == 2) FEDTGAN_GEMM_ADAM(V, T, 2);              \
   else if (g_adam_store == 16) FEDTGAN_GEMM_ADAM(V, T, 16);       \
