@@ -1299,6 +1299,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
   // d = x - shift reduce together, so the workgroup pays ONE cross-wave reduction instead of two
   // (mean, then centred variance).  The shift keeps E[d^2] - E[d]^2 free of cancellation.
   const float sh0 = a[cc], sh1 = a[(size_t)min(rpg, rows - 1) * lda + cc];
+  // the column's affine and running-statistic parameters are requested with the rows (they are consumed
+  // after the cross-wave reduction, whose barriers would otherwise leave their round trip exposed)
+  const float gm = gamma[cc], bt = beta[cc], rm0 = rm[cc], rv0 = rv[cc];
   float x[MAXR];
   float s[2 * BN_MAXG] = {0.f, 0.f, 0.f, 0.f};   // sum d (batch 0, 1), sum d^2 (batch 0, 1)
 #pragma unroll
@@ -1318,7 +1321,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
   const float is0 = rsqrtf(var0 + eps), is1 = rsqrtf(var1 + eps);
   if (grp == 0 && ok) {
     const float unb = (float)rpg / (float)max(rpg - 1, 1);
-    float m = rm[c], v = rv[c];
+    float m = rm0, v = rv0;
     mean[c] = mu0;
     invstd[c] = is0;
     m = (1.f - momentum) * m + momentum * mu0;          // batch after batch, in row order
@@ -1333,7 +1336,6 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     rv[c] = v;
   }
   if (!ok) return;
-  const float gm = gamma[c], bt = beta[c];
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
     const int r = grp + i * GROUPS;
@@ -1595,6 +1597,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
   const int c = blockIdx.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
+  // gamma * invstd is requested with the rows (consumed after the reduction's barriers)
+  const float k = gamma[cc] * invstd[cc];
   float dy[MAXR], nh[MAXR];
   float st[3] = {0.f, 0.f, 0.f};   // sum dy, sum dy * nhat, sum nhat
 #pragma unroll
@@ -1615,7 +1619,6 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
   }
   bn_colsum<COLS, 3>(st, sh);
   const float sdy = st[0], sdyn = st[1], snh = st[2];
-  const float k = gamma[cc] * invstd[cc];
   const float invn = 1.f / (float)rows;
   // the preceding Linear's bias gradient sum_r da_r, in closed form from the same single
   // reduction: k * (sum dy - rows * sdy / rows - sum nhat * sdyn / rows)
