@@ -690,7 +690,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   // loaded in one unrolled loop with no global store in between (all loads in flight together, one
   // memory round trip) and folded into the accumulators before the epilogue.  Split-K slabs leave it
   // to gemm_splitk_epilogue.
-  if (g.oh_w && gz == 1) {
+  // (the host refuses a one-hot block with op(A) = A^T: weight-gradient instantiations carry none of it)
+  if (!TA && g.oh_w && gz == 1) {
     int rows[MI][4];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -875,7 +876,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         if (g.bias) v += g.bias[n];
         st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
-  if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
+  if constexpr (!TA && TB) {   // (host: BN partials need C = A B^T)
+    if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
+  }
 }
 
 // batched clients (launch.h ClientBatch): client c's copy of every buffer of a GEMM and its Philox seed
