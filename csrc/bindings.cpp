@@ -131,6 +131,8 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
           const optional<Tensor>& tile_cnt, bool chain) {
   const bool bin = a.scalar_type() == at::kBFloat16;
   const bool cbf = c.scalar_type() == at::kBFloat16;
+  // op(A) = A^T (weight gradients): the kernels' A^T instantiations carry no epilogue code
+  TORCH_CHECK(!ta || epi == fedtgan::EPI_NONE, "gemm: op(A) = A^T takes the plain epilogue only (bias / alpha / beta)");
   if (bin) {
     TORCH_CHECK(!ta && tb && !f32, "gemm: bf16 operands need C = A B^T on the bf16 MFMA path");
     check_bf16_operand(a, "a");

@@ -462,7 +462,7 @@ struct Cfg {
 //   sc1) and applies the epilogue, summing the slabs in the same order as gemm_splitk_epilogue (so
 //   both paths give bit-identical outputs).
 // Nothing waits on another workgroup (no spinning): every workgroup ends.
-template <int TM, int TN, int MI, int NJ>
+template <int TM, int TN, int MI, int NJ, bool PLAIN = false>
 __device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (&acc)[MI][NJ], int m0, int n0, int tile,
                                                 int bz, int gz, int lane, int wm, int wn, unsigned char* smem,
                                                 uint64_t step) {
@@ -528,7 +528,7 @@ __device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (
       if (g.beta != 0.f) v += g.beta * (*cp);
       if (g.bias) v += g.bias[nn];
       if (g.oh_w) v += onehot_term(g, m, nn);
-      st_out(g.c, (size_t)m * g.ldc + nn, apply_epi(g, v, m, nn, step, (uint64_t)m * g.N + nn), g.wt);
+      st_out(g.c, (size_t)m * g.ldc + nn, PLAIN ? v : apply_epi(g, v, m, nn, step, (uint64_t)m * g.N + nn), g.wt);
     }
   }
 }
@@ -714,7 +714,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
           acc[i][j][r] += g.oh_trans ? g.oh_w[(size_t)rows[i][r] * g.oh_ld + n] : g.oh_w[(size_t)n * g.oh_ld + rows[i][r]];
       }
   }
-  const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  // weight-gradient instantiations (op(A) = A^T) have a plain epilogue (host-checked): no epilogue code at all
+  constexpr bool PLAIN = TA;
+  const uint64_t step = (!PLAIN && g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   if constexpr (BIN && TM <= 64) if (g.c16) {
     // bf16 output (host: unsplit, beta = 0, epilogue NONE / RELU / BN_EVAL_RELU): the tile goes
     // through LDS and each thread writes 8 consecutive columns of a row as one 16-B store (128x128
@@ -777,7 +779,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   }
   if constexpr (TM <= 64) {
     if (gz > 1 && g.red_inl) {
-      splitk_inlaunch<TM, TN, MI, NJ>(g, acc, m0, n0, by * gx + bx, bz, gz, lane, wm, wn, smem, step);
+      splitk_inlaunch<TM, TN, MI, NJ, PLAIN>(g, acc, m0, n0, by * gx + bx, bz, gz, lane, wm, wn, smem, step);
       return;
     }
   }
@@ -822,7 +824,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       float* cp = g.c + (size_t)m * g.ldc + n;
       if (g.beta != 0.f) v += g.beta * (*cp);
       if (g.bias) v += colb;
-      st_out(g.c, (size_t)m * g.ldc + n, apply_epi_c(g, v, m, n, step, (uint64_t)m * g.N + n, ce), g.wt);
+      st_out(g.c, (size_t)m * g.ldc + n, PLAIN ? v : apply_epi_c(g, v, m, n, step, (uint64_t)m * g.N + n, ce), g.wt);
     }
     return;
   }
@@ -874,7 +876,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
         if (g.bias) v += g.bias[n];
-        st_out(g.c, (size_t)m * g.ldc + n, apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
+        st_out(g.c, (size_t)m * g.ldc + n, PLAIN ? v : apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
       }
   if constexpr (!TA && TB) {   // (host: BN partials need C = A B^T)
     if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
