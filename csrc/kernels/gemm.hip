@@ -539,7 +539,11 @@ __device__ __forceinline__ void splitk_inlaunch(const GemmArgs& g, const f32x4 (
 // 4 waves in a 2x2 grid, each owning (TM/2)x(TN/2) = MI x NJ blocks of 16x16 MFMA accumulators.
 // The body of one output tile; (bx, by, bz) index the tile within a (gx, gy, gz) tile grid.  Called by
 // gemm_kernel (one GEMM per launch) and gemm_pair_kernel (two independent GEMMs in one launch).
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool ADAM = false>
+// EK (epilogue kind, chosen on the host per launch): 0 = every epilogue (runtime g.epi); 1 = plain (EPI_NONE:
+// bias / alpha / beta / one-hot only); 2 = split-K slice whose slab is reduced by a separate launch (raw
+// accumulators only); 3 = the mask product (EPI_MASK: the A / R chains).  The Philox / mask / BN epilogue code a launch cannot reach is then not compiled into
+// it -- measured on the weight-gradient tiles (op(A) = A^T, always plain): the dW0 || R0 pair 17.7 -> 14.0 us.
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool ADAM = false, int EK = 0>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int bz, int gx, int gy, int gz,
                                           unsigned char* __restrict__ smem) {
   static_assert(!BIN || (!TA && TB && !F32), "bf16 operands: C = A B^T, both k-contiguous, bf16 MFMA");
@@ -686,6 +690,19 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
   }
 
+  if constexpr (EK == 2) {   // split-K slice: the raw accumulators to this slice's slab
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WN + j * 16 + (lane & 15);
+          if (m < g.M && n < g.N) st_out(g.ws, ((size_t)bz * g.M + m) * g.N + n, acc[i][j][r], g.wt);
+        }
+    return;
+  }
   // one-hot block (alpha == 1, checked on the host): every gathered weight of this lane's outputs is
   // loaded in one unrolled loop with no global store in between (all loads in flight together, one
   // memory round trip) and folded into the accumulators before the epilogue.  Split-K slabs leave it
@@ -715,7 +732,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       }
   }
   // weight-gradient instantiations (op(A) = A^T) have a plain epilogue (host-checked): no epilogue code at all
-  constexpr bool PLAIN = TA;
+  constexpr bool PLAIN = TA || EK == 1;
+  constexpr bool MASKED = !TA && EK == 3;
   const uint64_t step = (!PLAIN && g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   if constexpr (BIN && TM <= 64) if (g.c16) {
     // bf16 output (host: unsplit, beta = 0, epilogue NONE / RELU / BN_EVAL_RELU): the tile goes
@@ -876,7 +894,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
         float* cp = g.c + (size_t)m * g.ldc + n;
         if (g.beta != 0.f) v += g.beta * (*cp);
         if (g.bias) v += g.bias[n];
-        st_out(g.c, (size_t)m * g.ldc + n, PLAIN ? v : apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n), g.wt);
+        st_out(g.c, (size_t)m * g.ldc + n,
+               PLAIN ? v : (MASKED ? v * g.ms[(size_t)m * g.ldms + n] : apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n)),
+               g.wt);
       }
   if constexpr (!TA && TB) {   // (host: BN partials need C = A B^T)
     if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
@@ -931,7 +951,7 @@ static void check_slab(const GemmArgs& g) {
 // BATCH: a batched multi-client launch (grid.z = split-K slices x clients, client-major).  The one-client
 // instantiation carries no client prologue at all: even a never-taken client branch costs the step's latency-
 // bound GEMMs measurably (the dW0 || R0 pair 17.6 -> 21.6 us, the step 215.5 -> 223 us; profiles/README.md).
-template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool BATCH = false>
+template <bool TA, bool TB, bool F32, bool VEC, int TM, int TN, bool BIN = false, bool BATCH = false, int EK = 0>
 __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if constexpr (BATCH) {
@@ -941,8 +961,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
     gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk, gridDim.x,
                                              gridDim.y, sk, smem);
   } else {
-    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y, gridDim.z,
-                                             smem);
+    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y,
+                                                        gridDim.z, smem);
   }
 }
 
@@ -983,15 +1003,15 @@ __global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2,
                                                                b / (grid1.x * grid1.y), grid1.x, grid1.y, grid1.z, smem);
   } else {
     b -= n1;
-    gemm_tile<P2::TA, P2::TB, false, P2::VEC, P2::TM, P2::TM>(g2, b % grid2.x, (b / grid2.x) % grid2.y,
+    gemm_tile<P2::TA, P2::TB, false, P2::VEC, P2::TM, P2::TM, false, false, P2::EK>(g2, b % grid2.x, (b / grid2.x) % grid2.y,
                                                                b / (grid2.x * grid2.y), grid2.x, grid2.y, grid2.z, smem);
   }
 }
 
-template <bool TA_, bool TB_, bool VEC_, int TM_>
+template <bool TA_, bool TB_, bool VEC_, int TM_, int EK_ = 0>
 struct GemmShape {
   static constexpr bool TA = TA_, TB = TB_, VEC = VEC_;
-  static constexpr int TM = TM_;
+  static constexpr int TM = TM_, EK = EK_;
 };
 
 constexpr int GEMM_MAX_SPLITS = 64;
@@ -1154,6 +1174,13 @@ static dim3 gemm_prepare(GemmArgs& g) {
   return dim3(tn, tm, g.splitk);
 }
 
+// epilogue kind of a launch (gemm_tile's EK): a split-K slice reduced by its own launch, a plain epilogue, or any
+static int gemm_ek(const GemmArgs& g) {
+  if (g.splitk > 1 && !g.red_inl) return 2;
+  if (g.splitk > 1) return 0;   // (in-launch reduction: the generic body)
+  return g.epi == EPI_NONE ? 1 : (g.epi == EPI_MASK ? 3 : 0);
+}
+
 template <bool BATCH>
 static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds, hipStream_t stream) {
   const int T = g.tile;
@@ -1164,18 +1191,33 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
     return;
   }
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
-#define FEDTGAN_GEMM_LAYOUTS(F, V, TT)                                                                        \
-  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);       \
-  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g); \
+// (op(A) = A^T layouts are plain whatever EK says; a split one keeps the generic body)
+#define FEDTGAN_GEMM_LAYOUTS(F, V, TT, EK)                                                                        \
+  if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT, false, BATCH, EK>), grid, block, lds, stream, g);       \
+  else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT, false, BATCH, EK>), grid, block, lds, stream, g); \
   else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);   \
   else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);
-#define FEDTGAN_GEMM_TILES(F, V)       \
-  if (T == 32) {                       \
-    FEDTGAN_GEMM_LAYOUTS(F, V, 32)     \
-  } else if (T == 128) {               \
-    FEDTGAN_GEMM_LAYOUTS(F, V, 128)    \
-  } else {                             \
-    FEDTGAN_GEMM_LAYOUTS(F, V, 64)     \
+// EK variants only where the one-client step runs: bf16, 32x32 tiles, no client batch
+#define FEDTGAN_GEMM_TILES(F, V)                                    \
+  if (T == 32) {                                                    \
+    if constexpr (!(F) && !BATCH) {                                 \
+      const int ek = gemm_ek(g);                                    \
+      if (ek == 2) {                                                \
+        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 2)                           \
+      } else if (ek == 3) {                                         \
+        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 3)                           \
+      } else if (ek == 1) {                                         \
+        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 1)                           \
+      } else {                                                      \
+        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 0)                           \
+      }                                                             \
+    } else {                                                        \
+      FEDTGAN_GEMM_LAYOUTS(F, V, 32, 0)                             \
+    }                                                               \
+  } else if (T == 128) {                                            \
+    FEDTGAN_GEMM_LAYOUTS(F, V, 128, 0)                              \
+  } else {                                                          \
+    FEDTGAN_GEMM_LAYOUTS(F, V, 64, 0)                               \
   }
 #define FEDTGAN_GEMM_DISPATCH(F) \
   if (vec) {                     \
@@ -1240,14 +1282,22 @@ void launch_gemm(GemmArgs g, hipStream_t stream) {
 template <bool V1, bool V2>
 static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3 b, hipStream_t stream) {
   const dim3 grid(a.x * a.y * a.z + b.x * b.y * b.z, 1, g1.nclient), block(NT);
-#define FEDTGAN_PAIR(T1, TA2, TB2)                                                                              \
-  do {                                                                                                          \
-    if (g1.nclient > 1)                                                                                         \
-      hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>, true>),   \
-                         grid, block, 0, stream, g1, g2, a, b);                                                  \
-    else                                                                                                        \
-      hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32>, false>),  \
-                         grid, block, 0, stream, g1, g2, a, b);                                                  \
+#define FEDTGAN_PAIR_K(T1, TA2, TB2, EK2, BT)                                                                     \
+  hipLaunchKernelGGL((gemm_pair_kernel<GemmShape<true, false, V1, T1>, GemmShape<TA2, TB2, V2, 32, EK2>, BT>), grid, \
+                     block, 0, stream, g1, g2, a, b)
+#define FEDTGAN_PAIR(T1, TA2, TB2)                                         \
+  do {                                                                     \
+    if (g1.nclient > 1) {                                                  \
+      FEDTGAN_PAIR_K(T1, TA2, TB2, 0, true);                               \
+    } else if constexpr ((T1) <= 64) {                                     \
+      const int ek2 = gemm_ek(g2);                                         \
+      if (ek2 == 2) FEDTGAN_PAIR_K(T1, TA2, TB2, 2, false);                \
+      else if (ek2 == 3) FEDTGAN_PAIR_K(T1, TA2, TB2, 3, false);           \
+      else if (ek2 == 1) FEDTGAN_PAIR_K(T1, TA2, TB2, 1, false);           \
+      else FEDTGAN_PAIR_K(T1, TA2, TB2, 0, false);                         \
+    } else {                                                               \
+      FEDTGAN_PAIR_K(T1, TA2, TB2, 0, false);                              \
+    }                                                                      \
   } while (0)
   if (!(g1.ta && !g1.tb) || g2.ta || g2.tile != 32) return false;
   if (g1.tile == 64) {
@@ -1260,6 +1310,7 @@ static bool gemm_pair_vec(const GemmArgs& g1, Grid3 a, const GemmArgs& g2, Grid3
     return false;
   }
 #undef FEDTGAN_PAIR
+#undef FEDTGAN_PAIR_K
   return true;
 }
 
