@@ -1021,7 +1021,8 @@ int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch
 int g_gemm_splitk_inlaunch = 1;   // 1: split-K reduced by the last-arriving slice (GemmArgs::tile_cnt)
 
 // the reduced, epilogue-applied value of output idx = m * N + n (stored to C by the caller)
-template <int SMAX>
+// MASK: the epilogue is EPI_MASK (host-checked) -- no Philox / BN code in the launch (see gemm_tile's EK)
+template <int SMAX, bool MASK = false>
 __device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int m, int n, uint64_t step) {
   const int splits = g.splitk;
   const size_t total = (size_t)g.M * g.N;
@@ -1037,6 +1038,7 @@ __device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int
   if (g.beta != 0.f) v += g.beta * (*cp);
   if (g.bias) v += g.bias[n];
   if (g.oh_w) v += onehot_term(g, m, n);
+  if constexpr (MASK) return v * g.ms[(size_t)m * g.ldms + n];
   return apply_epi(g, v, m, n, step, idx);
 }
 
@@ -1060,7 +1062,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
 // The discriminator's second layer (150 or 50 x 256 x 256) and its R-chain link R1 = (R0 W1^T) . MS1
 // were launches of their own after D0's / R0's reduction.
 constexpr int CH_MAXK = 1024, CH_COLS = 64;
-template <int SMAX>
+// MASK: head and tail both EPI_MASK (the R chain) -- the launch carries no Philox / BN epilogue code
+template <int SMAX, bool MASK = false>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
   __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
   __shared__ float part[4][CH_COLS];
@@ -1073,7 +1076,7 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
   for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
     float v;
     if constexpr (SMAX > 0) {
-      v = splitk_value<SMAX>(g, (size_t)m * g.N + n, m, n, step);
+      v = splitk_value<SMAX, MASK>(g, (size_t)m * g.N + n, m, n, step);
       if (s == 0) st_out(g.c, (size_t)m * g.ldc + n, v, g.wt);
     } else {
       v = g.c[(size_t)m * g.ldc + n];
@@ -1103,7 +1106,8 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
     float v = t.alpha * ((part[0][jl] + part[1][jl]) + (part[2][jl] + part[3][jl]));
     if (t.bias) v += t.bias[j];
     const uint64_t st = (t.epi == EPI_LRELU_DROPOUT && t.rng_ctr) ? *t.rng_ctr : 0ull;
-    t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+    if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
+    else t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
   }
 }
 
@@ -1250,11 +1254,18 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     t.seed_step = g.seed_step;
     t.nclient = g.nclient;
     const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS, g.nclient), block(256);
-    if (g.splitk <= 1 || g.red_inl) hipLaunchKernelGGL(chain_epilogue_kernel<0>, grid, block, 0, stream, h, t);
-    else if (g.splitk <= 8) hipLaunchKernelGGL(chain_epilogue_kernel<8>, grid, block, 0, stream, h, t);
-    else if (g.splitk <= 16) hipLaunchKernelGGL(chain_epilogue_kernel<16>, grid, block, 0, stream, h, t);
-    else if (g.splitk <= 32) hipLaunchKernelGGL(chain_epilogue_kernel<32>, grid, block, 0, stream, h, t);
-    else hipLaunchKernelGGL(chain_epilogue_kernel<64>, grid, block, 0, stream, h, t);
+    const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
+#define FEDTGAN_CHAIN(S)                                                                                 \
+  do {                                                                                                   \
+    if (mk) hipLaunchKernelGGL((chain_epilogue_kernel<S, true>), grid, block, 0, stream, h, t);          \
+    else hipLaunchKernelGGL((chain_epilogue_kernel<S, false>), grid, block, 0, stream, h, t);            \
+  } while (0)
+    if (g.splitk <= 1 || g.red_inl) FEDTGAN_CHAIN(0);
+    else if (g.splitk <= 8) FEDTGAN_CHAIN(8);
+    else if (g.splitk <= 16) FEDTGAN_CHAIN(16);
+    else if (g.splitk <= 32) FEDTGAN_CHAIN(32);
+    else FEDTGAN_CHAIN(64);
+#undef FEDTGAN_CHAIN
     return;
   }
   if (g.splitk <= 1 || g.red_inl) return;
