@@ -958,8 +958,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
     const int sk = (int)gridDim.z / g.nclient;
     const int cl = (int)blockIdx.z / sk;
     if (cl) client_view(g, cl);
-    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk, gridDim.x,
-                                             gridDim.y, sk, smem);
+    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk,
+                                                        gridDim.x, gridDim.y, sk, smem);
   } else {
     gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y,
                                                         gridDim.z, smem);
@@ -1201,27 +1201,29 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
   else if (!g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<false, false, F, V, TT, TT, false, BATCH, EK>), grid, block, lds, stream, g); \
   else if (g.ta && !g.tb) hipLaunchKernelGGL((gemm_kernel<true, false, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);   \
   else hipLaunchKernelGGL((gemm_kernel<true, true, F, V, TT, TT, false, BATCH>), grid, block, lds, stream, g);
-// EK variants only where the one-client step runs: bf16, 32x32 tiles, no client batch
+// EK variants for the bf16 32x32 and 64x64 tiles (the one-client step runs 32-tiles; the batched step 64-tiles)
+#define FEDTGAN_GEMM_EK(F, V, TT)                                   \
+  if constexpr (!(F)) {                                             \
+    const int ek = gemm_ek(g);                                      \
+    if (ek == 2) {                                                  \
+      FEDTGAN_GEMM_LAYOUTS(F, V, TT, 2)                             \
+    } else if (ek == 3) {                                           \
+      FEDTGAN_GEMM_LAYOUTS(F, V, TT, 3)                             \
+    } else if (ek == 1) {                                           \
+      FEDTGAN_GEMM_LAYOUTS(F, V, TT, 1)                             \
+    } else {                                                        \
+      FEDTGAN_GEMM_LAYOUTS(F, V, TT, 0)                             \
+    }                                                               \
+  } else {                                                          \
+    FEDTGAN_GEMM_LAYOUTS(F, V, TT, 0)                               \
+  }
 #define FEDTGAN_GEMM_TILES(F, V)                                    \
   if (T == 32) {                                                    \
-    if constexpr (!(F) && !BATCH) {                                 \
-      const int ek = gemm_ek(g);                                    \
-      if (ek == 2) {                                                \
-        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 2)                           \
-      } else if (ek == 3) {                                         \
-        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 3)                           \
-      } else if (ek == 1) {                                         \
-        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 1)                           \
-      } else {                                                      \
-        FEDTGAN_GEMM_LAYOUTS(F, V, 32, 0)                           \
-      }                                                             \
-    } else {                                                        \
-      FEDTGAN_GEMM_LAYOUTS(F, V, 32, 0)                             \
-    }                                                               \
+    FEDTGAN_GEMM_EK(F, V, 32)                                       \
   } else if (T == 128) {                                            \
     FEDTGAN_GEMM_LAYOUTS(F, V, 128, 0)                              \
   } else {                                                          \
-    FEDTGAN_GEMM_LAYOUTS(F, V, 64, 0)                               \
+    FEDTGAN_GEMM_EK(F, V, 64)                                       \
   }
 #define FEDTGAN_GEMM_DISPATCH(F) \
   if (vec) {                     \
@@ -1235,6 +1237,7 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
     FEDTGAN_GEMM_DISPATCH(false)
   }
 #undef FEDTGAN_GEMM_TILES
+#undef FEDTGAN_GEMM_EK
 #undef FEDTGAN_GEMM_LAYOUTS
 #undef FEDTGAN_GEMM_DISPATCH
 }
