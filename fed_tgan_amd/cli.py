@@ -144,6 +144,17 @@ def device_index(local: int, ngpu: int, colocated: bool, mode: str = "fedavg") -
     return local % ngpu if (colocated or mode == "mdgan") else max(local - 1, 0) % ngpu
 
 
+def clients_own_gpus(world: int, colocated: bool) -> bool:
+    """Does every client rank of this node get a GPU no other client uses (RCCL: one rank per device)?
+    A dedicated federator (rank 0, not a client) may share one."""
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    if not n:
+        return False
+    clients = range(world) if colocated else range(1, world)
+    idx = [device_index(r, n, colocated) for r in clients]
+    return len(set(idx)) == len(idx)
+
+
 def gpus_shared(world: int, colocated: bool, mode: str = "fedavg") -> bool:
     """Will several ranks of this node run on one GPU (a dedicated federator next to client 1, or
     more clients than GPUs)?"""
@@ -177,8 +188,9 @@ def cap_shared_queues() -> None:
         os.environ["GPU_MAX_HW_QUEUES"] = str(target)
 
 
-def run_rank(rank: int, args) -> None:
-    """One process of the federation (the reference ``run()``, `Server/dtds/distributed.py:838-891`)."""
+def run_rank(rank: int, args, on_done=None) -> None:
+    """One process of the federation (the reference ``run()``, `Server/dtds/distributed.py:838-891`).
+    ``on_done(runtime, comm)`` (probes, tests) runs after the last round, before the process groups close."""
     from .fed.runtime import FedRuntime
     from .fed.mdgan import MDGANRuntime
     from .parallel.comm import Comm
@@ -200,7 +212,12 @@ def run_rank(rank: int, args) -> None:
         if args.mode == "mdgan":
             data_backend = "nccl" if (device.type == "cuda" and world <= torch.cuda.device_count()) else "gloo"
         else:
-            data_backend = "nccl" if (device.type == "cuda" and colocated) else "gloo"
+            # RCCL among the client ranks whenever every client has a GPU of its own; a dedicated federator
+            # stays outside the RCCL group and receives the aggregate from the first client
+            # (Comm.share_with_federator)
+            data_backend = "nccl" if (device.type == "cuda" and clients_own_gpus(world, colocated)) else "gloo"
+    if not args.quiet:
+        print(f"[rank {rank}] data plane {data_backend} over client ranks {client_ranks}", flush=True)
     comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
     try:
         if args.local_clients:      # K clients as threads of this rank: clients rank*K .. rank*K+K-1
@@ -213,6 +230,8 @@ def run_rank(rank: int, args) -> None:
         rt = cls(fed_config_from_args(args), comm, device, federator=0)
         rt.initialize()
         rt.fit()
+        if on_done is not None:
+            on_done(rt, comm)
         comm.barrier()
     finally:
         comm.destroy()

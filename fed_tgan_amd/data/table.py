@@ -120,7 +120,16 @@ class TablePreprocessor:
         Cached: ``local_meta`` and ``encode`` both need it."""
         hit = self._cat_cache.get(c)
         if hit is None:
-            codes, uniq = pd.factorize(self.df[c], use_na_sentinel=False)
+            col = self.df[c]
+            if col.dtype == object and pd.api.types.infer_dtype(col, skipna=False) != "string":
+                # factorize merges objects that hash and compare equal (1, 1.0, True) although they print
+                # differently ('1', '1.0', 'True'): key a mixed object column by (type, value)
+                keys = pd.Series([(type(v).__name__, v if v == v else None) for v in col.tolist()], dtype=object)
+                codes, _ = pd.factorize(keys, use_na_sentinel=False)
+                first = pd.Series(np.arange(len(codes))).groupby(codes).first().to_numpy()
+                uniq = col.to_numpy()[first]
+            else:
+                codes, uniq = pd.factorize(col, use_na_sentinel=False)
             strs = pd.Index(uniq).astype(str)
             remap, labels = pd.factorize(strs)          # distinct raw values that print the same merge
             hit = (remap[codes], np.asarray(labels, dtype=object))

@@ -56,3 +56,26 @@ class CategoryVocab:
 
     def __repr__(self) -> str:
         return f"CategoryVocab({self.column_name!r}, n={len(self)})"
+
+
+def write_label_encoders(path: str, vocabs: Sequence[CategoryVocab]) -> str:
+    """``label_encoders_{name}.pickle``: a list of ``{column_name, label_encoder}`` with sklearn
+    ``LabelEncoder`` objects (`Server/dtds/distributed.py:669-684`).  Written to a temporary name and
+    renamed, so a reader never sees a partial file."""
+    import os
+    import pickle
+    les = [{"column_name": v.column_name, "label_encoder": v.to_sklearn()} for v in vocabs]
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "wb") as f:
+        pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
+    os.replace(tmp, path)
+    return path
+
+
+if __name__ == "__main__":
+    # helper process of the federated runtime (fed/runtime.py start_label_encoders): the sklearn import
+    # and the pickle happen here, off the federator's critical path.  stdin: {"path", "vocabs": [[name, classes]]}
+    import json
+    import sys
+    req = json.load(sys.stdin)
+    write_label_encoders(req["path"], [CategoryVocab(c, n) for n, c in req["vocabs"]])

@@ -38,6 +38,22 @@ class LocalGroup:
         # thread 0 then issues every client's training steps, the FedAvg and the generation
         self.batch = None
         self.lock = threading.Lock()
+        self._acc = None
+
+    def reduce_buffer(self, like: torch.Tensor) -> torch.Tensor:
+        """The accumulator of ``stream_reduce`` (kept across rounds: the other threads' streams read it
+        after the host has moved on, so it must never return to the caching allocator mid-round)."""
+        if self._acc is None or self._acc.shape != like.shape or self._acc.device != like.device:
+            self._acc = torch.empty_like(like)
+        return self._acc
+
+    def local_all(self, t: int, ok: bool) -> bool:
+        """Host-side AND of a flag over the group's threads (collective)."""
+        self.slots[t] = bool(ok)
+        self.wait()
+        out = all(self.slots)
+        self.wait()
+        return out
 
     def wait(self):
         if self.failed.is_set():
@@ -46,6 +62,50 @@ class LocalGroup:
             self.barrier.wait(timeout=3600)
         except threading.BrokenBarrierError:
             raise RuntimeError("emulated federation aborted")
+
+
+def _stream_event(t: torch.Tensor):
+    """An event recorded on the current stream of ``t``'s device (None for a host tensor)."""
+    if not t.is_cuda:
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+
+def stream_reduce(g: LocalGroup, t: int, flat: torch.Tensor, weight: float, outer=None) -> torch.Tensor:
+    """sum_i w_i * flat_i over the threads of ``g``; every thread ends holding the sum in ``flat``.
+
+    The threads' HIP streams are ordered by events, exchanged at host barriers: thread i records an
+    event once its ``flat`` is final; thread 0's stream waits for every one of them, accumulates into a
+    buffer kept by the group, runs ``outer(acc)`` (HierComm: the process-level all-reduce), and records
+    a done event; every thread's stream waits for that event and copies the sum.  The host never waits
+    for the device, and the clients' kernels keep running while the host exchanges events (the thread
+    path used to synchronise the whole device three times per round)."""
+    g.slots[t] = (flat, float(weight), _stream_event(flat))
+    g.wait()
+    if t == 0:
+        parts = list(g.slots)
+        if flat.is_cuda:
+            cur = torch.cuda.current_stream(flat.device)
+            for _, _, ev in parts:
+                if ev is not None:
+                    cur.wait_event(ev)
+        acc = g.reduce_buffer(flat)
+        acc.zero_()
+        for buf, w, _ in parts:
+            if w != 0.0:
+                acc.add_(buf, alpha=w)
+        if outer is not None:
+            outer(acc)
+        g.result = (acc, _stream_event(acc))
+    g.wait()
+    acc, done = g.result
+    if t != 0 and done is not None:
+        torch.cuda.current_stream(flat.device).wait_event(done)
+    flat.copy_(acc)
+    g.wait()        # g.result stays valid until every thread has read it
+    return flat
 
 
 class ThreadComm(Comm):
@@ -113,33 +173,17 @@ class ThreadComm(Comm):
     def weighted_all_reduce(self, flat, weight: float):
         """sum_i w_i * flat_i: every rank posts (buffer, weight); rank 0 accumulates on the device.
         Batched clients (the buffers live in one arena): thread 0 reduces over the arena on its stream,
-        the stream every client's training ran on -- no device synchronisation, no copies."""
+        the stream every client's training ran on -- no copies.  Otherwise the clients' streams are
+        ordered by events (``stream_reduce``).  No host synchronisation with the device either way."""
         b = self.g.batch
         if b is not None and flat.is_cuda and b.owns(flat):
             self.g.slots[self.rank] = float(weight)
             self.g.wait()
             if self.rank == 0:
-                b.weighted_average(list(self.g.slots))
+                b.weighted_average(b.slab_weights(list(self.g.slots)))
             self.g.wait()
             return flat
-        if flat.is_cuda:
-            device_sync(flat.device)
-        self.g.slots[self.rank] = (flat, float(weight))
-        self.g.wait()
-        if self.rank == 0:
-            acc = torch.zeros_like(flat)
-            for buf, w in self.g.slots:
-                if w != 0.0:
-                    acc.add_(buf, alpha=w)
-            if flat.is_cuda:
-                device_sync(flat.device)
-            self.g.result = acc
-        self.g.wait()
-        flat.copy_(self.g.result)
-        if flat.is_cuda:
-            device_sync(flat.device)
-        self.g.wait()
-        return flat
+        return stream_reduce(self.g, self.rank, flat, weight)
 
 
 class HierComm(Comm):
@@ -238,22 +282,20 @@ class HierComm(Comm):
     # ---- data plane
     def weighted_all_reduce(self, flat, weight: float):
         """sum_i w_i * flat_i: the process' clients are summed on its GPU by thread 0, which then
-        runs ONE process-level all-reduce (weight 1: the terms are already scaled)."""
-        self._sync()
-        parts = self._tgather((flat, float(weight)))
-
-        def reduce():
-            acc = torch.zeros_like(flat)
-            for buf, w in parts:
-                if w != 0.0:
-                    acc.add_(buf, alpha=w)
-            self.outer.weighted_all_reduce(acc, 1.0)
-            self._sync()
-            return acc
-        flat.copy_(self._lead(reduce))
-        self._sync()
-        self.g.wait()
-        return flat
+        runs ONE process-level all-reduce (weight 1: the terms are already scaled).  Batched clients:
+        the local sum is one reduction over the arena (models/batched.py), the aggregate is copied into
+        every slab; otherwise the threads' streams are ordered by events (``stream_reduce``)."""
+        b = self.g.batch
+        if b is not None and flat.is_cuda and b.owns(flat):
+            self.g.slots[self.t] = float(weight)
+            self.g.wait()
+            if self.t == 0:
+                agg = b.weighted_sum(b.slab_weights(list(self.g.slots)))
+                self.outer.weighted_all_reduce(agg, 1.0)
+                b.set_all(agg)
+            self.g.wait()
+            return flat
+        return stream_reduce(self.g, self.t, flat, weight, outer=lambda acc: self.outer.weighted_all_reduce(acc, 1.0))
 
     def share_with_federator(self, flat, federator: int = 0):
         return flat         # co-located: the federator is a client and already holds the aggregate
@@ -262,17 +304,20 @@ class HierComm(Comm):
         """The process' client shares are concatenated on its GPU, then one process-level gather."""
         if list(ranks) != self.client_ranks:
             raise ValueError("HierComm.gather_rows gathers from every client, in client order")
-        self._sync()
-        parts = self._tgather(t)
+        parts = self._tgather((t, _stream_event(t)))
         k, n = self.k, self.outer.world_size
 
         def gather():
             me = self.outer.rank
-            local = torch.cat([p[:counts[me * k + i]] for i, p in enumerate(parts)])
+            if t.is_cuda:      # thread 0's stream waits for every thread's rows (events, no host sync)
+                cur = torch.cuda.current_stream(t.device)
+                for p, ev in parts:
+                    if ev is not None:
+                        cur.wait_event(ev)
+                    p.record_stream(cur)     # freed by its thread later: not reused before this stream reads it
+            local = torch.cat([p[:counts[me * k + i]] for i, (p, _) in enumerate(parts)])
             per = [sum(counts[q * k:(q + 1) * k]) for q in range(n)]
-            out = self.outer.gather_rows(local, per, list(range(n)), dst=dst // k, to_host=to_host)
-            self._sync()
-            return out
+            return self.outer.gather_rows(local, per, list(range(n)), dst=dst // k, to_host=to_host)
         out = self._lead(gather)
         return out if self.rank == dst else None
 

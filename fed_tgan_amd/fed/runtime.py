@@ -33,7 +33,6 @@ import contextlib
 import dataclasses
 import json
 import os
-import pickle
 import threading
 import time
 from typing import Dict, List, Optional
@@ -126,6 +125,7 @@ class FedConfig:
     # 8 clients 58.4 vs 48.8 -- the batched kernels are throughput-bound at 8 clients' work
     batched_clients: str = "auto"
     batched_max_auto: int = 4
+    batched_arena_mb: float = 0.0           # per-client arena slab of the batched engine (0: estimated)
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -279,6 +279,7 @@ class FedRuntime:
         self.cat_idx = cat_idx
         if self.is_fed:
             self._write_meta_artifacts()
+            self.start_label_encoders()
         if warm is not None:
             warm.join()
         self.init_times = {"meta": time.time() - t0}
@@ -331,22 +332,35 @@ class FedRuntime:
         if self.device.type == "cuda":
             with torch.cuda.device(self.device):
                 torch.cuda.manual_seed(cfg.seed + self.rank)
+        self.steps = [n // cfg.engine.batch_size for n in self.rows]
+        self.engine = None
         batch = self._batch_group(lay)
         if batch is not None:
-            self.engine = batch.engine_for(c.client_index, lay, cfg.engine, cfg.seed * 7919 + self.rank,
-                                           backend=cfg.backend)
-        else:
+            # (a slab too small for a client's tables raises here: in "auto" mode every thread of the process
+            # then falls back to an engine of its own, see _batch_ready)
+            failed = None
+            try:
+                self.engine = batch.engine_for(self.batch_slab, lay, cfg.engine, self.batch_seed, backend=cfg.backend)
+                self.engine.set_training_data(self.train_matrix)
+            except MemoryError as e:
+                failed = e
+            if not self._batch_ready(failed):
+                self.engine = None
+        if self.engine is None:
             self.engine = CTGANEngine(lay, cfg.engine, self.device, backend=cfg.backend,
                                       seed=cfg.seed * 7919 + self.rank)
+            if self.is_client:
+                self.engine.set_training_data(self.train_matrix)
         if getattr(self, "thread_local_capture", False):
             self.engine.capture_mode = "thread_local"
-        if self.is_client:
-            self.engine.set_training_data(self.train_matrix)
         self.engine.set_generation_tables(self.gen_cond, self.transformer)
         self._initial_weights()
-        self.steps = [n // cfg.engine.batch_size for n in self.rows]
         if cfg.resume:
             self.load_checkpoint()
+        if self.batched:
+            # freeze the arena and capture the epoch's step graphs now (collective over the process' client
+            # threads): a failure falls back to per-thread engines instead of aborting round 0
+            self._prepare_batched()
         self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
         self.init_times["engine"] = time.time() - t0
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
@@ -361,27 +375,98 @@ class FedRuntime:
         cfg, c = self.cfg, self.comm
         g = getattr(c, "g", None)
         self.batched = False
-        if cfg.batched_clients == "off" or g is None or type(c).__name__ != "ThreadComm" or not self.is_client:
+        kind = type(c).__name__
+        if cfg.batched_clients == "off" or g is None or kind not in ("ThreadComm", "HierComm") or not self.is_client:
             return None
-        ok = (self.device.type == "cuda" and cfg.backend in ("auto", "hip") and len(set(self.rows)) == 1 and
-              cfg.drop_client_prob <= 0 and c.client_ranks == list(range(c.world_size)) and c.n_clients > 1 and
-              cfg.mode == "fedavg")
-        if ok and cfg.batched_clients == "auto" and c.n_clients > cfg.batched_max_auto:
+        # this process' clients are the threads of g: client (rank - t) + i is thread i
+        t = c.t if kind == "HierComm" else c.rank
+        first = self.rank - t
+        local_rows = self.rows[first:first + g.k]
+        ok = (self.device.type == "cuda" and cfg.backend in ("auto", "hip") and cfg.drop_client_prob <= 0 and
+              c.client_ranks == list(range(c.world_size)) and g.k > 1 and cfg.mode == "fedavg")
+        if ok and cfg.batched_clients == "auto" and g.k > cfg.batched_max_auto:
             return None
         if not ok:
             if cfg.batched_clients == "on":
-                raise RuntimeError("batched_clients='on' needs a GPU, the HIP backend, equal client row counts, "
+                raise RuntimeError("batched_clients='on' needs a GPU, the HIP backend, several clients per process, "
                                    "every rank a client and no fault injection")
             return None
         from ..models.arena import Arena
-        from ..models.batched import BatchedClients
+        from ..models.batched import BatchedClients, slab_order
+        # slabs in non-increasing order of steps per epoch (clients with fewer rows finish their epoch first and
+        # leave the batched launches; models/batched.py); engine seeds consecutive in slab order
+        order = slab_order([n // cfg.engine.batch_size for n in local_rows])
+        self.batch_slab = order.index(t)
+        self.batch_seed = cfg.seed * 7919 + first + self.batch_slab
+        self._local_t = t
         with g.lock:
             if g.batch is None:
-                g.batch = BatchedClients.empty(c.n_clients, self.device,
-                                               Arena.estimate_slab_bytes(lay, cfg.engine, max(self.rows)))
+                slab = int(cfg.batched_arena_mb * (1 << 20)) or \
+                    Arena.estimate_slab_bytes(lay, cfg.engine, max(local_rows))
+                g.batch = BatchedClients.empty(g.k, self.device, slab, n_rows=max(local_rows))
+                g.batch.client_of_slab = order
         self.batched = True
         self.batch_clients = g.batch       # (strong reference: the engine only holds a weak one)
         return g.batch
+
+    def _batch_ready(self, err: Optional[BaseException]) -> bool:
+        """Collective over the process' client threads: did every thread build its slab engine?  If not,
+        "auto" mode falls back to one engine per thread (False), "on" mode raises."""
+        g = self.comm.g
+        if g.local_all(self._local_t, err is None):
+            return True
+        if self.cfg.batched_clients == "on":
+            raise RuntimeError(f"batched clients: a client's engine does not fit its arena slab ({err}); "
+                               "raise FedConfig.batched_arena_mb") from err
+        _log(self.cfg, self.rank, f"[init] batched clients do not fit the arena ({err}): one engine per client")
+        self._drop_batch()
+        return False
+
+    def _drop_batch(self):
+        g = self.comm.g
+        g.wait()
+        if self._local_t == 0:
+            g.batch = None
+        self.batched = False
+        self.batch_clients = None
+        g.wait()
+
+    def _prepare_batched(self):
+        """Collective over the process' client threads: thread 0 freezes the arena (one device sync: every
+        thread's initial state is on the device) and captures the epoch's step graphs.  On a failure
+        ("auto" mode) every thread continues with an engine of its own, holding its client's state."""
+        g, t = self.comm.g, self._local_t
+        g.wait()                    # every thread's initial weights / checkpoint are enqueued
+        err = None
+        if t == 0:
+            try:
+                self.batch_clients.prepare(self.cfg.use_graph)
+            except (MemoryError, RuntimeError) as e:
+                err = e
+                if hasattr(self.engine.ops, "reset_held"):
+                    self.engine.ops.reset_held()
+        if g.local_all(t, err is None):
+            return
+        if self.cfg.batched_clients == "on":
+            raise RuntimeError(f"batched clients: preparing the batched step failed ({err})") from err
+        _log(self.cfg, self.rank, f"[init] batched step unavailable ({err}): one engine per client")
+        if t == 0:
+            from ..utils.devsync import device_sync
+            device_sync(self.device)
+        g.wait()
+        old = self.engine
+        e = CTGANEngine(old.layout, self.cfg.engine, self.device, backend=self.cfg.backend,
+                        seed=self.cfg.seed * 7919 + self.rank)
+        e.capture_mode = old.capture_mode
+        e.set_training_data(self.train_matrix)
+        e.set_generation_tables(self.gen_cond, self.transformer)
+        for name in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
+            getattr(e, name).copy_(getattr(old, name))
+        if hasattr(e.ops, "ctr"):
+            e.ops.ctr.copy_(old.ops.ctr)
+        e.bn_batches = old.bn_batches
+        self.engine = e
+        self._drop_batch()
 
     def _initial_weights(self):
         """Step F: the clients keep their own random init (reference) or adopt the first client's;
@@ -418,16 +503,48 @@ class FedRuntime:
         os.makedirs(mdir, exist_ok=True)
         dump_meta_json(self.global_meta, os.path.join(mdir, f"{self.name}.json"))
 
-    def write_label_encoders(self):
-        """``models/label_encoders_{name}.pickle`` (`Server/dtds/distributed.py:679-684`).
-
-        Written after training, not during initialisation: building sklearn ``LabelEncoder`` objects
-        imports scikit-learn (0.5-0.9 s), which sat on the critical path of every run's start."""
+    def _label_encoder_path(self) -> str:
         mdir = os.path.join(self.cfg.out_dir, "models")
         os.makedirs(mdir, exist_ok=True)
-        les = [{"column_name": v.column_name, "label_encoder": v.to_sklearn()} for v in self.vocabs]
-        with open(os.path.join(mdir, f"label_encoders_{self.name}.pickle"), "wb") as f:
-            pickle.dump(les, f, protocol=pickle.HIGHEST_PROTOCOL)
+        return os.path.join(mdir, f"label_encoders_{self.name}.pickle")
+
+    def start_label_encoders(self):
+        """Start writing ``models/label_encoders_{name}.pickle`` during initialisation, as the reference
+        does (`Server/dtds/distributed.py:679-684`), so a crashed or killed run still leaves it next to
+        the meta JSON.  Building sklearn ``LabelEncoder`` objects imports scikit-learn (0.5-0.9 s of
+        Python), so a helper process does it (data/vocab.py ``__main__``): neither this process' GIL nor
+        its critical path sees the import.  ``write_label_encoders`` waits for it."""
+        import subprocess
+        import sys
+        self._le_proc = None
+        req = json.dumps({"path": os.path.abspath(self._label_encoder_path()),
+                          "vocabs": [[v.column_name, v.tolist()] for v in self.vocabs]})
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        try:
+            p = subprocess.Popen([sys.executable, "-m", "fed_tgan_amd.data.vocab"], stdin=subprocess.PIPE,
+                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
+            p.stdin.write(req.encode())
+            p.stdin.close()
+            self._le_proc = p
+        except OSError:
+            self._le_proc = None
+
+    def write_label_encoders(self):
+        """Make sure ``models/label_encoders_{name}.pickle`` exists: wait for the helper process of
+        ``start_label_encoders``, or write the file here if there was none or it failed."""
+        p = getattr(self, "_le_proc", None)
+        self._le_proc = None
+        if p is not None:
+            try:
+                _, err = p.communicate(timeout=120)
+                if p.returncode == 0 and os.path.exists(self._label_encoder_path()):
+                    return self._label_encoder_path()
+                print(f"[init] label-encoder helper failed ({p.returncode}): {err.decode()[-300:]}", flush=True)
+            except Exception:            # noqa: BLE001 - fall back to an in-process write
+                p.kill()
+        from ..data.vocab import write_label_encoders
+        return write_label_encoders(self._label_encoder_path(), self.vocabs)
 
     # ================================================================= rounds
     def _sub(self, name: str):
@@ -543,13 +660,14 @@ class FedRuntime:
         alive = round_alive_mask(self.cfg, epoch, c.n_clients)
         with self.timer.phase("train", self.device):
             if getattr(self, "batched", False):
-                # every client's epoch in one batched launch sequence, issued by client 0's thread
-                c.barrier()
-                if c.client_index == 0:
+                # every client's epoch in one batched launch sequence, issued by the process' thread 0 (host
+                # barriers over the process' threads only; the device work is on thread 0's stream)
+                c.g.wait()
+                if self._local_t == 0:
                     self.batch_clients.train_epoch(self.cfg.use_graph)
                     if self.gradflow is not None:
                         self.gradflow.update(self.engine)
-                c.barrier()
+                c.g.wait()
             elif self.is_client and alive[c.client_index]:
                 self.engine.train_epoch(self.cfg.use_graph)
                 if self.gradflow is not None:

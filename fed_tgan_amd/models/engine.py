@@ -194,6 +194,7 @@ class CTGANEngine:
         self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
         self.batch = None         # models/batched.py BatchedClients when this engine issues K clients' steps
+        self.pad_rows = None      # batched clients: row tables sized for the largest client (set_training_data)
 
     # ================================================================= parameters
     def _build_params(self):
@@ -438,21 +439,32 @@ class CTGANEngine:
         """encoded: the host matrix [N, data_dim], or a ``DeviceEncoded`` from the HIP encoder
         (matrix, row lists and counts already on the device)."""
         lay = self.layout
-        dev = self.device
         dev_enc = hasattr(encoded, "opt") and hasattr(encoded, "rows")
         mk = self.mem.tensor
+        n = len(encoded)
+        # the batched engine's clients may hold different row counts (models/batched.py): every slab then
+        # reserves the largest client's row tables (identical layouts), filled up to this client's rows
+        pad = max(int(self.pad_rows or 0), n)
+
+        def rows_of(data, per_row: int = 1, dtype=None):
+            src = torch.as_tensor(data, dtype=dtype)
+            if src.shape[0] == pad * per_row:
+                return mk(src)
+            out = self.mem.zeros(pad * per_row, *src.shape[1:], dtype=src.dtype)
+            out[:src.shape[0]].copy_(src)
+            return out
         if dev_enc:
             cond = cond or CondTables(lay, encoded.counts)
             rt = encoded.rows
-            t = {"data": mk(encoded.data), "row_offset": mk(rt["row_offset"]), "row_count": mk(rt["row_count"]),
-                 "rows": mk(rt["rows"])}
+            t = {"data": rows_of(encoded.data), "row_offset": mk(rt["row_offset"]), "row_count": mk(rt["row_count"]),
+                 "rows": rows_of(rt["rows"], lay.n_col)}
         else:
             rows = rows or RowIndex(encoded, lay)
             cond = cond or CondTables.from_encoded(encoded, lay)
-            t = {"data": mk(np.ascontiguousarray(encoded, dtype=np.float32)),
+            t = {"data": rows_of(np.ascontiguousarray(encoded, dtype=np.float32)),
                  "row_offset": mk(np.asarray(rows.offset), dtype=torch.int64),
                  "row_count": mk(np.asarray(rows.count), dtype=torch.int64),
-                 "rows": mk(np.asarray(rows.rows), dtype=torch.int64)}
+                 "rows": rows_of(np.asarray(rows.rows), lay.n_col, dtype=torch.int64)}
         t.update({
             "cdf_log": mk(np.asarray(cond.cdf_log), dtype=torch.float32),
             "cdf_emp": mk(np.asarray(cond.cdf_emp), dtype=torch.float32),
@@ -868,12 +880,12 @@ class CTGANEngine:
             U = max(1, int(self.cfg.graph_unroll))
             left = n
             if left >= U:
-                g = self.graphs.get(U) or self._capture(U)
+                g = self.graphs.get(self._graph_key(U)) or self._capture(U)
                 for _ in range(left // U):
                     g.replay()
                 left %= U
             if left:
-                g1 = self.graphs.get(1) or self._capture(1)
+                g1 = self.graphs.get(self._graph_key(1)) or self._capture(1)
                 for _ in range(left):
                     g1.replay()
         else:
@@ -885,6 +897,12 @@ class CTGANEngine:
 
     def train_epoch(self, use_graph: bool | None = None):
         self.train_steps(self.steps_per_epoch, use_graph)
+
+    def _graph_key(self, steps: int):
+        """Captured step graphs are per (steps, clients): a batched engine whose clients hold different row
+        counts runs the tail of an epoch with fewer clients per launch (models/batched.py)."""
+        k = getattr(self.ops, "batch_k", 1)
+        return steps if k == 1 else (steps, k)
 
     def _capture(self, steps: int = 1):
         from ..utils.devsync import CAPTURE_LOCK
@@ -912,7 +930,7 @@ class CTGANEngine:
         with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
             for _ in range(steps):      # every step re-reads the device RNG/step counters
                 self._one_step()
-        self.graphs[steps] = g
+        self.graphs[self._graph_key(steps)] = g
         return g
 
     @property

@@ -160,13 +160,61 @@ def test_batched_launch_refuses_buffers_outside_the_arena():
 
 
 @pytest.mark.gpu
-def test_batched_clients_refuse_unequal_tables():
+def test_batched_clients_refuse_misordered_or_oversized_tables():
+    """Slabs must hold the clients in non-increasing order of steps per epoch, and no client may hold more
+    rows than the arena's row tables were sized for (n_rows)."""
     from fed_tgan_amd.models.batched import BatchedClients
     from fed_tgan_amd.ops import native
     native.require()
     _, _, _, _, _, _, tr, X = small_table(2000, 0)
     bc = BatchedClients(tr.layout, EngineConfig(batch_size=500), DEV, [5, 6], n_rows=len(X))
+    bc.engines[0].set_training_data(X[:1500])
+    bc.engines[1].set_training_data(X)
+    with pytest.raises(RuntimeError, match="non-increasing"):
+        bc.train_steps(1, use_graph=False)
+    bc = BatchedClients(tr.layout, EngineConfig(batch_size=500), DEV, [5, 6], n_rows=1500)
     bc.engines[0].set_training_data(X)
     bc.engines[1].set_training_data(X[:1500])
-    with pytest.raises(RuntimeError):
+    with pytest.raises(RuntimeError, match="mirror"):
         bc.train_steps(1, use_graph=False)
+
+
+@pytest.mark.gpu
+def test_batched_ragged_clients_bit_identical_to_single_engines():
+    """Clients with different row counts (non-IID shards) in one batched engine: each trains its own
+    len(rows) // batch steps per epoch (`Client/.../dtds/distributed.py:155, 186`) and ends every epoch
+    bit-identical to a single engine with its own row count.  Epoch segments here: 3 clients x 2 steps
+    (one-step graphs), 2 x 8 (an 8-step graph), then the largest client alone for 8 (plain launches)."""
+    from fed_tgan_amd.models.batched import BatchedClients
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table(4000, 0)
+    rng = np.random.default_rng(11)
+    rows = [9000, 5000, 1000]
+    data = [X[rng.integers(0, len(X), n)] for n in rows]
+    # no D1 chain / fused D Adam: the launch sequence of one client alone (k = 1) is then the batched one
+    cfg = EngineConfig(batch_size=500, chain_d1=False, fuse_d_adam=False)
+    seeds = [3000 + c for c in range(3)]
+    bc = BatchedClients(tr.layout, cfg, DEV, seeds, n_rows=max(rows))
+    bc.engines[0].ops.batch_plan = False
+    for e, Xc in zip(bc.engines, data):
+        e.set_training_data(Xc)
+    assert bc.steps() == [18, 10, 2] and bc._segments() == [(3, 2), (2, 8), (1, 8)]
+    plain = []
+    for s, e, Xc in zip(seeds, bc.engines, data):
+        p = CTGANEngine(tr.layout, cfg, DEV, backend="hip", seed=s)
+        p.flat.copy_(e.flat)
+        p.set_training_data(Xc)
+        plain.append(p)
+    for _ in range(2):
+        bc.train_epoch()
+        for p in plain:
+            p.train_epoch()
+    torch.cuda.synchronize()
+    for c, (e, p) in enumerate(zip(bc.engines, plain)):
+        for name in ("flat", "mG", "vG", "mD", "vD", "stepG", "stepD"):
+            assert torch.equal(getattr(e, name), getattr(p, name)), (c, name)
+        assert torch.equal(e.ops.ctr, p.ops.ctr), c
+        assert e.bn_batches == p.bn_batches == 4 * p.steps_per_epoch
+        assert float(e.stepD) == 2 * p.steps_per_epoch
+    assert set(bc.engines[0].graphs) == {(1, 3), (8, 2), 8}

@@ -80,6 +80,17 @@ def test_integer_detection_and_empty():
     assert tp.df["d"].tolist() == ["x", "empty", "y"]
 
 
+def test_mixed_object_column_keeps_printed_categories():
+    """1, 1.0 and True hash equal but print differently: the categories are what astype(str) gives
+    (`Server/dtds/data/utils/file_generator.py:197-205` value_counts of the stringified column)."""
+    df = pd.DataFrame({"m": pd.Series([1, 1.0, True, "1", 1, "x"], dtype=object), "v": [1.0, 2, 3, 4, 5, 6]})
+    tp = TablePreprocessor(df, "t", "", "", ["m"], [])
+    i2s = tp.local_meta()["columns"][0]["i2s"]
+    want = df["m"].astype(str).value_counts()
+    assert i2s == {str(k): int(v) for k, v in want.items()}
+    assert i2s["1"] == 3 and i2s["1.0"] == 1 and i2s["True"] == 1
+
+
 def test_date_split_join_roundtrip():
     df = pd.DataFrame({"when": ["2020-01-31", "2019-02-15", "empty"], "v": [1, 2, 3]})
     out, cats = split_dates(df, {"when": "YYYY-MM-DD"}, ["when"])

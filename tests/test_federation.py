@@ -39,6 +39,23 @@ def test_local_emulation_two_clients(tmp_path):
     assert np.isclose(rt.weights.sum(), 1.0) and len(rt.weights) == 2
 
 
+def test_label_encoders_written_during_init(tmp_path):
+    """The pickle exists once initialisation is over (the reference writes it there,
+    `Server/dtds/distributed.py:679-684`): a run killed mid-training still leaves it."""
+    import pickle
+    from fed_tgan_amd.fed.local import LocalGroup, ThreadComm
+    from fed_tgan_amd.fed.runtime import FedRuntime
+    rt = FedRuntime(_cfg(tmp_path), ThreadComm(LocalGroup(1), 0, torch.device("cpu")), torch.device("cpu"))
+    rt.initialize()
+    rt._le_proc.wait(timeout=120)
+    path = tmp_path / "models" / "label_encoders_Intrusion.pickle"
+    with open(path, "rb") as f:       # our own file
+        les = pickle.load(f)
+    assert [d["column_name"] for d in les] == [v.column_name for v in rt.vocabs]
+    assert all(d["label_encoder"].classes_.tolist() == v.tolist() for d, v in zip(les, rt.vocabs))
+    assert rt.write_label_encoders() == str(path)
+
+
 def test_weighted_aggregation_is_weighted_average(tmp_path):
     """Every client ends the round holding sum_i w_i * theta_i of ALL flat entries (incl. BN stats)."""
     from fed_tgan_amd.fed.local import LocalGroup, ThreadComm

@@ -188,10 +188,76 @@ def test_gpu_emulated_clients_batched(tmp_path):
 
 
 def test_gpu_emulated_clients_batched_off_and_unequal_rows(tmp_path):
-    """batched_clients='off', and clients with different row counts, keep the per-thread engines."""
+    """batched_clients='off' keeps the per-thread engines; clients with different row counts (Dirichlet
+    shards) batch, each training its own steps per epoch (slabs in non-increasing order of steps)."""
     from fed_tgan_amd.ops import native
     native.require()
     rt = run_local_emulation(_cfg(tmp_path, epochs=1, batched_clients="off"), 2, backend="hip", device=DEV)
     assert not rt.batched and rt.engine.batch is None
-    rt = run_local_emulation(_cfg(tmp_path / "u", epochs=1, shard_mode="dirichlet"), 2, backend="hip", device=DEV)
-    assert len(set(rt.rows)) > 1 and not rt.batched
+    rt = run_local_emulation(_cfg(tmp_path / "u", epochs=2, shard_mode="dirichlet"), 3, backend="hip", device=DEV)
+    assert len(set(rt.rows)) > 1 and rt.batched
+    b = rt.batch_clients
+    steps = [n // 500 for n in rt.rows]
+    assert b.steps() == sorted(steps, reverse=True) and [steps[c] for c in b.client_of_slab] == b.steps()
+    torch.cuda.synchronize()
+    for s, e in enumerate(b.engines):
+        assert float(e.stepD) == 2 * b.steps()[s]       # each client trained its own epoch length, twice
+        assert torch.equal(e.flat, b.engines[0].flat)   # and holds the aggregate
+    _check_outputs(tmp_path / "u", 2, 3000)
+
+
+def _final_flats(tmp, n, **kw):
+    rt = run_local_emulation(_cfg(tmp, **kw), n, backend="hip", device=DEV)
+    torch.cuda.synchronize()
+    return rt, rt.engine.flat.detach().clone()
+
+
+def test_gpu_batched_matches_threads_broadcast_init(tmp_path):
+    """The same federation with batched clients and with one engine per client thread (init='broadcast':
+    every client starts from client 0's weights) ends the rounds with the same aggregate, to the
+    reassociation noise of the other split-K plans and epilogue fusions (the clients' streams
+    are ordered before the batched steps)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    kw = dict(epochs=2, synthetic_rows=2000, init="broadcast", shard_mode="dirichlet", seed=3,
+              engine=EngineConfig(batch_size=500, precision="fp32"))
+    rb, fb = _final_flats(tmp_path / "b", 3, batched_clients="on", **kw)
+    rt, ft = _final_flats(tmp_path / "t", 3, batched_clients="off", **kw)
+    assert rb.batched and not rt.batched and rb.rows == rt.rows and len(set(rb.rows)) > 1
+    rel = ((fb - ft).norm() / ft.norm()).item()
+    assert rel < 2e-3, rel
+
+
+def test_hier_one_rank_rccl_four_batched_clients(tmp_path):
+    """-local_clients 4 over a one-rank RCCL process group (HierComm) batch like the in-process emulation:
+    the arena's weighted sum, then the process-level RCCL all-reduce; the aggregate equals ThreadComm's."""
+    from fed_tgan_amd.cli import free_port
+    from fed_tgan_amd.ops import native
+    native.require()
+    kw = dict(epochs=2, shard_mode="dirichlet", batched_clients="on")
+    comm = Comm(0, 1, [0], "nccl", port=free_port(), device=DEV, force_dist=True)
+    try:
+        rh = run_local_emulation(_cfg(tmp_path / "h", **kw), 4, backend="hip", device=DEV, outer=comm)
+        rh.flush_writes()
+        torch.cuda.synchronize()
+        fh = rh.engine.flat.detach().clone()
+        assert rh.batched and type(rh.comm).__name__ == "HierComm" and comm.data_backend == "nccl"
+    finally:
+        comm.destroy()
+    rt, ft = _final_flats(tmp_path / "t", 4, **kw)
+    assert rt.batched and rh.rows == rt.rows
+    assert torch.equal(fh, ft)
+    _check_outputs(tmp_path / "h", 2, 3000)
+
+
+def test_dedicated_federator_rccl_among_clients(tmp_path):
+    """The reference topology (`R/README.md:7-25`): rank 0 a dataless federator, rank 1 the client, on the
+    box's one GPU.  The aggregation is RCCL among the client ranks (the federator sits outside the group)
+    and the federator receives the aggregate over its pair group: both ranks end with the same weights."""
+    r = _run(["tools/topology_probe.py", "--world-size", "2", "--epochs", "2", "--out", str(tmp_path)], timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    import json
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["data_backend"] == ["nccl", "nccl"] and res["data_world_size"][1] == 1
+    assert res["flat_equal"] and res["epochs"] == 2
+    _check_outputs(tmp_path, 2, 3000)

@@ -10,6 +10,7 @@ import sys
 import threading
 
 import pandas as pd
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -90,16 +91,21 @@ def test_hier_rejects_dedicated_federator():
     raise AssertionError("expected a ValueError")
 
 
-def test_cli_two_ranks_two_clients_each(tmp_path):
+@pytest.mark.parametrize("k,extra", [(2, []), (4, ["-shard", "dirichlet", "-alpha", "0.5"])])
+def test_cli_two_ranks_k_clients_each(tmp_path, k, extra):
+    """2 processes x k clients; k = 4 with Dirichlet shards (clients with different row counts)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
-    r = subprocess.run([sys.executable, "-m", "dtds.distributed", "-world_size", "2", "-local_clients", "2", "-epochs",
-                        "2", "-backend", "torch", "-synthetic_rows", "800", "-n_sample", "503", "-batch_size", "100",
-                        "-out_dir", str(tmp_path), "-dump_real", "-quiet"], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=420)
+    r = subprocess.run([sys.executable, "-m", "dtds.distributed", "-world_size", "2", "-local_clients", str(k),
+                        "-epochs", "2", "-backend", "torch", "-synthetic_rows", "800", "-n_sample", "503",
+                        "-batch_size", "100", "-out_dir", str(tmp_path), "-dump_real", "-quiet"] + extra, cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stderr[-3000:]
     raw = tmp_path / "data" / "raw"
     assert sorted(p.name for p in raw.glob("Intrusion_train_client*.csv")) == \
-        [f"Intrusion_train_client{i}.csv" for i in range(4)]
+        [f"Intrusion_train_client{i}.csv" for i in range(2 * k)]
+    if extra:
+        sizes = [len(pd.read_csv(raw / f"Intrusion_train_client{i}.csv")) for i in range(2 * k)]
+        assert len(set(sizes)) > 1
     df = pd.read_csv(tmp_path / "Intrusion_result" / "Intrusion_synthesis_epoch_1.csv")
     assert df.shape == (503, 42)
     assert len(pd.read_csv(tmp_path / "timestamp_experiment.csv", header=None)) == 2
