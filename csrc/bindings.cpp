@@ -117,6 +117,7 @@ int64_t set_client_batch(int64_t k, int64_t stride, int64_t seed_step, int64_t b
   cb.stride = k > 1 ? stride : 0;
   cb.seed_step = k > 1 ? (uint64_t)seed_step : 0;
   cb.base = k > 1 ? reinterpret_cast<const char*>(base) : nullptr;
+  cb.xcd = k > 1 ? fedtgan::g_xcd_clients : 0;
   return prev;
 }
 
@@ -1016,6 +1017,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     TORCH_CHECK(value == 0 || value == 1, "act_row_mode: 0 or 1");
     const int prev = fedtgan::g_act_row_mode;
     fedtgan::g_act_row_mode = (int)value;
+    return prev;
+  }
+  if (key == "xcd_clients") {   // batched launches: each client on its own XCD(s) (1) or round-robin (0)
+    TORCH_CHECK(value == 0 || value == 1, "xcd_clients: 0 or 1");
+    const int64_t prev = fedtgan::g_xcd_clients;
+    fedtgan::g_xcd_clients = (int)value;
     return prev;
   }
   if (key == "adam_store") {

@@ -53,7 +53,12 @@ __device__ __forceinline__ void adam_store4(float4* base, __amdgpu_buffer_rsrc_t
 // skips the float4 groups the jobs own (and [skip_lo, skip_hi), a fused GEMM's): job outputs start
 // 16-B aligned and own ceil4(cols) elements (the flat layout stores every tensor that way), so no
 // float4 is shared.  bid / nblk: this workgroup's index and the count among the launch's Adam ones.
-template <int AUX>
+// U: float4 per thread and operand per pass of the Adam loop (1, or ADAM_U for large optimizers: adam_unroll)
+constexpr int ADAM_U = 4;
+// the launchers' choice of U: the unrolled loop for optimizers of >= 4 M elements over the launch's clients
+inline int adam_unroll(int64_t n4, int clients) { return n4 * (clients > 1 ? clients : 1) >= (int64_t)(1 << 20) ? ADAM_U : 1; }
+
+template <int AUX, int U = 1>
 __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restrict__ p, const float* __restrict__ g,
                                              float* __restrict__ m, float* __restrict__ v,
                                              const float* __restrict__ step, int64_t n4, float lr, float b1, float b2,
@@ -177,6 +182,49 @@ __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restric
   const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(m4, 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(v4, 0, bytes, 0x00020000);
   const int64_t stride = (int64_t)(nblk - nb) * blockDim.x;
+  if constexpr (U > 1) {
+    // U float4 of each operand per thread, all 4U loads issued before the first update: the bytes in flight
+    // per wave no longer depend on how many workgroups share a CU (a fused GEMM launch keeps the tile's LDS
+    // for every workgroup -- 2 per CU -- which left the one-float4-per-thread loop HBM-starved on the wide
+    // table's 35 M-parameter D).  The fused GEMM's range [skip_lo, skip_hi) is cut out of the index space
+    // (no wasted loads); the column-sum jobs' few elements are loaded and left to the jobs.
+    const int64_t lo4 = cs.skip_lo >> 2, hi4 = max(cs.skip_hi >> 2, lo4);
+    const int64_t nn = n4 - (hi4 - lo4);
+    for (int64_t i0 = (int64_t)(bid - nb) * blockDim.x + threadIdx.x; i0 < nn; i0 += U * stride) {
+      float4 pp[U], gg[U], mm[U], vv[U];
+      int64_t ix[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t j = min(i0 + u * stride, nn - 1);
+        ix[u] = j < lo4 ? j : j + (hi4 - lo4);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        pp[u] = p4[ix[u]];
+        gg[u] = g4[ix[u]];
+        mm[u] = m4[ix[u]];
+        vv[u] = v4[ix[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t e = ix[u] * 4;
+        bool skip = i0 + u * stride >= nn;
+        for (int k = 0; k < cs.n_jobs; ++k) skip |= e >= cs.own_lo[k] && e < cs.own_hi[k];
+        if (skip) continue;
+        float* pf = reinterpret_cast<float*>(&pp[u]);
+        float* gf = reinterpret_cast<float*>(&gg[u]);
+        float* mf = reinterpret_cast<float*>(&mm[u]);
+        float* vf = reinterpret_cast<float*>(&vv[u]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) adam_elem(gf[q], pf[q], mf[q], vf[q], b1, b2, eps, wd, sz, bc2s);
+        adam_store4<AUX>(p4, rp, ix[u], pp[u]);
+        adam_store4<AUX>(m4, rm, ix[u], mm[u]);
+        adam_store4<AUX>(v4, rv, ix[u], vv[u]);
+      }
+    }
+    if (rng_bump && bid == nb && threadIdx.x == 0) rng_bump[0] += 1ull;
+    return;
+  }
   for (int64_t i = (int64_t)(bid - nb) * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const int64_t e = i * 4;
     bool owned = false;

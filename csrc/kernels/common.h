@@ -46,6 +46,57 @@ __device__ __forceinline__ T* cptr(T* p, int64_t off) {
   return p ? (T*)((const char*)p + off) : p;
 }
 
+// Batched clients, XCD-aware: the dispatcher deals a grid's workgroups round-robin over the 8 XCDs by linear id
+// (MI355X_MICROARCH.md "Workgroup dispatch"), so in a client-major grid every client's tiles land on all 8 XCDs
+// and each XCD's 4 MB L2 holds pieces of all K clients' operands -- the tiles' re-reads of a client's
+// activations and weights (a few MB per client) then miss L2.  Remapped, the workgroups of XCD x (linear id
+// % 8 == x) serve clients {x / (8 / K)} (K <= 8) or {x * (K / 8) + ...} (K >= 8): a client's whole launch
+// runs on its own XCD(s), and every kernel of a step places the client there, so its data stays in that L2
+// from kernel to kernel.  lin = the workgroup's linear id in a grid of K * T workgroups, T per client
+// (client-major); valid when K divides 8 or 8 divides K, and 8 divides K * T.  Returns false otherwise
+// (then client = lin / T).
+__device__ __forceinline__ bool xcd_client_map(int lin, int T, int K, int& client, int& local) {
+  if (K > 1 && ((K * T) & 7) == 0 && ((8 % K) == 0 || (K & 7) == 0)) {
+    const int x = lin & 7, slot = lin >> 3;
+    if (K <= 8) {
+      const int xpc = 8 / K;                  // XCDs per client
+      client = x / xpc;
+      local = slot * xpc + x % xpc;
+    } else {
+      const int cpx = K >> 3;                 // clients per XCD
+      client = x * cpx + slot / T;
+      local = slot % T;
+    }
+    return true;
+  }
+  client = lin / T;
+  local = lin - client * T;
+  return false;
+}
+
+// the block coordinates a workgroup serves in a batched grid (gridDim.x, gridDim.y, K clients = gridDim.z):
+// blockIdx itself, or with `xcd` (ClientBatch::xcd) the XCD-aware client placement above.  Every batched kernel
+// reads its (x, y, client) from here, so a client's producer and consumer kernels run on the same XCD(s).
+struct BIdx {
+  int x, y, z;
+};
+// (xcd is nonzero only in batched launches -- the host sets it from ClientBatch::k -- and nothing else is read on
+// the one-client path: a grid-size read there would put a dispatch-packet load in front of every kernel's first
+// loads, ~5 us over a latency-bound one-client step's 25 launches)
+__device__ __forceinline__ BIdx batch_bidx(int xcd) {
+  BIdx b{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  if (__builtin_expect(xcd != 0, 0)) {
+    const int gx = (int)gridDim.x, T = gx * (int)gridDim.y;
+    int cl, loc;
+    if (xcd_client_map(b.x + T * b.z + gx * b.y, T, (int)gridDim.z, cl, loc)) {
+      b.x = loc % gx;
+      b.y = loc / gx;
+      b.z = cl;
+    }
+  }
+  return b;
+}
+
 struct RngArgs {
   uint64_t seed;
   const uint64_t* ctr;  // device-resident step counter

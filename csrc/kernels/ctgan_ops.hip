@@ -26,8 +26,9 @@
 namespace fedtgan {
 
 // ---------------------------------------------------------------------------- batched clients (launch.h)
+int g_xcd_clients = 1;
 ClientBatch& client_batch() {
-  static thread_local ClientBatch cb{1, 0, 0, nullptr};
+  static thread_local ClientBatch cb{1, 0, 0, nullptr, 0};
   return cb;
 }
 
@@ -123,8 +124,9 @@ __device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint4 k
 }
 
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
-  if (blockIdx.z) {   // batched clients: this client's buffers and seed
-    const int64_t o = (int64_t)blockIdx.z * a.cb.stride;
+  const BIdx bi_ = batch_bidx(a.cb.xcd);
+  if (bi_.z) {   // batched clients: this client's buffers and seed
+    const int64_t o = (int64_t)bi_.z * a.cb.stride;
     a.h = cptr(a.h, o);
     a.h16 = cptr(a.h16, o);
     a.xf = cptr(a.xf, o);
@@ -142,18 +144,18 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     a.step_bump2 = cptr(a.step_bump2, o);
     a.metrics = cptr(a.metrics, o);
     a.rng_ctr = cptr(a.rng_ctr, o);
-    a.seed += (uint64_t)blockIdx.z * a.cb.seed_step;
+    a.seed += (uint64_t)bi_.z * a.cb.seed_step;
   }
   const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (blockIdx.x == 0 && tid == 0) {
+  if (bi_.x == 0 && tid == 0) {
     if (a.step_bump) a.step_bump[0] += 1.0f;
     if (a.step_bump2) a.step_bump2[0] += 1.0f;
     if (a.zero_metrics && a.metrics) {
       a.metrics[0] = 0.f; a.metrics[1] = 0.f; a.metrics[2] = 0.f; a.metrics[3] = 0.f;
     }
   }
-  const int b = blockIdx.x * SAMPLE_ROWS + wv;
+  const int b = bi_.x * SAMPLE_ROWS + wv;
   if (b >= a.B) return;
   // rows [0, n_real) get a real row (the D phase); the rest only noise + condition (the G phase
   // of the same step when both batches are drawn by one launch)
@@ -364,18 +366,19 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
                                                                   const uint64_t* ctr, uint32_t stream_id,
                                                                   SlerpFuse sl, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx(cb.xcd);
   extern __shared__ float act_smem[];
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     logits = cptr(logits, co);
     out = cptr(out, co);
     ctr = cptr(ctr, co);
     client_off(sp, co);
     client_off(sl, co);
-    seed += (uint64_t)blockIdx.z * cb.seed_step;
+    seed += (uint64_t)bi_.z * cb.seed_step;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
+  const int r = bi_.x * (int)(blockDim.x >> 6) + wv;
   const int rc = min(r, rows - 1);
   const int D = sp.dim, S = sp.n_span;
   const float* x = logits + (size_t)rc * ldl;
@@ -533,20 +536,21 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
                                                                       SpanTables sp, float inv_tau, uint64_t seed,
                                                                       const uint64_t* ctr, uint32_t stream_id,
                                                                       SlerpFuse sl, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx(cb.xcd);
   // LDS holds only the row image and the span statistics; the element -> span map (the first D
   // words of the packed table, shared by every row and L2-resident) is read next to the logits
   extern __shared__ float act_smem[];
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     logits = cptr(logits, co);
     out = cptr(out, co);
     ctr = cptr(ctr, co);
     client_off(sp, co);
     client_off(sl, co);
-    seed += (uint64_t)blockIdx.z * cb.seed_step;
+    seed += (uint64_t)bi_.z * cb.seed_step;
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int r = blockIdx.x;
+  const int r = bi_.x;
   const int D = sp.dim, S = sp.n_span;
   const float* x = logits + (size_t)r * ldl;
   const int* einfo = sp.packed;
@@ -636,9 +640,10 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
                                                                         float* __restrict__ dl, int ldg, int rows,
                                                                         float inv_tau, float* loss, int loss_per_row,
                                                                         ClientBatch cb) {
+  const BIdx bi_ = batch_bidx(cb.xcd);
   extern __shared__ float act_smem[];
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     dact = cptr(dact, co);
     act = cptr(act, co);
     logits = cptr(logits, co);
@@ -649,7 +654,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
     client_off(sp, co);
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int r = blockIdx.x;
+  const int r = bi_.x;
   const int D = sp.dim, S = sp.n_span;
   const float* g = dact + (size_t)r * ldd;
   const float* y = act + (size_t)r * lda;
@@ -804,9 +809,10 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
                                                                     int ldg, int rows, float inv_tau, float* loss,
                                                                     int loss_per_row, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx(cb.xcd);
   extern __shared__ float act_smem[];
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     dact = cptr(dact, co);
     act = cptr(act, co);
     logits = cptr(logits, co);
@@ -817,7 +823,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
     client_off(sp, co);
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int r = blockIdx.x * (int)(blockDim.x >> 6) + wv;
+  const int r = bi_.x * (int)(blockDim.x >> 6) + wv;
   const int rc = min(r, rows - 1);
   const int D = sp.dim, S = sp.n_span;
   const float* g = dact + (size_t)rc * ldd;
@@ -966,16 +972,17 @@ size_t activation_smem_bytes(const SpanTables& sp) {
 __global__ __launch_bounds__(256) void slerp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
                                                     float* __restrict__ out, int rows, int cols, int ld, uint64_t seed,
                                                     const uint64_t* ctr, uint32_t stream_id, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     real = cptr(real, co);
     fake = cptr(fake, co);
     out = cptr(out, co);
     ctr = cptr(ctr, co);
-    seed += (uint64_t)blockIdx.z * cb.seed_step;
+    seed += (uint64_t)bi_.z * cb.seed_step;
   }
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int r = bi_.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r >= rows) return;
   const float* a = real + (size_t)r * ld;
   const float* b = fake + (size_t)r * ld;
@@ -1022,14 +1029,15 @@ __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, f
 __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                           int ldo, int rows, int cols, float lam, float* loss,
                                                           int loss_per_row, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
     out = cptr(out, co);
     loss = cptr(loss, co);
   }
   __shared__ float sh[8];
-  const int r = blockIdx.x;
+  const int r = bi_.x;
   const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
   const int n4 = cols / 4;
   f32x4 v[GP_V4];
@@ -1050,14 +1058,15 @@ __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restric
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                        int ldo, int rows, int cols, float lam, float* loss,
                                                        int loss_per_row, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
     out = cptr(out, co);
     loss = cptr(loss, co);
   }
   __shared__ float sh[8];
-  const int r = blockIdx.x;
+  const int r = bi_.x;
   const float* x = g + (size_t)r * ldg;
   float s0 = 0.f, s1 = 0.f;
   int i = threadIdx.x;
@@ -1078,14 +1087,15 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __restrict__ g, int ldg,
                                                                float* __restrict__ out, int ldo, int rows, int cols,
                                                                float lam, float* loss, int loss_per_row, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
     out = cptr(out, co);
     loss = cptr(loss, co);
   }
   __shared__ float sh[8];
-  const int r = blockIdx.x;
+  const int r = bi_.x;
   const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
   const int n4 = cols / 4;
   float s = 0.f;
@@ -1176,11 +1186,12 @@ struct ColsumBatch {
 };
 
 __global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch bt, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx(cb.xcd);
   __shared__ float part[2][CS_GROUPS][CS_COLS + 1];
-  const ColsumJob jb = client_job(bt.jobs[blockIdx.y], (int64_t)blockIdx.z * cb.stride);
-  const int c = blockIdx.x * CS_COLS + (threadIdx.x % CS_COLS);
+  const ColsumJob jb = client_job(bt.jobs[bi_.y], (int64_t)bi_.z * cb.stride);
+  const int c = bi_.x * CS_COLS + (threadIdx.x % CS_COLS);
   const int grp = threadIdx.x / CS_COLS;
-  if ((int)(blockIdx.x * CS_COLS) >= jb.cols) return;
+  if ((int)(bi_.x * CS_COLS) >= jb.cols) return;
   const int cc = min(c, jb.cols - 1);
   const float* uw = jb.dot_w ? jb.dot_w : jb.w;   // the dot's row weights
   float s = 0.f, s2 = 0.f;
@@ -1202,7 +1213,7 @@ __global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch 
     if (c < jb.cols && jb.out) jb.out[c] = t;
     if (jb.dot_v) {
       float d = c < jb.cols ? (jb.dot_w ? t2 : t) * jb.dot_v[c] : 0.f;
-      if (blockIdx.x == 0 && jb.dot_e) {   // + e * sum_r u[r], once per job
+      if (bi_.x == 0 && jb.dot_e) {   // + e * sum_r u[r], once per job
         float ws = 0.f;
         for (int r = threadIdx.x; r < jb.rows; r += 64) ws += uw ? uw[r] : 1.f;
         d += wave_sum(ws) * (threadIdx.x == 0 ? jb.dot_e[0] : 0.f);
@@ -1275,8 +1286,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
     gamma = cptr(gamma, co);
     beta = cptr(beta, co);
@@ -1291,7 +1303,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
-  const int c = blockIdx.x * COLS + lc;
+  const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   const int rpg = rows / groups;
@@ -1358,8 +1370,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
     gamma = cptr(gamma, co);
     beta = cptr(beta, co);
@@ -1374,7 +1387,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
-  const int c = blockIdx.x * COLS + lc;
+  const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   const int rpg = rows / groups;
@@ -1444,8 +1457,9 @@ __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
     const float* __restrict__ beta, float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn,
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows,
     int cols, int groups, float momentum, float eps, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
     part = cptr(part, co);
     gamma = cptr(gamma, co);
@@ -1460,10 +1474,10 @@ __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
 
   __shared__ float st[BNA_COLS][2][3];   // [col][batch] = (mean, invstd, biased var)
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int c0 = blockIdx.x * BNA_COLS;
+  const int c0 = bi_.x * BNA_COLS;
   const int rpg = rows / groups;
   // this thread's float4 of the GEMM output: requested first, in flight during the merge
-  const int r = blockIdx.y * BNA_ROWS + (t >> 2);
+  const int r = bi_.y * BNA_ROWS + (t >> 2);
   const int cq = (t & 3) * 4;
   float x[4];
 #pragma unroll
@@ -1500,7 +1514,7 @@ __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
       }
     }
   __syncthreads();
-  if (blockIdx.y == 0 && t < BNA_COLS && c0 + t < cols) {
+  if (bi_.y == 0 && t < BNA_COLS && c0 + t < cols) {
     const int c = c0 + t;
     const float unb = (float)rpg / (float)max(rpg - 1, 1);
     float m = rm[c], v = rv[c];
@@ -1578,8 +1592,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     dr = cptr(dr, co);
     r_ = cptr(r_, co);
     nhat = cptr(nhat, co);
@@ -1594,7 +1609,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[3 * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
-  const int c = blockIdx.x * COLS + lc;
+  const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   // gamma * invstd is requested with the rows (consumed after the reduction's barriers)
@@ -1640,8 +1655,9 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_stream_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     dr = cptr(dr, co);
     r_ = cptr(r_, co);
     nhat = cptr(nhat, co);
@@ -1656,7 +1672,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_stream_kernel(
   constexpr int GROUPS = BN_THREADS / COLS;
   __shared__ float sh[3 * BN_WAVES * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
-  const int c = blockIdx.x * COLS + lc;
+  const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
   const int cc = min(c, cols - 1);
   float st[3] = {0.f, 0.f, 0.f};
@@ -1730,8 +1746,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
                                                    float4* __restrict__ m, float4* __restrict__ v,
                                                    const float* __restrict__ step, int64_t n4, float lr, float b1,
                                                    float b2, float eps, float wd, uint64_t* rng_bump, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     p = cptr(p, co);
     g = cptr(g, co);
     m = cptr(m, co);
@@ -1747,7 +1764,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(p, 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(m, 0, bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(v, 0, bytes, 0x00020000);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t i = (int64_t)bi_.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
     float* pf = reinterpret_cast<float*>(&pp);
     float* gf = reinterpret_cast<float*>(&gg);
@@ -1759,13 +1776,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
     adam_store4<AUX>(m, rm, i, mm);
     adam_store4<AUX>(v, rv, i, vv);
   }
-  if (rng_bump && blockIdx.x == 0 && threadIdx.x == 0) rng_bump[0] += 1ull;
+  if (rng_bump && bi_.x == 0 && threadIdx.x == 0) rng_bump[0] += 1ull;
 }
 
 __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, const float* step, int64_t start,
                                  int64_t n, float lr, float b1, float b2, float eps, float wd, ClientBatch cb) {
-  if (blockIdx.z) {
-    const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
     p = cptr(p, co);
     g = cptr(g, co);
     m = cptr(m, co);
@@ -1791,13 +1809,14 @@ __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, c
 // exactly those elements straight from registers.  Every other workgroup runs the float4 Adam and
 // skips the float4 groups the jobs own: job outputs start 16-B aligned and own ceil4(cols)
 // elements (the flat layout stores every tensor that way), so no float4 is shared.
-template <int AUX>
+template <int AUX, int U>
 __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       const float* __restrict__ step, int64_t n4, float lr, float b1,
                                                       float b2, float eps, float wd, uint64_t* rng_bump, AdamColsum cs,
                                                       ClientBatch cb) {
-  const int64_t co = (int64_t)blockIdx.z * cb.stride;
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  const int64_t co = (int64_t)bi_.z * cb.stride;
   if (co) {
     p = cptr(p, co);
     g = cptr(g, co);
@@ -1806,7 +1825,7 @@ __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, con
     step = cptr(step, co);
     rng_bump = cptr(rng_bump, co);
   }
-  adam_cs_body<AUX>((int)blockIdx.x, (int)gridDim.x, p, g, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
+  adam_cs_body<AUX, U>((int)bi_.x, (int)gridDim.x, p, g, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
 }
 
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
@@ -1817,19 +1836,24 @@ void launch_adam_colsum(float* p, const float* g, float* m, float* v, const floa
   cs.blk_start[0] = 0;
   for (int k = 0; k < cs.n_jobs; ++k) cs.blk_start[k + 1] = cs.blk_start[k] + (cs.jobs[k].cols + ACS_COLS - 1) / ACS_COLS;
   const int64_t n4 = n / 4;
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
-  const int grid = std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
   const ClientBatch cb = client_batch();
+  const int U = adam_unroll(n4, cb.k);
+  const int blocks = (int)std::min<int64_t>((n4 + 256 * U - 1) / (256 * U), g_adam_max_blocks);
+  const int grid = std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
   if (cb.k > 1) {
     check_slabs("adam operand", p, g, m, v, step, rng_ctr_bump);
     check_slab(cs);
   }
-#define FEDTGAN_ADAM_CS(AUX)                                                                                       \
-  hipLaunchKernelGGL(adam_cs_kernel<AUX>, dim3(grid, 1, cb.k), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, b2, \
-                     eps, wd, rng_ctr_bump, cs, cb)
-  if (g_adam_store == 2) FEDTGAN_ADAM_CS(2);
-  else if (g_adam_store == 16) FEDTGAN_ADAM_CS(16);
-  else FEDTGAN_ADAM_CS(0);
+#define FEDTGAN_ADAM_CS(AUX, UU)                                                                                       \
+  hipLaunchKernelGGL((adam_cs_kernel<AUX, UU>), dim3(grid, 1, cb.k), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, \
+                     b2, eps, wd, rng_ctr_bump, cs, cb)
+#define FEDTGAN_ADAM_CS_U(AUX)                  \
+  if (U == ADAM_U) FEDTGAN_ADAM_CS(AUX, ADAM_U); \
+  else FEDTGAN_ADAM_CS(AUX, 1);
+  if (g_adam_store == 2) { FEDTGAN_ADAM_CS_U(2) }
+  else if (g_adam_store == 16) { FEDTGAN_ADAM_CS_U(16) }
+  else { FEDTGAN_ADAM_CS_U(0) }
+#undef FEDTGAN_ADAM_CS_U
 #undef FEDTGAN_ADAM_CS
   if (n4 * 4 < n)
     hipLaunchKernelGGL(adam_tail_kernel, dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
@@ -2081,7 +2105,8 @@ void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream) {
 }
 
 __global__ void rng_bump_kernel(uint64_t* ctr, ClientBatch cb) {
-  ctr = cptr(ctr, (int64_t)blockIdx.z * cb.stride);
+  const BIdx bi_ = batch_bidx(cb.xcd);
+  ctr = cptr(ctr, (int64_t)bi_.z * cb.stride);
   ctr[0] += 1ull;
 }
 

@@ -956,10 +956,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if constexpr (BATCH) {
     const int sk = (int)gridDim.z / g.nclient;
-    const int cl = (int)blockIdx.z / sk;
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+    int cl, loc;
+    if (g.xcd_cl && xcd_client_map((int)(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z)), gx * gy * sk, g.nclient,
+                                   cl, loc)) {
+      g.xcd_remap = 0;    // the client's tiles already share one XCD's L2
+    } else {
+      cl = (int)blockIdx.z / sk;
+      loc = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * ((int)blockIdx.z - cl * sk));
+    }
     if (cl) client_view(g, cl);
-    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, blockIdx.x, blockIdx.y, (int)blockIdx.z - cl * sk,
-                                                        gridDim.x, gridDim.y, sk, smem);
+    gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, loc % gx, (loc / gx) % gy, loc / (gx * gy), gx, gy, sk, smem);
   } else {
     gemm_tile<TA, TB, F32, VEC, TM, TN, BIN, false, EK>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.x, gridDim.y,
                                                         gridDim.z, smem);
@@ -988,16 +995,17 @@ struct Grid3 {
 
 template <class P1, class P2, bool BATCH = false>
 __global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2, Grid3 grid1, Grid3 grid2) {
+  const BIdx bi_ = batch_bidx(g1.xcd_cl);
   constexpr int S1 = 2 * Cfg<false, P1::TM, P1::TM>::STAGE, S2 = 2 * Cfg<false, P2::TM, P2::TM>::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[S1 > S2 ? S1 : S2];
   if constexpr (BATCH) {
-    if (blockIdx.z) {
-      client_view(g1, blockIdx.z);
-      client_view(g2, blockIdx.z);
+    if (bi_.z) {
+      client_view(g1, bi_.z);
+      client_view(g2, bi_.z);
     }
   }
   const int n1 = grid1.x * grid1.y * grid1.z;
-  int b = blockIdx.x;
+  int b = bi_.x;
   if (b < n1) {
     gemm_tile<P1::TA, P1::TB, false, P1::VEC, P1::TM, P1::TM>(g1, b % grid1.x, (b / grid1.x) % grid1.y,
                                                                b / (grid1.x * grid1.y), grid1.x, grid1.y, grid1.z, smem);
@@ -1044,10 +1052,11 @@ __device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int
 
 template <int SMAX>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
-  if (blockIdx.z) client_view(g, blockIdx.z);
+  const BIdx bi_ = batch_bidx(g.xcd_cl);
+  if (bi_.z) client_view(g, bi_.z);
   const size_t total = (size_t)g.M * g.N;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
-  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+  for (size_t idx = (size_t)bi_.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(idx / g.N), n = (int)(idx % g.N);
     st_out(g.c, (size_t)m * g.ldc + n, splitk_value<SMAX>(g, idx, m, n, step), g.wt);
   }
@@ -1065,13 +1074,14 @@ constexpr int CH_MAXK = 1024, CH_COLS = 64;
 // MASK: head and tail both EPI_MASK (the R chain) -- the launch carries no Philox / BN epilogue code
 template <int SMAX, bool MASK = false>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
+  const BIdx bi_ = batch_bidx(g.xcd_cl);
   __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
   __shared__ float part[4][CH_COLS];
-  if (blockIdx.z) {
-    client_view(g, blockIdx.z);
-    client_view(t, blockIdx.z);
+  if (bi_.z) {
+    client_view(g, bi_.z);
+    client_view(t, bi_.z);
   }
-  const int m = blockIdx.x, s = blockIdx.y;
+  const int m = bi_.x, s = bi_.y;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
     float v;
@@ -1116,17 +1126,18 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
 // flat-buffer Adam with its folded column sums (adam_cs_body), skipping the GEMM's range.  The step's
 // last two launches (the generator's first-layer weight gradient, then the generator's Adam) become
 // one: none of the other Adam work waits for that gradient.
-template <bool VEC, int TM, int AUX, bool BATCH = false>
+template <bool VEC, int TM, int AUX, bool BATCH = false, int U = 1>
 __global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, float* p, const float* gr, float* m,
                                                        float* v, const float* step, int64_t n4, float lr, float b1,
                                                        float b2, float eps, float wd, uint64_t* rng_bump,
                                                        AdamColsum cs) {
+  const BIdx bi_ = batch_bidx(g.xcd_cl);
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, TM, TM>::STAGE];
   int64_t co = 0;
   if constexpr (BATCH) {
-    co = (int64_t)blockIdx.z * g.cstride;
+    co = (int64_t)bi_.z * g.cstride;
     if (co) {   // batched clients: the GEMM's buffers (its Adam pointers included) and the Adam operands
-      client_view(g, blockIdx.z);
+      client_view(g, bi_.z);
       p = cptr(p, co);
       gr = cptr(gr, co);
       m = cptr(m, co);
@@ -1136,12 +1147,12 @@ __global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, flo
     }
   }
   const int nt = gd.x * gd.y * gd.z;
-  const int b = blockIdx.x;
+  const int b = bi_.x;
   if (b < nt) {
     gemm_tile<true, false, false, VEC, TM, TM, false, true>(g, b % gd.x, (b / gd.x) % gd.y, b / (gd.x * gd.y), gd.x,
                                                              gd.y, gd.z, smem);
   } else {
-    adam_cs_body<AUX>(b - nt, (int)gridDim.x - nt, p, gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
+    adam_cs_body<AUX, U>(b - nt, (int)gridDim.x - nt, p, gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_bump, cs, co);
   }
 }
 
@@ -1152,6 +1163,7 @@ static dim3 gemm_prepare(GemmArgs& g) {
   const ClientBatch& cb = client_batch();
   g.nclient = cb.k > 1 ? cb.k : 1;
   g.cstride = cb.k > 1 ? cb.stride : 0;
+  g.xcd_cl = cb.k > 1 ? cb.xcd : 0;
   g.seed_step = cb.k > 1 ? cb.seed_step : 0;
   const int KC = gemm_kc(g.f32);
   const int T = g.tile == 32 ? 32 : (g.tile == 128 ? 128 : 64);   // square output tile
@@ -1377,17 +1389,22 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
   cs.blk_start[0] = 0;
   for (int k = 0; k < cs.n_jobs; ++k) cs.blk_start[k + 1] = cs.blk_start[k] + (cs.jobs[k].cols + ACS_COLS - 1) / ACS_COLS;
   const int64_t n4 = n / 4;
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, g_adam_max_blocks);
+  const int U = adam_unroll(n4, g.nclient);
+  const int blocks = (int)std::min<int64_t>((n4 + 256 * U - 1) / (256 * U), g_adam_max_blocks);
   const Grid3 gd{(int)d.x, (int)d.y, (int)d.z};
   const int grid = gd.x * gd.y * gd.z + std::max(blocks, 1) + cs.blk_start[cs.n_jobs];
-#define FEDTGAN_GEMM_ADAM(V, T, AUX)                                                                                  \
-  do {                                                                                                                   \
-    if (g.nclient > 1)                                                                                                   \
-      hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX, true>), dim3(grid, 1, g.nclient), dim3(NT), 0, stream, g, gd, p,   \
-                         gr, m, v, step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs);                                     \
-    else                                                                                                                 \
-      hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX, false>), dim3(grid, 1, 1), dim3(NT), 0, stream, g, gd, p, gr, m,   \
-                         v, step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs);                                            \
+#define FEDTGAN_GEMM_ADAM_K(V, T, AUX, B, UU)                                                                       \
+  hipLaunchKernelGGL((gemm_adam_kernel<V, T, AUX, B, UU>), dim3(grid, 1, g.nclient), dim3(NT), 0, stream, g, gd, p, gr, \
+                     m, v, step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cs)
+#define FEDTGAN_GEMM_ADAM(V, T, AUX)                                      \
+  do {                                                                   \
+    if (g.nclient > 1) {                                                 \
+      if (U == ADAM_U) FEDTGAN_GEMM_ADAM_K(V, T, AUX, true, ADAM_U);     \
+      else FEDTGAN_GEMM_ADAM_K(V, T, AUX, true, 1);                      \
+    } else {                                                             \
+      if (U == ADAM_U) FEDTGAN_GEMM_ADAM_K(V, T, AUX, false, ADAM_U);    \
+      else FEDTGAN_GEMM_ADAM_K(V, T, AUX, false, 1);                     \
+    }                                                                    \
   } while (0)
 #define FEDTGAN_GEMM_ADAM_T(V, T)                                 \
   if (g_adam_store == 2) FEDTGAN_GEMM_ADAM(V, T, 2);              \
@@ -1400,6 +1417,7 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
   }
 #undef FEDTGAN_GEMM_ADAM_T
 #undef FEDTGAN_GEMM_ADAM
+#undef FEDTGAN_GEMM_ADAM_K
   return true;
 }
 

@@ -21,7 +21,9 @@ struct ClientBatch {
   int64_t stride;
   uint64_t seed_step;
   const char* base;
+  int xcd;     // 1: place each client's workgroups on its own XCD(s) (common.h xcd_client_map)
 };
+extern int g_xcd_clients;   // set_tuning("xcd_clients"): the ClientBatch::xcd of new batched contexts
 ClientBatch& client_batch();
 // host: throws std::runtime_error when a batched launch is handed a pointer outside client 0's slab
 void check_slab(const void* p, const char* what);
@@ -115,6 +117,7 @@ struct GemmArgs {
   int64_t cstride;
   uint64_t seed_step;
   int nclient;
+  int xcd_cl;   // ClientBatch::xcd
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);

@@ -132,11 +132,26 @@ class ThreadComm(Comm):
         self.g.wait()
 
     def broadcast_tensor(self, t, src: int = 0):
+        # the source's copy is made on its stream: the readers' streams wait for it (event), not the host
         if self.rank == src:
-            self.g.result = t.detach().clone()
+            c = t.detach().clone()
+            self.g.result = (c, _stream_event(c))
         self.g.wait()
         if self.rank != src:
-            t.copy_(self.g.result)
+            c, ev = self.g.result
+            if ev is not None:
+                torch.cuda.current_stream(t.device).wait_event(ev)
+            t.copy_(c)
+            done = _stream_event(t)
+        else:
+            done = None
+        self.g.slots[self.rank] = done
+        self.g.wait()
+        if self.rank == src and t.is_cuda:   # the copy stays alive until every reader's stream has read it
+            cur = torch.cuda.current_stream(t.device)
+            for ev in self.g.slots:
+                if ev is not None:
+                    cur.wait_event(ev)
         self.g.wait()
         return t
 

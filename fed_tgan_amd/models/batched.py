@@ -126,7 +126,7 @@ class BatchedClients:
         """Every client's persistent training state (the capture warm-up snapshot)."""
         out = []
         for e in self.engines:
-            out += [e.flat, e.mG, e.vG, e.mD, e.vD, e.stepG, e.stepD]
+            out += [e.flat, e.mG, e.vG, e.mD, e.vD, e.stepG, e.stepD, e.ops.ctr]
         return out
 
     # ------------------------------------------------------------------ training

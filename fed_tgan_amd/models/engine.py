@@ -113,6 +113,10 @@ class EngineConfig:
     # HIP, two hidden D layers: R1 = (R0 W1^T) * MS1 is computed in R0's split-K reduction launch, so
     # D1's weight gradient is the last D GEMM and shares its launch with the D Adam (as fuse_g_adam)
     fuse_d_adam: bool = True
+    # the two fusions above only up to this many optimizer elements per launch (parameters x batched clients;
+    # 0 = no limit): a fused launch gets the GEMM tile's LDS for every workgroup, so its Adam workgroups run at
+    # 2 per CU -- fine for a few M parameters, HBM-starved for the wide table's 35-55 M (A/B knob)
+    fuse_adam_max: int = 0
     # HIP, two hidden D layers: the second layer's forward is computed row by row in the first layer's
     # split-K reduction launch (chain_epilogue_kernel)
     chain_d1: bool = True
@@ -318,9 +322,27 @@ class CTGANEngine:
         return buf.as_strided(g.shape, g.stride(), g.storage_offset())
 
     def reset_parameters(self):
-        """PyTorch default init of the reference modules (Linear kaiming-uniform, BN 1/0)."""
-        G = Generator(self.E + self.C, self.gdims, self.Dd)
-        D = Discriminator(self.Din, self.ddims, self.P)
+        """PyTorch's default init of the reference modules (`Server/dtds/synthesizers/ctgan.py:15-64`:
+        nn.Linear's kaiming-uniform weights and U(+-1/sqrt(fan_in)) biases, BN 1/0), drawn from a generator
+        of this engine's own (seeded by the engine seed) instead of torch's process-wide one: client threads
+        that build their engines concurrently (fed/local.py) would otherwise race on the global generator and
+        an emulated federation would not reproduce run to run.  The modules are built on the meta device,
+        so each weight is drawn once."""
+        import math
+        from torch import nn
+        gen = torch.Generator().manual_seed(self.seed)
+        with torch.device("meta"):
+            G = Generator(self.E + self.C, self.gdims, self.Dd)
+            D = Discriminator(self.Din, self.ddims, self.P)
+        G, D = G.to_empty(device="cpu"), D.to_empty(device="cpu")
+        with torch.no_grad():
+            for m in list(G.modules()) + list(D.modules()):
+                if isinstance(m, nn.Linear):
+                    nn.init.kaiming_uniform_(m.weight, a=math.sqrt(5), generator=gen)
+                    bound = 1.0 / math.sqrt(m.weight.shape[1]) if m.weight.shape[1] > 0 else 0.0
+                    nn.init.uniform_(m.bias, -bound, bound, generator=gen)
+                elif isinstance(m, nn.BatchNorm1d):
+                    m.reset_parameters()
         self.load_modules(G, D)
         self.mG.zero_(); self.vG.zero_(); self.mD.zero_(); self.vD.zero_()
         self.stepG.zero_(); self.stepD.zero_()
@@ -682,6 +704,7 @@ class CTGANEngine:
         # two hidden layers: R1 rides on R0's split-K reduction launch, and dW1 (then the last D GEMM)
         # is held for the D Adam launch (gemm_adam_kernel)
         fuse_d = pair and L == 2 and self.cfg.fuse_d_adam and getattr(o, "gemm_adam", False) and \
+            self._adam_fusable(self.nD) and \
             self.ddims[0] % 16 == 0 and self.ddims[0] <= 1024 and o.gemm_is_split(self.nP, self.ddims[0], self.K1) and \
             getattr(o, "batch_k", 1) == 1
         # otherwise D0's weight gradient may be the GEMM held for the Adam launch (its operands, A0 and X, are
@@ -797,11 +820,16 @@ class CTGANEngine:
             else:
                 x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
                 # held for the Adam launch that follows (fold_colsum: _g_adam(jobs) is next on this stream)
-                fuse = fold_colsum and self.lanes is None and self.cfg.fuse_g_adam and \
+                fuse = fold_colsum and self.lanes is None and self.cfg.fuse_g_adam and self._adam_fusable(self.nG) and \
                     getattr(o, "gemm_adam", False)
                 o.gemm(self.da[i], x, dW, ta=True, group=3 if fuse else 0)
         self._join(1, 2, 3)
         return jobs if fold_colsum else None
+
+    def _adam_fusable(self, n: int) -> bool:
+        """May an optimizer of n parameters share its launch with a weight-gradient GEMM (fuse_adam_max)?"""
+        lim = int(self.cfg.fuse_adam_max)
+        return lim <= 0 or n * getattr(self.ops, "batch_k", 1) <= lim
 
     def _g_adam(self, jobs=None):
         b1, b2 = self.cfg.betas
@@ -914,8 +942,11 @@ class CTGANEngine:
         # enqueued BEFORE the side stream forks from the current one, so the warm-up step cannot overtake
         # the copies (it could, racing them, when the fork came first).  (A batched engine's warm-up step
         # trains every client: all of their states are restored.)
+        # (the device Philox counter too: a capture must not shift the clients' random streams, whatever step of
+        # an epoch -- or which epoch segment of a batched engine with ragged clients -- it happens at)
         state = self.batch.state_tensors() if self.batch is not None else \
-            [self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD]
+            [self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD] + \
+            ([self.ops.ctr] if hasattr(self.ops, "ctr") else [])
         snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))

@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--profile-k", type=int, default=0, help="only run the batched engine with this K (profiling)")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override (repeatable), e.g. --engine chain_d1=0")
+    ap.add_argument("--ops", action="append", default=[], metavar="KEY=VALUE",
+                    help="HipOps attribute of the issuing engine (repeatable), e.g. --ops bn_fused=1")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
+                    help="native set_tuning knob (repeatable), e.g. --tuning bn_cols=16")
     ap.add_argument("--skip-plain", action="store_true")
     ap.add_argument("--groups", type=int, nargs="*", default=[],
                     help="also K clients as G batched groups of K/G clients on G streams (one entry per G)")
@@ -56,6 +60,18 @@ def main():
         cur = getattr(cfg, key)
         setattr(cfg, key, (val.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(val))
 
+    from fed_tgan_amd.ops import native
+    for kv in args.tuning:
+        key, val = kv.split("=", 1)
+        native.require().set_tuning(key, int(val))
+
+    def set_ops(bc):
+        for kv in args.ops:
+            key, val = kv.split("=", 1)
+            for e in bc.engines:
+                cur = getattr(e.ops, key)
+                setattr(e.ops, key, (val.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(val))
+
     def timed(fn, reps):
         fn()                       # capture / warm-up
         torch.cuda.synchronize()
@@ -70,6 +86,7 @@ def main():
     if args.profile_k:
         bc = BatchedClients(tr.layout, cfg, dev, [100 + c for c in range(args.profile_k)], n_rows=len(X))
         bc.engines[0].ops.batch_plan = args.plan != "off"
+        set_ops(bc)
         for c, e in enumerate(bc.engines):
             e.set_training_data(X if c == 0 else X[rng.permutation(len(X))])
         for _ in range(args.reps):
@@ -87,11 +104,13 @@ def main():
         for plan in plans:
             bc = BatchedClients(tr.layout, cfg, dev, [100 + c for c in range(k)], n_rows=len(X))
             bc.engines[0].ops.batch_plan = plan
+            set_ops(bc)
             for c, e in enumerate(bc.engines):
                 e.set_training_data(X if c == 0 else X[rng.permutation(len(X))])
             tk = timed(bc.train_epoch, args.reps)
             tagg = timed(lambda: bc.weighted_average([1.0 / k] * k), args.reps)
-            print(json.dumps({"mode": "batched", "k": k, "batch_plan": plan, "engine": args.engine,
+            print(json.dumps({"mode": "batched", "k": k, "batch_plan": plan, "engine": args.engine, "ops": args.ops,
+                              "tuning": args.tuning,
                               "epoch_ms": round(tk * 1e3, 3),
                               "step_us": round(tk / steps * 1e6, 1), "vs_one_client": round(tk / t1, 3),
                               "fedavg_us": round(tagg * 1e6, 1)}), flush=True)
