@@ -80,18 +80,22 @@ __device__ __forceinline__ bool xcd_client_map(int lin, int T, int K, int& clien
 struct BIdx {
   int x, y, z;
 };
-// (xcd is nonzero only in batched launches -- the host sets it from ClientBatch::k -- and nothing else is read on
-// the one-client path: a grid-size read there would put a dispatch-packet load in front of every kernel's first
-// loads, ~5 us over a latency-bound one-client step's 25 launches)
+// B: the batched instantiation of the kernel (the launchers pick it when ClientBatch::xcd is set, i.e. only in
+// batched launches); the one-client instantiation reads nothing -- even a never-taken runtime branch on a kernel
+// argument put a scalar load and a wait in front of every kernel's first loads, +3.5 us over the latency-bound
+// one-client step's 25 launches (profiles/xcd_clients_r4.txt)
+template <bool B>
 __device__ __forceinline__ BIdx batch_bidx(int xcd) {
   BIdx b{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-  if (__builtin_expect(xcd != 0, 0)) {
-    const int gx = (int)gridDim.x, T = gx * (int)gridDim.y;
-    int cl, loc;
-    if (xcd_client_map(b.x + T * b.z + gx * b.y, T, (int)gridDim.z, cl, loc)) {
-      b.x = loc % gx;
-      b.y = loc / gx;
-      b.z = cl;
+  if constexpr (B) {
+    if (xcd) {
+      const int gx = (int)gridDim.x, T = gx * (int)gridDim.y;
+      int cl, loc;
+      if (xcd_client_map(b.x + T * b.z + gx * b.y, T, (int)gridDim.z, cl, loc)) {
+        b.x = loc % gx;
+        b.y = loc / gx;
+        b.z = cl;
+      }
     }
   }
   return b;

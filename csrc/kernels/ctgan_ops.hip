@@ -123,8 +123,9 @@ __device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint4 k
   return x;
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
-  const BIdx bi_ = batch_bidx(a.cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(a.cb.xcd);
   if (bi_.z) {   // batched clients: this client's buffers and seed
     const int64_t o = (int64_t)bi_.z * a.cb.stride;
     a.h = cptr(a.h, o);
@@ -259,7 +260,7 @@ void launch_sample(const SampleArgs& a0, hipStream_t stream) {
       check_slab(p, "sample operand");
   }
   const int blocks = (a.B + SAMPLE_ROWS - 1) / SAMPLE_ROWS;
-  hipLaunchKernelGGL(sample_kernel, dim3(blocks, 1, a.cb.k), dim3(SAMPLE_THREADS), 0, stream, a);
+  hipLaunchKernelGGL((client_batch().xcd ? sample_kernel<true> : sample_kernel<false>), dim3(blocks, 1, a.cb.k), dim3(SAMPLE_THREADS), 0, stream, a);
 }
 
 // ============================================================================ activation
@@ -361,12 +362,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 // span's LDS statistics with ds_max_u32 / ds_add_f32 (per-wave statistics block), so the cost
 // no longer scales with the widest span.  Gumbel noise: one Philox call feeds 4 elements of a
 // lane (index (row, k/4, lane)).
+template <bool BT_ = false>
 __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* __restrict__ logits, int ldl,
                                                                   float* __restrict__ out, int ldo, int rows,
                                                                   SpanTables sp, float inv_tau, uint64_t seed,
                                                                   const uint64_t* ctr, uint32_t stream_id,
                                                                   SlerpFuse sl, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   extern __shared__ float act_smem[];
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
@@ -531,12 +533,13 @@ __device__ __forceinline__ float3 block_sum3(float a, float b, float c, float* s
   return r;
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const float* __restrict__ logits, int ldl,
                                                                       float* __restrict__ out, int ldo, int rows,
                                                                       SpanTables sp, float inv_tau, uint64_t seed,
                                                                       const uint64_t* ctr, uint32_t stream_id,
                                                                       SlerpFuse sl, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   // LDS holds only the row image and the span statistics; the element -> span map (the first D
   // words of the packed table, shared by every row and L2-resident) is read next to the logits
   extern __shared__ float act_smem[];
@@ -632,6 +635,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
   for (int j = tid; j < sl.cols; j += blockDim.x) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const float* __restrict__ dact, int ldd,
                                                                         const float* __restrict__ act, int lda,
                                                                         const float* __restrict__ logits, int ldl,
@@ -640,7 +644,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
                                                                         float* __restrict__ dl, int ldg, int rows,
                                                                         float inv_tau, float* loss, int loss_per_row,
                                                                         ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   extern __shared__ float act_smem[];
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
@@ -788,20 +792,23 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
   }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_fwd_smem_bytes(sp);
-    allow_big_lds(activate_row_kernel, lds);
-    hipLaunchKernelGGL(activate_row_kernel, dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out,
+    allow_big_lds(activate_row_kernel<false>, lds);
+    allow_big_lds(activate_row_kernel<true>, lds);
+    hipLaunchKernelGGL((client_batch().xcd ? activate_row_kernel<true> : activate_row_kernel<false>), dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out,
                        ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);
     return;
   }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
-  allow_big_lds(activate_kernel, lds);
-  hipLaunchKernelGGL(activate_kernel, dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, logits, ldl, out,
+  allow_big_lds(activate_kernel<false>, lds);
+    allow_big_lds(activate_kernel<true>, lds);
+  hipLaunchKernelGGL((client_batch().xcd ? activate_kernel<true> : activate_kernel<false>), dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, logits, ldl, out,
                      ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);
 }
 
 // backward of the activation + fused conditional cross-entropy, one wave per row; the per-span
 // sums of g*y are LDS ds_add_f32 folds (no serial per-span loops)
+template <bool BT_ = false>
 __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float* __restrict__ dact, int ldd,
                                                                     const float* __restrict__ act, int lda,
                                                                     const float* __restrict__ logits, int ldl,
@@ -809,7 +816,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void act_bwd_ce_kernel(const float*
                                                                     const int* __restrict__ opt, float* __restrict__ dl,
                                                                     int ldg, int rows, float inv_tau, float* loss,
                                                                     int loss_per_row, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   extern __shared__ float act_smem[];
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
@@ -951,15 +958,17 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
   }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_smem_bytes(sp);
-    allow_big_lds(act_bwd_ce_row_kernel, lds);
-    hipLaunchKernelGGL(act_bwd_ce_row_kernel, dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, dact, ldd, act,
+    allow_big_lds(act_bwd_ce_row_kernel<false>, lds);
+    allow_big_lds(act_bwd_ce_row_kernel<true>, lds);
+    hipLaunchKernelGGL((client_batch().xcd ? act_bwd_ce_row_kernel<true> : act_bwd_ce_row_kernel<false>), dim3(rows, 1, cb.k), dim3(ROW_WAVES * 64), lds, stream, dact, ldd, act,
                        lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row, cb);
     return;
   }
   const int nw = act_waves(sp);
   const size_t lds = act_smem_bytes(sp, nw);
-  allow_big_lds(act_bwd_ce_kernel, lds);
-  hipLaunchKernelGGL(act_bwd_ce_kernel, dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, dact, ldd, act,
+  allow_big_lds(act_bwd_ce_kernel<false>, lds);
+    allow_big_lds(act_bwd_ce_kernel<true>, lds);
+  hipLaunchKernelGGL((client_batch().xcd ? act_bwd_ce_kernel<true> : act_bwd_ce_kernel<false>), dim3((rows + nw - 1) / nw, 1, cb.k), dim3(nw * 64), lds, stream, dact, ldd, act,
                      lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, loss_per_row, cb);
 }
 
@@ -969,10 +978,11 @@ size_t activation_smem_bytes(const SpanTables& sp) {
 
 // ============================================================================ gradient penalty pieces
 // one wave per row
+template <bool BT_ = false>
 __global__ __launch_bounds__(256) void slerp_kernel(const float* __restrict__ real, const float* __restrict__ fake,
                                                     float* __restrict__ out, int rows, int cols, int ld, uint64_t seed,
                                                     const uint64_t* ctr, uint32_t stream_id, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     real = cptr(real, co);
@@ -1006,7 +1016,7 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
   if (rows == 0) return;
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("slerp operand", real, fake, out, ctr);
-  hipLaunchKernelGGL(slerp_kernel, dim3((rows + 3) / 4, 1, cb.k), dim3(256), 0, stream, real, fake, out, rows, cols, ld,
+  hipLaunchKernelGGL((client_batch().xcd ? slerp_kernel<true> : slerp_kernel<false>), dim3((rows + 3) / 4, 1, cb.k), dim3(256), 0, stream, real, fake, out, rows, cols, ld,
                      seed, ctr, stream_id, cb);
 }
 
@@ -1026,10 +1036,11 @@ __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, f
   }
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                           int ldo, int rows, int cols, float lam, float* loss,
                                                           int loss_per_row, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
@@ -1055,10 +1066,11 @@ __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restric
     if ((int)threadIdx.x + 256 * i < n4) o[threadIdx.x + 256 * i] = v[i] * coef;
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                        int ldo, int rows, int cols, float lam, float* loss,
                                                        int loss_per_row, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
@@ -1084,10 +1096,11 @@ __global__ __launch_bounds__(256) void gp_scale_kernel(const float* __restrict__
 
 // rows wider than the register-resident variant: two passes over the row in chunks of
 // GP_V4 float4 per thread, each chunk's loads issued together
+template <bool BT_ = false>
 __global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __restrict__ g, int ldg,
                                                                float* __restrict__ out, int ldo, int rows, int cols,
                                                                float lam, float* loss, int loss_per_row, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     g = cptr(g, co);
@@ -1132,13 +1145,13 @@ void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int
   const bool v4 = al && cols <= GP_V4 * 256 * 4;
   const dim3 grid(rows, 1, cb.k);
   if (al && !v4)
-    hipLaunchKernelGGL(gp_scale_v4_wide_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+    hipLaunchKernelGGL((client_batch().xcd ? gp_scale_v4_wide_kernel<true> : gp_scale_v4_wide_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
   else if (v4)
-    hipLaunchKernelGGL(gp_scale_v4_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+    hipLaunchKernelGGL((client_batch().xcd ? gp_scale_v4_kernel<true> : gp_scale_v4_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
   else
-    hipLaunchKernelGGL(gp_scale_kernel, grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
+    hipLaunchKernelGGL((client_batch().xcd ? gp_scale_kernel<true> : gp_scale_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
 }
 
@@ -1185,8 +1198,9 @@ struct ColsumBatch {
   int n_jobs;
 };
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(CS_COLS* CS_GROUPS) void colsum_kernel(ColsumBatch bt, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   __shared__ float part[2][CS_GROUPS][CS_COLS + 1];
   const ColsumJob jb = client_job(bt.jobs[bi_.y], (int64_t)bi_.z * cb.stride);
   const int c = bi_.x * CS_COLS + (threadIdx.x % CS_COLS);
@@ -1239,7 +1253,7 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
     for (int i = 0; i < n_jobs; ++i)
       check_slabs("colsum job", bt.jobs[i].a, bt.jobs[i].out, bt.jobs[i].w, bt.jobs[i].dot_v, bt.jobs[i].dot_e,
                   bt.jobs[i].dot_out, bt.jobs[i].dot_w);
-  hipLaunchKernelGGL(colsum_kernel, dim3((maxc + CS_COLS - 1) / CS_COLS, n_jobs, cb.k), dim3(CS_COLS * CS_GROUPS), 0,
+  hipLaunchKernelGGL((client_batch().xcd ? colsum_kernel<true> : colsum_kernel<false>), dim3((maxc + CS_COLS - 1) / CS_COLS, n_jobs, cb.k), dim3(CS_COLS * CS_GROUPS), 0,
                      stream, bt, cb);
 }
 
@@ -1251,6 +1265,9 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
 // Loads use clamped (always valid) addresses and are masked afterwards (no predicated loads).
 constexpr int BN_THREADS = 512, BN_WAVES = BN_THREADS / 64;
 int g_bn_cols = 8;    // columns per workgroup (tuning knob, see set_tuning)
+// (16 columns for batched launches measured +1.0 ms per 8-client epoch once the clients sit on their own XCDs:
+// 47.7 vs 48.7 ms, profiles/batched_r4.md; 8 everywhere)
+static int bn_cols_for_launch() { return g_bn_cols; }
 
 // ``groups`` (1 or 2) independent batches of rows/groups consecutive rows each: the D-phase and
 // G-phase batches of a step go through the generator as ONE M = 2B GEMM chain, but BatchNorm keeps
@@ -1280,13 +1297,13 @@ __device__ __forceinline__ void bn_colsum(float (&v)[NV], float* sh) {
   __syncthreads();
 }
 
-template <int COLS, int MAXR>
+template <int COLS, int MAXR, bool BT_ = false>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
@@ -1364,13 +1381,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
 // Large batches (more rows than the register-resident kernel holds): two passes over the
 // column block, statistics first, then normalise + ReLU re-reading the GEMM output (L2-resident at
 // these sizes).  Same shifted one-pass statistics and running-stat order as above.
-template <int COLS>
+template <int COLS, bool BT_ = false>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_stream_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
     float momentum, float eps, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
@@ -1452,12 +1469,13 @@ __device__ __forceinline__ void chan_merge(float& n, float& mu, float& m2, float
   }
 }
 
+template <bool BT_ = false>
 __global__ __launch_bounds__(BNA_THREADS) void bn_relu_apply_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ part, int n_tiles, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn,
     float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows,
     int cols, int groups, float momentum, float eps, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     a = cptr(a, co);
@@ -1547,7 +1565,7 @@ void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tile
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("bn_relu_apply operand", a, part, gamma, beta, out, nhat, mean, invstd, rm, rv);
   const dim3 grid((cols + BNA_COLS - 1) / BNA_COLS, (rows + BNA_ROWS - 1) / BNA_ROWS, cb.k);
-  hipLaunchKernelGGL(bn_relu_apply_kernel, grid, dim3(BNA_THREADS), 0, stream, a, lda, part, n_tiles, gamma, beta,
+  hipLaunchKernelGGL((client_batch().xcd ? bn_relu_apply_kernel<true> : bn_relu_apply_kernel<false>), grid, dim3(BNA_THREADS), 0, stream, a, lda, part, n_tiles, gamma, beta,
                      out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb);
 }
 
@@ -1560,7 +1578,7 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
   if (cb.k > 1) check_slabs("bn_relu_train operand", a, gamma, beta, out, nhat, mean, invstd, rm, rv);
   const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
 #define BN_TRAIN_LAUNCH(R)                                                                                          \
-  hipLaunchKernelGGL((bn_relu_train_kernel<COLS, R>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, \
+  hipLaunchKernelGGL((client_batch().xcd ? bn_relu_train_kernel<COLS, R, true> : bn_relu_train_kernel<COLS, R, false>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, \
                      ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb)
   if (rows <= 4 * GROUPS) BN_TRAIN_LAUNCH(4);
   else if (rows <= 8 * GROUPS) BN_TRAIN_LAUNCH(8);
@@ -1568,7 +1586,7 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
   else if (rows <= 32 * GROUPS) BN_TRAIN_LAUNCH(32);
   else if (rows <= 64 * GROUPS) BN_TRAIN_LAUNCH(64);
   else
-    hipLaunchKernelGGL((bn_relu_train_stream_kernel<COLS>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo,
+    hipLaunchKernelGGL((client_batch().xcd ? bn_relu_train_stream_kernel<COLS, true> : bn_relu_train_stream_kernel<COLS, false>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo,
                        nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb);
 #undef BN_TRAIN_LAUNCH
 }
@@ -1576,10 +1594,11 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
 void launch_bn_relu_train(const float* a, int lda, const float* gamma, const float* beta, float* out, int ldo,
                           float* nhat, int ldn, float* mean, float* invstd, float* rm, float* rv, int rows, int cols,
                           int groups, float momentum, float eps, hipStream_t stream) {
-  if (g_bn_cols == 4)
+  const int bc = bn_cols_for_launch();
+  if (bc == 4)
     bn_train_cols<4>(a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps,
                      stream);
-  else if (g_bn_cols == 16)
+  else if (bc == 16)
     bn_train_cols<16>(a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows, cols, groups, momentum,
                       eps, stream);
   else
@@ -1587,12 +1606,12 @@ void launch_bn_relu_train(const float* a, int lda, const float* gamma, const flo
                      stream);
 }
 
-template <int COLS, int MAXR>
+template <int COLS, int MAXR, bool BT_ = false>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     dr = cptr(dr, co);
@@ -1650,12 +1669,12 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
 }
 
 // Large-batch backward: the three column sums in a first pass, da in a second (re-reading).
-template <int COLS>
+template <int COLS, bool BT_ = false>
 __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_stream_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     dr = cptr(dr, co);
@@ -1710,7 +1729,7 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
   if (cb.k > 1) check_slabs("bn_relu_bwd operand", dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias);
   const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
 #define BN_BWD_LAUNCH(R)                                                                                          \
-  hipLaunchKernelGGL((bn_relu_bwd_kernel<COLS, R>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, \
+  hipLaunchKernelGGL((client_batch().xcd ? bn_relu_bwd_kernel<COLS, R, true> : bn_relu_bwd_kernel<COLS, R, false>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, \
                      invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, cb)
   if (rows <= 4 * GROUPS) BN_BWD_LAUNCH(4);
   else if (rows <= 8 * GROUPS) BN_BWD_LAUNCH(8);
@@ -1718,7 +1737,7 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
   else if (rows <= 32 * GROUPS) BN_BWD_LAUNCH(32);
   else if (rows <= 64 * GROUPS) BN_BWD_LAUNCH(64);
   else
-    hipLaunchKernelGGL((bn_relu_bwd_stream_kernel<COLS>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma,
+    hipLaunchKernelGGL((client_batch().xcd ? bn_relu_bwd_stream_kernel<COLS, true> : bn_relu_bwd_stream_kernel<COLS, false>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma,
                        invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, cb);
 #undef BN_BWD_LAUNCH
 }
@@ -1726,9 +1745,10 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream) {
-  if (g_bn_cols == 4)
+  const int bc = bn_cols_for_launch();
+  if (bc == 4)
     bn_bwd_cols<4>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
-  else if (g_bn_cols == 16)
+  else if (bc == 16)
     bn_bwd_cols<16>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
   else
     bn_bwd_cols<8>(dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, stream);
@@ -1741,12 +1761,12 @@ void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, cons
 int g_adam_store = 16;
 int g_adam_max_blocks = 65535;
 
-template <int AUX>
+template <int AUX, bool BT_ = false>
 __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
                                                    float4* __restrict__ m, float4* __restrict__ v,
                                                    const float* __restrict__ step, int64_t n4, float lr, float b1,
                                                    float b2, float eps, float wd, uint64_t* rng_bump, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     p = cptr(p, co);
@@ -1779,9 +1799,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const
   if (rng_bump && bi_.x == 0 && threadIdx.x == 0) rng_bump[0] += 1ull;
 }
 
+template <bool BT_ = false>
 __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, const float* step, int64_t start,
                                  int64_t n, float lr, float b1, float b2, float eps, float wd, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   if (bi_.z) {
     const int64_t co = (int64_t)bi_.z * cb.stride;
     p = cptr(p, co);
@@ -1809,13 +1830,13 @@ __global__ void adam_tail_kernel(float* p, const float* g, float* m, float* v, c
 // exactly those elements straight from registers.  Every other workgroup runs the float4 Adam and
 // skips the float4 groups the jobs own: job outputs start 16-B aligned and own ceil4(cols)
 // elements (the flat layout stores every tensor that way), so no float4 is shared.
-template <int AUX, int U>
+template <int AUX, int U, bool BT_ = false>
 __global__ __launch_bounds__(256) void adam_cs_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       const float* __restrict__ step, int64_t n4, float lr, float b1,
                                                       float b2, float eps, float wd, uint64_t* rng_bump, AdamColsum cs,
                                                       ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   const int64_t co = (int64_t)bi_.z * cb.stride;
   if (co) {
     p = cptr(p, co);
@@ -1845,7 +1866,7 @@ void launch_adam_colsum(float* p, const float* g, float* m, float* v, const floa
     check_slab(cs);
   }
 #define FEDTGAN_ADAM_CS(AUX, UU)                                                                                       \
-  hipLaunchKernelGGL((adam_cs_kernel<AUX, UU>), dim3(grid, 1, cb.k), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, \
+  hipLaunchKernelGGL((client_batch().xcd ? adam_cs_kernel<AUX, UU, true> : adam_cs_kernel<AUX, UU, false>), dim3(grid, 1, cb.k), dim3(256), 0, stream, p, g, m, v, step, n4, lr, b1, \
                      b2, eps, wd, rng_ctr_bump, cs, cb)
 #define FEDTGAN_ADAM_CS_U(AUX)                  \
   if (U == ADAM_U) FEDTGAN_ADAM_CS(AUX, ADAM_U); \
@@ -1856,7 +1877,7 @@ void launch_adam_colsum(float* p, const float* g, float* m, float* v, const floa
 #undef FEDTGAN_ADAM_CS_U
 #undef FEDTGAN_ADAM_CS
   if (n4 * 4 < n)
-    hipLaunchKernelGGL(adam_tail_kernel, dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
+    hipLaunchKernelGGL((client_batch().xcd ? adam_tail_kernel<true> : adam_tail_kernel<false>), dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
                        eps, wd, cb);
 }
 
@@ -1869,7 +1890,7 @@ void launch_adam(float* p, const float* g, float* m, float* v, const float* step
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("adam operand", p, g, m, v, step, rng_ctr_bump);
 #define FEDTGAN_ADAM(AUX)                                                                                       \
-  hipLaunchKernelGGL(adam_kernel<AUX>, dim3(std::max(blocks, 1), 1, cb.k), dim3(256), 0, stream,                 \
+  hipLaunchKernelGGL((client_batch().xcd ? adam_kernel<AUX, true> : adam_kernel<AUX, false>), dim3(std::max(blocks, 1), 1, cb.k), dim3(256), 0, stream,                 \
                      reinterpret_cast<float4*>(p), reinterpret_cast<const float4*>(g), reinterpret_cast<float4*>(m), \
                      reinterpret_cast<float4*>(v), step, n4, lr, b1, b2, eps, wd, rng_ctr_bump, cb)
   if (g_adam_store == 2) FEDTGAN_ADAM(2);
@@ -1877,7 +1898,7 @@ void launch_adam(float* p, const float* g, float* m, float* v, const float* step
   else FEDTGAN_ADAM(0);
 #undef FEDTGAN_ADAM
   if (n4 * 4 < n)
-    hipLaunchKernelGGL(adam_tail_kernel, dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
+    hipLaunchKernelGGL((client_batch().xcd ? adam_tail_kernel<true> : adam_tail_kernel<false>), dim3(1, 1, cb.k), dim3(64), 0, stream, p, g, m, v, step, n4 * 4, n, lr, b1, b2,
                        eps, wd, cb);
 }
 
@@ -2104,8 +2125,9 @@ void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream) {
   hipLaunchKernelGGL(gen_weight_prep_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a);
 }
 
+template <bool BT_ = false>
 __global__ void rng_bump_kernel(uint64_t* ctr, ClientBatch cb) {
-  const BIdx bi_ = batch_bidx(cb.xcd);
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
   ctr = cptr(ctr, (int64_t)bi_.z * cb.stride);
   ctr[0] += 1ull;
 }
@@ -2113,7 +2135,7 @@ __global__ void rng_bump_kernel(uint64_t* ctr, ClientBatch cb) {
 void launch_rng_bump(uint64_t* ctr, hipStream_t stream) {
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slab(ctr, "rng counter");
-  hipLaunchKernelGGL(rng_bump_kernel, dim3(1, 1, cb.k), dim3(1), 0, stream, ctr, cb);
+  hipLaunchKernelGGL((client_batch().xcd ? rng_bump_kernel<true> : rng_bump_kernel<false>), dim3(1, 1, cb.k), dim3(1), 0, stream, ctr, cb);
 }
 
 }  // namespace fedtgan

@@ -995,7 +995,7 @@ struct Grid3 {
 
 template <class P1, class P2, bool BATCH = false>
 __global__ __launch_bounds__(NT) void gemm_pair_kernel(GemmArgs g1, GemmArgs g2, Grid3 grid1, Grid3 grid2) {
-  const BIdx bi_ = batch_bidx(g1.xcd_cl);
+  const BIdx bi_ = batch_bidx<BATCH>(g1.xcd_cl);
   constexpr int S1 = 2 * Cfg<false, P1::TM, P1::TM>::STAGE, S2 = 2 * Cfg<false, P2::TM, P2::TM>::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[S1 > S2 ? S1 : S2];
   if constexpr (BATCH) {
@@ -1050,9 +1050,9 @@ __device__ __forceinline__ float splitk_value(const GemmArgs& g, size_t idx, int
   return apply_epi(g, v, m, n, step, idx);
 }
 
-template <int SMAX>
+template <int SMAX, bool BT_ = false>
 __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
-  const BIdx bi_ = batch_bidx(g.xcd_cl);
+  const BIdx bi_ = batch_bidx<BT_>(g.xcd_cl);
   if (bi_.z) client_view(g, bi_.z);
   const size_t total = (size_t)g.M * g.N;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
@@ -1072,9 +1072,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
 // were launches of their own after D0's / R0's reduction.
 constexpr int CH_MAXK = 1024, CH_COLS = 64;
 // MASK: head and tail both EPI_MASK (the R chain) -- the launch carries no Philox / BN epilogue code
-template <int SMAX, bool MASK = false>
+template <int SMAX, bool MASK = false, bool BT_ = false>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
-  const BIdx bi_ = batch_bidx(g.xcd_cl);
+  const BIdx bi_ = batch_bidx<BT_>(g.xcd_cl);
   __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
   __shared__ float part[4][CH_COLS];
   if (bi_.z) {
@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(NT) void gemm_adam_kernel(GemmArgs g, Grid3 gd, flo
                                                        float* v, const float* step, int64_t n4, float lr, float b1,
                                                        float b2, float eps, float wd, uint64_t* rng_bump,
                                                        AdamColsum cs) {
-  const BIdx bi_ = batch_bidx(g.xcd_cl);
+  const BIdx bi_ = batch_bidx<BATCH>(g.xcd_cl);
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, TM, TM>::STAGE];
   int64_t co = 0;
   if constexpr (BATCH) {
@@ -1184,9 +1184,11 @@ static dim3 gemm_prepare(GemmArgs& g) {
   // an L2 whatever K is (generate_decoded(40000): 375 -> 360 us)
   g.red_inl = g.tile_cnt != nullptr && g_gemm_splitk_inlaunch && g.splitk > 1 && T <= 64 && g.N % 4 == 0 &&
               (int64_t)g.splitk * g.M * g.N * 4 < (int64_t)INT32_MAX;
+  // (and on any grid of >= 1024 workgroups: the wide table's GEMMs -- dW_out 3,190 128-tiles over K = 500, dW0,
+  // g = A0 W0 over 2,154 tiles -- 0.3256 -> 0.3145 s/epoch with the remap forced, profiles/wide_r4.md)
   g.xcd_remap = g_gemm_xcd_remap == 2 ||
                 (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768) ||
-                                           (T == 128 && tm >= 64)));
+                                           (T == 128 && tm >= 64) || (int64_t)tm * tn * g.splitk >= 1024));
   return dim3(tn, tm, g.splitk);
 }
 
@@ -1272,8 +1274,8 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
 #define FEDTGAN_CHAIN(S)                                                                                 \
   do {                                                                                                   \
-    if (mk) hipLaunchKernelGGL((chain_epilogue_kernel<S, true>), grid, block, 0, stream, h, t);          \
-    else hipLaunchKernelGGL((chain_epilogue_kernel<S, false>), grid, block, 0, stream, h, t);            \
+    if (mk) hipLaunchKernelGGL((g.xcd_cl ? chain_epilogue_kernel<S, true, true> : chain_epilogue_kernel<S, true, false>), grid, block, 0, stream, h, t);          \
+    else hipLaunchKernelGGL((g.xcd_cl ? chain_epilogue_kernel<S, false, true> : chain_epilogue_kernel<S, false, false>), grid, block, 0, stream, h, t);            \
   } while (0)
     if (g.splitk <= 1 || g.red_inl) FEDTGAN_CHAIN(0);
     else if (g.splitk <= 8) FEDTGAN_CHAIN(8);
@@ -1287,10 +1289,10 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
   const size_t total = (size_t)g.M * g.N;
   int blocks = (int)std::min<size_t>((total + 255) / 256, 2048);
   const dim3 grid(blocks, 1, g.nclient);
-  if (g.splitk <= 8) hipLaunchKernelGGL(gemm_splitk_epilogue<8>, grid, dim3(256), 0, stream, g);
-  else if (g.splitk <= 16) hipLaunchKernelGGL(gemm_splitk_epilogue<16>, grid, dim3(256), 0, stream, g);
-  else if (g.splitk <= 32) hipLaunchKernelGGL(gemm_splitk_epilogue<32>, grid, dim3(256), 0, stream, g);
-  else hipLaunchKernelGGL(gemm_splitk_epilogue<64>, grid, dim3(256), 0, stream, g);
+  if (g.splitk <= 8) hipLaunchKernelGGL((g.xcd_cl ? gemm_splitk_epilogue<8, true> : gemm_splitk_epilogue<8, false>), grid, dim3(256), 0, stream, g);
+  else if (g.splitk <= 16) hipLaunchKernelGGL((g.xcd_cl ? gemm_splitk_epilogue<16, true> : gemm_splitk_epilogue<16, false>), grid, dim3(256), 0, stream, g);
+  else if (g.splitk <= 32) hipLaunchKernelGGL((g.xcd_cl ? gemm_splitk_epilogue<32, true> : gemm_splitk_epilogue<32, false>), grid, dim3(256), 0, stream, g);
+  else hipLaunchKernelGGL((g.xcd_cl ? gemm_splitk_epilogue<64, true> : gemm_splitk_epilogue<64, false>), grid, dim3(256), 0, stream, g);
 }
 
 void launch_gemm(GemmArgs g, hipStream_t stream) {

@@ -76,6 +76,8 @@ if __name__ == "__main__":
     # helper process of the federated runtime (fed/runtime.py start_label_encoders): the sklearn import
     # and the pickle happen here, off the federator's critical path.  stdin: {"path", "vocabs": [[name, classes]]}
     import json
+    import os
     import sys
+    os.nice(19)          # the federator's rounds run meanwhile: this process only takes idle CPU time
     req = json.load(sys.stdin)
     write_label_encoders(req["path"], [CategoryVocab(c, n) for n, c in req["vocabs"]])

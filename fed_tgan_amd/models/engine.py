@@ -130,6 +130,9 @@ class EngineConfig:
     # HIP, bf16: each generator layer's Linear -> BatchNorm(train) -> ReLU as ONE launch, a workgroup
     # owning 16 output columns of one batch (kernels/bn_fused.hip) instead of a tile GEMM + BN launch
     bn_colown: bool = False
+    # initial weights drawn from a generator of the engine's own, seeded by the engine seed ("engine": reproducible
+    # whatever other threads do), or from torch's process-wide generator ("global", the reference modules' init)
+    init_rng: str = "engine"
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -330,6 +333,11 @@ class CTGANEngine:
         so each weight is drawn once."""
         import math
         from torch import nn
+        if self.cfg.init_rng == "global":      # torch's process-wide generator (the reference modules' own init)
+            self.load_modules(Generator(self.E + self.C, self.gdims, self.Dd), Discriminator(self.Din, self.ddims, self.P))
+            self.mG.zero_(); self.vG.zero_(); self.mD.zero_(); self.vD.zero_()
+            self.stepG.zero_(); self.stepD.zero_()
+            return
         gen = torch.Generator().manual_seed(self.seed)
         with torch.device("meta"):
             G = Generator(self.E + self.C, self.gdims, self.Dd)

@@ -23,6 +23,9 @@ from . import native
 EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 4
 
 
+LONG_K_64 = True    # _plan's long-K rule with 64x64 tiles when workgroups are plentiful (A/B knob)
+
+
 def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
     """(output tile, split-K factor) for the burst GEMM (one K-burst = ``kc`` values per row).
 
@@ -55,7 +58,16 @@ def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
         return 32, 1
     cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
     want = max(-(-512 // t32), -(-bursts // 8))
-    return 32, int(max(1, min(want, -(-bursts // 2), cap_ws)))
+    sk32 = int(max(1, min(want, -(-bursts // 2), cap_ws)))
+    if LONG_K_64 and c == 1 and t32 * min(sk32, 64) >= 768:
+        # plenty of workgroups either way (the wide table's K = 137k): 64x64 tiles re-read the long operands half as
+        # often (the 150-row D0 input by 4 instead of 8 column tiles, W0 by 3 instead of 5 row tiles).  Measured
+        # (tools/batched_ops.py): the wide table's D0 forward 101.5 -> 72.3 us; the one-client Intrusion GEMMs stay
+        # below the threshold.  (8 batched clients: 42.9 -> 37.7 us for D0's forward alone, but the step lost
+        # 0.3 ms per epoch -- profiles/batched_r4.md -- so batched launches keep the 32-tile plan)
+        want = max(-(-512 // t64), -(-bursts // 8))
+        return 64, int(max(1, min(want, -(-bursts // 2), cap_ws)))
+    return 32, sk32
 
 
 def _is_transposed(t) -> bool:

@@ -20,6 +20,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--spec", default="intrusion", help="dataset schema (intrusion, wide, ...)")
+    ap.add_argument("--only", type=int, nargs="*", default=None, help="only these call indices")
     ap.add_argument("--rows", type=int, default=40000)
     ap.add_argument("--tiles", type=int, nargs="+", default=[32, 64, 128])
     ap.add_argument("--splits", type=int, nargs="+", default=[0, 1, 2, 4, 8], help="0 = the planner's split-K")
@@ -30,7 +32,7 @@ def main():
     args = ap.parse_args()
     import numpy as np
     import torch
-    from fed_tgan_amd.data.schema import intrusion_spec
+    from fed_tgan_amd.data.schema import get_spec
     from fed_tgan_amd.data.synthetic import generate
     from fed_tgan_amd.data.table import TablePreprocessor
     from fed_tgan_amd.features.transformer import VGMTransformer
@@ -43,7 +45,7 @@ def main():
         key, val = kv.split("=", 1)
         native.require().set_tuning(key, int(val))
     dev = torch.device("cuda:0")
-    spec = intrusion_spec()
+    spec = get_spec(args.spec)
     df = generate(spec, args.rows, seed=0)
     tp = TablePreprocessor(df, "Intrusion", spec.problem_type, spec.target_column, spec.categorical_list,
                            spec.nonnegative_list)
@@ -93,6 +95,8 @@ def main():
 
     with bc._batched():
         for i, (a, b, c, kw) in enumerate(calls):
+            if args.only is not None and i not in args.only:
+                continue
             kw = dict(kw)
             kw["group"] = 0
             kw.pop("chain", None)

@@ -29,6 +29,8 @@ def main():
                     help="HipOps attribute of the issuing engine (repeatable), e.g. --ops bn_fused=1")
     ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
                     help="native set_tuning knob (repeatable), e.g. --tuning bn_cols=16")
+    ap.add_argument("--module", action="append", default=[], metavar="KEY=VALUE",
+                    help="boolean fed_tgan_amd.ops.hip module flag, e.g. --module LONG_K_64=0")
     ap.add_argument("--skip-plain", action="store_true")
     ap.add_argument("--groups", type=int, nargs="*", default=[],
                     help="also K clients as G batched groups of K/G clients on G streams (one entry per G)")
@@ -64,6 +66,11 @@ def main():
     for kv in args.tuning:
         key, val = kv.split("=", 1)
         native.require().set_tuning(key, int(val))
+
+    import fed_tgan_amd.ops.hip as hipmod
+    for kv in args.module:
+        key, val = kv.split("=", 1)
+        setattr(hipmod, key, val.lower() in ("1", "true", "yes"))
 
     def set_ops(bc):
         for kv in args.ops:

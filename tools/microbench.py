@@ -260,6 +260,7 @@ def unroll_sweep(eng, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--init-rng", default=None, help="EngineConfig.init_rng (engine | global)")
     ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
     ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
     ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
@@ -282,7 +283,10 @@ def main():
     from helpers import small_table
     dev = torch.device("cuda:0")
     _, _, _, _, _, _, tr, X = small_table(40000, 0)
-    eng = CTGANEngine(tr.layout, EngineConfig(precision=args.precision), dev, backend="hip", seed=1)
+    cfg = EngineConfig(precision=args.precision)
+    if args.init_rng:
+        cfg.init_rng = args.init_rng
+    eng = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=1)
     eng.set_training_data(X)
     o = eng.ops
     nP, B = eng.nP, eng.B

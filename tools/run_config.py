@@ -50,7 +50,14 @@ def main():
                     help="emulated clients as one batched engine (FedConfig.batched_clients) or one engine per thread")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override for A/B runs, e.g. --engine g_wt=1")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
+                    help="native set_tuning knob for A/B runs, e.g. --tuning gemm_pairs=0")
     args = ap.parse_args()
+    if args.tuning:
+        from fed_tgan_amd.ops import native
+        for kv in args.tuning:
+            key, val = kv.split("=", 1)
+            native.require().set_tuning(key, int(val))
 
     from fed_tgan_amd.data.schema import get_spec
     from fed_tgan_amd.data.synthetic import generate, shard
@@ -102,6 +109,8 @@ def main():
             "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
     if args.engine:
         summ["engine_overrides"] = args.engine
+    if args.tuning:
+        summ["tuning"] = args.tuning
     print(json.dumps(summ), flush=True)
     if args.json:
         with open(args.json, "a") as f:
