@@ -58,6 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="EngineConfig override for A/B measurements, e.g. --engine onehot=0")
     ap.add_argument("--fed", action="append", default=[], metavar="KEY=VALUE",
                     help="FedConfig override for A/B measurements, e.g. --fed csv_threads=8")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
+                    help="native set_tuning knob for A/B measurements, e.g. --tuning gemm_xcd_remap=0")
     ap.add_argument("--phase-timer", default="events", choices=["events", "sync"],
                     help="phase timers: HIP events (no host sync) or stream-synchronised wall time")
     ap.add_argument("--force-dist", action="store_true",
@@ -199,6 +201,11 @@ def run_rank(args) -> None:
         k, v = kv.split("=", 1)
         cur = getattr(cfg, k)
         setattr(cfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+    if args.tuning:
+        from fed_tgan_amd.ops import native
+        for kv in args.tuning:
+            k, v = kv.split("=", 1)
+            native.require().set_tuning(k, int(v))
     rt = FedRuntime(cfg, comm, device)
     rt.initialize()
     for ep in range(args.warmup):
@@ -272,6 +279,8 @@ def run_rank(args) -> None:
                            "rccl_version": ver, "transport": _rccl_transport(rccl_dir)}
         if args.engine:
             rec["engine_overrides"] = args.engine
+        if args.tuning:
+            rec["tuning"] = args.tuning
         print(json.dumps(rec), flush=True)
     comm.destroy()
 

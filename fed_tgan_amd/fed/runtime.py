@@ -126,6 +126,9 @@ class FedConfig:
     batched_clients: str = "auto"
     batched_max_auto: int = 4
     batched_arena_mb: float = 0.0           # per-client arena slab of the batched engine (0: estimated)
+    # write models/label_encoders_{name}.pickle during initialisation (a helper process, as the reference writes it
+    # there) instead of after the last round
+    label_encoders_early: bool = True
 
 
 def _log(cfg: FedConfig, rank: int, *msg):
@@ -279,7 +282,8 @@ class FedRuntime:
         self.cat_idx = cat_idx
         if self.is_fed:
             self._write_meta_artifacts()
-            self.start_label_encoders()
+            if cfg.label_encoders_early:
+                self.start_label_encoders()
         if warm is not None:
             warm.join()
         self.init_times = {"meta": time.time() - t0}

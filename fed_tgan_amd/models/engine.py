@@ -329,29 +329,32 @@ class CTGANEngine:
         nn.Linear's kaiming-uniform weights and U(+-1/sqrt(fan_in)) biases, BN 1/0), drawn from a generator
         of this engine's own (seeded by the engine seed) instead of torch's process-wide one: client threads
         that build their engines concurrently (fed/local.py) would otherwise race on the global generator and
-        an emulated federation would not reproduce run to run.  The modules are built on the meta device,
-        so each weight is drawn once."""
+        an emulated federation would not reproduce run to run.  The draws go straight into the flat buffer in
+        module order (weight then bias of each Linear, G then D) with nn.Linear's bounds: kaiming-uniform with
+        a=sqrt(5) is U(+-1/sqrt(fan_in)).  No torch modules are built (a meta-device build imports
+        torch._meta_registrations, 0.4 s of cold start)."""
         import math
-        from torch import nn
         if self.cfg.init_rng == "global":      # torch's process-wide generator (the reference modules' own init)
             self.load_modules(Generator(self.E + self.C, self.gdims, self.Dd), Discriminator(self.Din, self.ddims, self.P))
             self.mG.zero_(); self.vG.zero_(); self.mD.zero_(); self.vD.zero_()
             self.stepG.zero_(); self.stepD.zero_()
             return
         gen = torch.Generator().manual_seed(self.seed)
-        with torch.device("meta"):
-            G = Generator(self.E + self.C, self.gdims, self.Dd)
-            D = Discriminator(self.Din, self.ddims, self.P)
-        G, D = G.to_empty(device="cpu"), D.to_empty(device="cpu")
         with torch.no_grad():
-            for m in list(G.modules()) + list(D.modules()):
-                if isinstance(m, nn.Linear):
-                    nn.init.kaiming_uniform_(m.weight, a=math.sqrt(5), generator=gen)
-                    bound = 1.0 / math.sqrt(m.weight.shape[1]) if m.weight.shape[1] > 0 else 0.0
-                    nn.init.uniform_(m.bias, -bound, bound, generator=gen)
-                elif isinstance(m, nn.BatchNorm1d):
-                    m.reset_parameters()
-        self.load_modules(G, D)
+            for key, name in self.g_key_map() + self.d_key_map():
+                p = self.p[name]
+                if key.endswith("running_mean") or key.endswith("bn.bias"):
+                    p.zero_()
+                elif key.endswith("running_var") or key.endswith("bn.weight"):
+                    p.fill_(1.0)
+                elif key.endswith("weight"):
+                    fan_in = p.shape[1]
+                    bound = 1.0 / math.sqrt(fan_in) if fan_in > 0 else 0.0
+                    p.copy_(torch.empty(tuple(p.shape)).uniform_(-bound, bound, generator=gen))
+                    wb = bound
+                else:                                  # the Linear's bias, right after its weight
+                    p.copy_(torch.empty(tuple(p.shape)).uniform_(-wb, wb, generator=gen))
+        self.bn_batches = 0
         self.mG.zero_(); self.vG.zero_(); self.mD.zero_(); self.vD.zero_()
         self.stepG.zero_(); self.stepD.zero_()
 

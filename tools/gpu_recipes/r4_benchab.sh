@@ -1,0 +1,13 @@
+# Same box: bench line and one-client step, round-3 tree vs HEAD, alternating.
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/${1:-r4benchab}
+mkdir -p $OUT
+for i in 1 2; do
+  (cd $R/_basetree && timeout -k 10 150 python bench.py --steps 20 --warmup 5 2>/dev/null | tail -1 >> $OUT/base_bench.jsonl) || exit 1
+  (cd $R && timeout -k 10 150 python bench.py --steps 20 --warmup 5 2>/dev/null | tail -1 >> $OUT/head_bench.jsonl) || exit 1
+done
+(cd $R/_basetree && timeout -k 10 150 python tools/microbench.py --step-only >> $OUT/base_step.txt 2>&1) || exit 1
+(cd $R && timeout -k 10 150 python tools/microbench.py --step-only >> $OUT/head_step.txt 2>&1) || exit 1
+echo "exit $?"
