@@ -457,6 +457,28 @@ void gp_scale(const Tensor& g, const Tensor& out, double lam, const Tensor& loss
                            fp(loss), per_row ? 1 : 0, cur_stream());
 }
 
+void onehot_wgrad(const std::vector<Tensor>& dy, const std::vector<Tensor>& w, const Tensor& col, const Tensor& opt,
+                  const Tensor& cond_off, int64_t zero) {
+  TORCH_CHECK(dy.size() == w.size() && !dy.empty() && dy.size() <= 4, "onehot_wgrad: 1-4 (dy, w) jobs");
+  TORCH_CHECK(col.scalar_type() == at::kInt && opt.scalar_type() == at::kInt && cond_off.scalar_type() == at::kInt &&
+                  col.is_contiguous() && opt.is_contiguous() && cond_off.is_contiguous(),
+              "onehot_wgrad: int32 contiguous col / opt / cond_off");
+  fedtgan::OnehotWBatch bt{};
+  bt.n_jobs = (int)dy.size();
+  bt.B = (int)dy[0].size(0);
+  TORCH_CHECK(col.numel() >= bt.B && opt.numel() >= bt.B, "onehot_wgrad: col / opt rows");
+  for (size_t j = 0; j < dy.size(); ++j) {
+    check_f32_2d(dy[j], "dy");
+    check_f32_2d(w[j], "w");
+    TORCH_CHECK(dy[j].size(0) == bt.B && dy[j].size(1) == w[j].size(1), "onehot_wgrad: shapes");
+    bt.jobs[j] = fedtgan::OnehotWJob{cfp(dy[j]), fp(w[j]), (int)ld_of(dy[j]), (int)ld_of(w[j]), (int)w[j].size(1)};
+  }
+  bt.col = col.data_ptr<int>();
+  bt.opt = opt.data_ptr<int>();
+  bt.cond_off = cond_off.data_ptr<int>();
+  fedtgan::launch_onehot_wgrad(bt, (int)zero, cur_stream());
+}
+
 void d_head(const Tensor& d, const Tensor& ms, const Tensor& v, const Tensor& e, const Tensor& coef,
             const Tensor& wloss, const Tensor& y, const Tensor& a, const Tensor& loss) {
   check_f32_2d(d, "d");
@@ -1014,7 +1036,7 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     return prev;
   }
   if (key == "act_row_mode") {
-    TORCH_CHECK(value == 0 || value == 1, "act_row_mode: 0 or 1");
+    TORCH_CHECK(value >= 0 && value <= 2, "act_row_mode: 0 per-wave, 1 row (LDS image), 2 row (registers; forward)");
     const int prev = fedtgan::g_act_row_mode;
     fedtgan::g_act_row_mode = (int)value;
     return prev;
@@ -1052,6 +1074,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gemm_pairs = value ? 1 : 0;
     return prev;
   }
+  if (key == "gemm_pair_max_wg") {   // pairs with more workgroups than this launch as two GEMMs (0: no limit)
+    TORCH_CHECK(value >= 0, "gemm_pair_max_wg: >= 0");
+    const int64_t prev = fedtgan::g_gemm_pair_max_wg;
+    fedtgan::g_gemm_pair_max_wg = (int)value;
+    return prev;
+  }
   if (key == "gemm_xcd_remap") {
     const int64_t prev = fedtgan::g_gemm_xcd_remap;
     TORCH_CHECK(value >= 0 && value <= 2, "gemm_xcd_remap: 0 off, 1 long-K tiles, 2 always");
@@ -1086,6 +1114,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor elem, Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");
   m.def("slerp(Tensor real, Tensor fake, Tensor(a!) out, int seed, Tensor rng_ctr, int stream) -> ()");
   m.def("gp_scale(Tensor g, Tensor(a!) out, float lam, Tensor(b!) loss) -> ()");
+  m.def("onehot_wgrad(Tensor[] dy, Tensor(a!)[] w, Tensor col, Tensor opt, Tensor cond_off, int zero) -> ()");
   m.def(
       "d_head(Tensor d, Tensor ms, Tensor v, Tensor e, Tensor coef, Tensor wloss, Tensor(a!) y, Tensor(b!) a, "
       "Tensor(c!) loss) -> ()");
@@ -1149,6 +1178,7 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("act_bwd_ce", &act_bwd_ce);
   m.impl("slerp", &slerp);
   m.impl("gp_scale", &gp_scale);
+  m.impl("onehot_wgrad", &onehot_wgrad);
   m.impl("d_head", &d_head);
   m.impl("colsum", &colsum);
   m.impl("colsum_ex", &colsum_ex);

@@ -243,9 +243,26 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
 #endif
   const float* src = a.data + (size_t)row * a.Dd;
   float* dst = a.xr + (size_t)b * a.ldx;
+  // the row copy: CP loads in flight per lane before their stores (a plain strided loop waits one memory
+  // round trip per 64 columns -- the compiler cannot move a load of `src` above a store to `dst`); the
+  // one-hot block is stored while the first loads are in flight
+  constexpr int CP = 8;
+  float v[CP];
+#pragma unroll
+  for (int u = 0; u < CP; ++u) v[u] = src[min(lane + 64 * u, a.Dd - 1)];
   const int phot = a.cond_off[pc] + po;
   for (int i = lane; i < a.C; i += 64) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
-  for (int i = lane; i < a.Dd; i += 64) dst[i] = src[i];
+  for (int i0 = 0; i0 < a.Dd; i0 += 64 * CP) {
+    float nx[CP];
+    const int n0 = i0 + 64 * CP;
+#pragma unroll
+    for (int u = 0; u < CP; ++u) nx[u] = n0 < a.Dd ? src[min(n0 + lane + 64 * u, a.Dd - 1)] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CP; ++u)
+      if (i0 + lane + 64 * u < a.Dd) dst[i0 + lane + 64 * u] = v[u];
+#pragma unroll
+    for (int u = 0; u < CP; ++u) v[u] = nx[u];
+  }
 }
 
 void launch_sample(const SampleArgs& a0, hipStream_t stream) {
@@ -285,7 +302,7 @@ __device__ __forceinline__ void slerp_weights(float saa, float sbb, float sab, f
   }
 }
 
-int g_act_row_mode = 1;   // wide rows: one 512-thread workgroup per row (set_tuning("act_row_mode"))
+int g_act_row_mode = 2;   // wide rows: one 512-thread workgroup per row, register-resident (2) or LDS row image (1)
 constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
 constexpr int ACT_PF = 8;      // logits prefetched per lane (rows up to 512 wide)
 constexpr int ACT_PFS = 12;    // slerp real-row values prefetched per lane (rows up to 768 wide)
@@ -635,6 +652,166 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
   for (int j = tid; j < sl.cols; j += blockDim.x) o[j] = wa * a[j] + wb * (j < D ? v[j] : y[j]);
 }
 
+// ---- wide rows, register-resident (act_row_mode 2): the same element -> (wave, lane, Philox word) map as
+// activate_row_kernel, but every element a lane owns (GPW groups of 4 blocks) stays in its registers across
+// the three passes, and the span map and the slerp's real row are requested with the logits in ONE burst.
+// The LDS-image kernel above pays a global round trip per pass and loop trip (the span map re-read from L2
+// in the exp and normalise passes, the real row twice in the slerp): ~100 us for the wide table's 1,000 rows
+// of 7,018 columns, where the bytes take ~25 us.  LDS holds only the span statistics, so more rows fit a CU.
+template <int GPW, bool BT_ = false>
+__global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const float* __restrict__ logits, int ldl,
+                                                                         float* __restrict__ out, int ldo, int rows,
+                                                                         SpanTables sp, float inv_tau, uint64_t seed,
+                                                                         const uint64_t* ctr, uint32_t stream_id,
+                                                                         SlerpFuse sl, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  extern __shared__ float act_smem[];
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    logits = cptr(logits, co);
+    out = cptr(out, co);
+    ctr = cptr(ctr, co);
+    client_off(sp, co);
+    client_off(sl, co);
+    seed += (uint64_t)bi_.z * cb.seed_step;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = bi_.x;
+  const int D = sp.dim, S = sp.n_span;
+  const float* x = logits + (size_t)r * ldl;
+  const int* einfo = sp.packed;
+  uint32_t* smax = reinterpret_cast<uint32_t*>(act_smem);
+  float* ssum = act_smem + S;
+  float* red = act_smem + 2 * S;   // [ROW_WAVES * 3] slerp partial sums
+  float* y = out + (size_t)r * ldo;
+  const bool do_sl = sl.real != nullptr && r < sl.rows;   // (uniform over the workgroup)
+  const float* a = do_sl ? sl.real + (size_t)r * sl.ld : x;
+  float xv[GPW][4], ar[GPW][4];
+  int ic[GPW][4];
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = min((4 * (wv + ROW_WAVES * g) + q) * 64 + lane, D - 1);
+      xv[g][q] = x[j];
+      ic[g][q] = einfo[j];
+      ar[g][q] = a[j];
+    }
+  for (int s2 = tid; s2 < S; s2 += blockDim.x) {
+    smax[s2] = 0u;
+    ssum[s2] = 0.f;
+  }
+  const uint64_t step = ctr ? *ctr : 0ull;
+  RngArgs rng{seed, ctr, stream_id};
+  const uint64_t base = (uint64_t)r << 20;
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < GPW; ++g) {
+    const int gi = wv + ROW_WAVES * g;
+    if (4 * gi * 64 >= D) break;   // (uniform over the wave)
+    const uint4 u4 = rng4(rng, step, base + (uint64_t)gi * 64u + (uint64_t)lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (4 * gi + q) * 64 + lane;
+      if (j >= D) break;
+      const uint32_t u = q == 0 ? u4.x : q == 1 ? u4.y : q == 2 ? u4.z : u4.w;
+      if (!(ic[g][q] & EI_SOFTMAX)) {
+        const float th = tanhf(xv[g][q]);
+        y[j] = th;
+        xv[g][q] = th;
+      } else {
+        const float gv = (xv[g][q] + gumbel(u)) * inv_tau;
+        xv[g][q] = gv;
+        atomicMax(&smax[ic[g][q] & (EI_SOFTMAX - 1)], f2ord(gv));
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      if (j < D && (ic[g][q] & EI_SOFTMAX)) {
+        const int s2 = ic[g][q] & (EI_SOFTMAX - 1);
+        const float e = __expf(xv[g][q] - ord2f(smax[s2]));
+        xv[g][q] = e;
+        atomicAdd(&ssum[s2], e);
+      }
+    }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      if (j < D && (ic[g][q] & EI_SOFTMAX)) {
+        const float o = xv[g][q] / ssum[ic[g][q] & (EI_SOFTMAX - 1)];
+        y[j] = o;
+        xv[g][q] = o;
+      }
+    }
+  if (!do_sl) return;
+  // fused slerp(real_r, fake_r): the fake row is this row's activation (registers, j < D) followed by its
+  // condition columns (global, written by the sampler)
+  float saa = 0.f, sbb = 0.f, sab = 0.f;
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      if (j < D) {
+        saa += ar[g][q] * ar[g][q];
+        sbb += xv[g][q] * xv[g][q];
+        sab += ar[g][q] * xv[g][q];
+      }
+    }
+  constexpr int TU = 4;   // tail loads in flight per thread
+  for (int j0 = D; j0 < sl.cols; j0 += TU * ROW_WAVES * 64) {
+    float ra[TU], fb[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int j = min(j0 + u * ROW_WAVES * 64 + tid, sl.cols - 1);
+      ra[u] = a[j];
+      fb[u] = y[j];
+    }
+#pragma unroll
+    for (int u = 0; u < TU; ++u)
+      if (j0 + u * ROW_WAVES * 64 + tid < sl.cols) {
+        saa += ra[u] * ra[u];
+        sbb += fb[u] * fb[u];
+        sab += ra[u] * fb[u];
+      }
+  }
+  const float3 tot = block_sum3(saa, sbb, sab, red);
+  RngArgs srng{seed, ctr, sl.stream};
+  const float alpha = u01(rng4(srng, step, (uint64_t)r).x);
+  float wa, wb;
+  slerp_weights(tot.x, tot.y, tot.z, alpha, wa, wb);
+  float* o = sl.out + (size_t)r * sl.ld;
+#pragma unroll
+  for (int g = 0; g < GPW; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      if (j < D) o[j] = wa * ar[g][q] + wb * xv[g][q];
+    }
+  for (int j0 = D; j0 < sl.cols; j0 += TU * ROW_WAVES * 64) {
+    float ra[TU], fb[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int j = min(j0 + u * ROW_WAVES * 64 + tid, sl.cols - 1);
+      ra[u] = a[j];
+      fb[u] = y[j];
+    }
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int j = j0 + u * ROW_WAVES * 64 + tid;
+      if (j < sl.cols) o[j] = wa * ra[u] + wb * fb[u];
+    }
+  }
+}
+
 template <bool BT_ = false>
 __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const float* __restrict__ dact, int ldd,
                                                                         const float* __restrict__ act, int lda,
@@ -752,6 +929,113 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
   }
 }
 
+// ---- register-resident backward (act_row_mode 2): a thread keeps its E elements (j = tid + 512 e) of the
+// upstream gradient, the activation and the span map in registers from ONE burst of loads; the conditioned
+// span's logits are read straight from global memory by one wave (a few dozen values, L2-resident).  The LDS
+// kernel above stages the whole span table (D + 4S words, 44 KB on the wide table) per row and reads g / y twice.
+template <int E, bool BT_ = false>
+__global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_rowreg_kernel(const float* __restrict__ dact, int ldd,
+                                                                           const float* __restrict__ act, int lda,
+                                                                           const float* __restrict__ logits, int ldl,
+                                                                           SpanTables sp, const int* __restrict__ col,
+                                                                           const int* __restrict__ opt,
+                                                                           float* __restrict__ dl, int ldg, int rows,
+                                                                           float inv_tau, float* loss, int loss_per_row,
+                                                                           ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  extern __shared__ float act_smem[];
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    dact = cptr(dact, co);
+    act = cptr(act, co);
+    logits = cptr(logits, co);
+    col = cptr(col, co);
+    opt = cptr(opt, co);
+    dl = cptr(dl, co);
+    loss = cptr(loss, co);
+    client_off(sp, co);
+  }
+  constexpr int NTH = ROW_WAVES * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = bi_.x;
+  const int D = sp.dim, S = sp.n_span;
+  const float* g = dact + (size_t)r * ldd;
+  const float* y = act + (size_t)r * lda;
+  const float* x = logits + (size_t)r * ldl;
+  const int* einfo = sp.packed;
+  const int* kind = einfo + D;
+  const int* start = kind + S;
+  const int* width = start + S;
+  const int* cidx = width + S;
+  float gc[E], yc[E];
+  int ic[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = min(tid + NTH * e, D - 1);
+    gc[e] = g[j];
+    yc[e] = y[j];
+    ic[e] = einfo[j];
+  }
+  const int cr = col[r];
+  const int orow = opt[r];
+  float* stat = act_smem;                                   // [S] per-span sum of g*y
+  int* cspan = reinterpret_cast<int*>(stat + S);            // the conditioned span
+  float* lse_sh = stat + S + 1;
+  for (int s2 = tid; s2 < S; s2 += NTH) stat[s2] = 0.f;
+  if (tid == 0) *cspan = -1;
+  __syncthreads();
+  for (int s2 = tid; s2 < S; s2 += NTH)
+    if (kind[s2] != 0 && cidx[s2] == cr) *cspan = s2;       // exactly one span matches
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (tid + NTH * e < D && (ic[e] & EI_SOFTMAX)) atomicAdd(&stat[ic[e] & (EI_SOFTMAX - 1)], gc[e] * yc[e]);
+  __syncthreads();
+  const int cs = *cspan;
+  int cst = 0, cw = 0;
+  if (cs >= 0) {
+    cst = start[cs];
+    cw = width[cs];
+  }
+  if (wv == 0) {   // log-sum-exp over the conditioned span (one wave, logits from L2)
+    float lse = 0.f;
+    if (cs >= 0) {
+      float m = -INFINITY;
+      for (int i = lane; i < cw; i += 64) m = fmaxf(m, x[cst + i]);
+      m = wave_max(m);
+      float sm = 0.f;
+      for (int i = lane; i < cw; i += 64) sm += __expf(x[cst + i] - m);
+      sm = wave_sum(sm);
+      lse = m + __logf(sm);
+      if (lane == 0) {
+        const float term = (lse - x[cst + min(orow, cw - 1)]) / (float)rows;
+        if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+      }
+    } else if (lane == 0 && loss_per_row) {
+      loss[r] = 0.f;
+    }
+    if (lane == 0) *lse_sh = lse;
+  }
+  __syncthreads();
+  const float lse = *lse_sh;
+  const int ot = cst + min(orow, max(cw - 1, 0));
+  const float invB = 1.f / (float)rows;
+  float* d = dl + (size_t)r * ldg;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = tid + NTH * e;
+    if (j < D) {
+      float vv;
+      if (!(ic[e] & EI_SOFTMAX)) {
+        vv = gc[e] * (1.f - yc[e] * yc[e]);
+      } else {
+        vv = yc[e] * (gc[e] - stat[ic[e] & (EI_SOFTMAX - 1)]) * inv_tau;
+        if (j >= cst && j < cst + cw) vv += (__expf(x[j] - lse) - (j == ot ? 1.f : 0.f)) * invB;
+      }
+      d[j] = vv;
+    }
+  }
+}
+
 // LDS of the row kernels: tables + one row image [D + 2S] + ROW_WAVES * 3 reduction slots
 static size_t act_row_smem_bytes(const SpanTables& sp) {
   return (size_t)span_packed_len(sp.dim, sp.n_span) * sizeof(int) +
@@ -789,6 +1073,26 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
   if (cb.k > 1) {
     check_slabs("activate operand", logits, out, ctr, sl.real, sl.out);
     check_slab(sp);
+  }
+  if (act_row_mode(sp) && g_act_row_mode == 2) {
+    // register-resident row kernel: GPW groups of 4 x 64 columns per wave
+    const int ng = ((sp.dim + 63) / 64 + 3) / 4, gpw = (ng + ROW_WAVES - 1) / ROW_WAVES;
+    const size_t lds = (size_t)(2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
+    const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
+    const bool xcd = cb.xcd != 0;
+#define FEDTGAN_ACT_REG(G)                                                                                          \
+  do {                                                                                                             \
+    allow_big_lds(activate_rowreg_kernel<G, false>, lds);                                                          \
+    allow_big_lds(activate_rowreg_kernel<G, true>, lds);                                                           \
+    hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, true> : activate_rowreg_kernel<G, false>), grid, block, lds, \
+                       stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);          \
+    return;                                                                                                        \
+  } while (0)
+    if (gpw <= 2) FEDTGAN_ACT_REG(2);
+    if (gpw <= 4) FEDTGAN_ACT_REG(4);
+    if (gpw <= 8) FEDTGAN_ACT_REG(8);
+#undef FEDTGAN_ACT_REG
+    // (wider rows: the LDS-image row kernel)
   }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_fwd_smem_bytes(sp);
@@ -955,6 +1259,25 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
   if (cb.k > 1) {
     check_slabs("act_bwd_ce operand", dact, act, logits, col, opt, dlogits, loss);
     check_slab(sp);
+  }
+  if (act_row_mode(sp) && g_act_row_mode == 2) {
+    const int ept = (sp.dim + ROW_WAVES * 64 - 1) / (ROW_WAVES * 64);   // elements per thread
+    const size_t lds = (size_t)(sp.n_span + 2) * sizeof(float);
+    const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
+    const bool xcd = cb.xcd != 0;
+#define FEDTGAN_BWD_REG(E)                                                                                             \
+  do {                                                                                                                \
+    allow_big_lds(act_bwd_ce_rowreg_kernel<E, false>, lds);                                                           \
+    allow_big_lds(act_bwd_ce_rowreg_kernel<E, true>, lds);                                                            \
+    hipLaunchKernelGGL((xcd ? act_bwd_ce_rowreg_kernel<E, true> : act_bwd_ce_rowreg_kernel<E, false>), grid, block, lds, \
+                       stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss,      \
+                       loss_per_row, cb);                                                                             \
+    return;                                                                                                           \
+  } while (0)
+    if (ept <= 8) FEDTGAN_BWD_REG(8);
+    if (ept <= 16) FEDTGAN_BWD_REG(16);
+    if (ept <= 32) FEDTGAN_BWD_REG(32);
+#undef FEDTGAN_BWD_REG
   }
   if (act_row_mode(sp)) {
     const size_t lds = act_row_smem_bytes(sp);
@@ -1153,6 +1476,89 @@ void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int
   else
     hipLaunchKernelGGL((client_batch().xcd ? gp_scale_kernel<true> : gp_scale_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
+}
+
+// ============================================================================ one-hot block weight gradient
+// Workgroup (r, job): the batch's condition indices are staged in LDS; the workgroup of the FIRST row holding
+// index k sums every row with index k in batch order and writes block row k (later rows with the same index
+// exit).  With zero != 0 every workgroup clears its row's block row (duplicates store the same zeros).
+// The wide table's G.out weight gradient is [7,402 x 7,018] of which the condition block is 6,762 rows: a dense
+// GEMM multiplies 500 one-hot rows through it (52 GFLOP, 190 MB of mostly-zero output per step); here at most
+// 500 rows of 7,018 floats are written and cleared.
+template <bool BT_ = false>
+__global__ __launch_bounds__(256) void onehot_wgrad_kernel(OnehotWBatch bt, int zero, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  extern __shared__ int oh_smem[];
+  OnehotWJob jb = bt.jobs[bi_.y];
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    jb.dy = cptr(jb.dy, co);
+    jb.w = cptr(jb.w, co);
+    bt.col = cptr(bt.col, co);
+    bt.opt = cptr(bt.opt, co);
+    bt.cond_off = cptr(bt.cond_off, co);
+  }
+  const int r = bi_.x, B = bt.B, tid = threadIdx.x;
+  const int my = bt.cond_off[bt.col[r]] + bt.opt[r];
+  if (zero) {
+    float* w = jb.w + (size_t)my * jb.ldw;
+    for (int o = tid; o < jb.n; o += 256) w[o] = 0.f;
+    return;
+  }
+  int* idx = oh_smem;            // [B] condition index of every row
+  int* list = oh_smem + B;       // [B] rows holding this workgroup's index, in batch order
+  int* flag = oh_smem + 2 * B;   // [2] an earlier row holds it | list length
+  if (tid == 0) flag[0] = 0;
+  for (int i = tid; i < B; i += 256) idx[i] = bt.cond_off[bt.col[i]] + bt.opt[i];
+  __syncthreads();
+  for (int i = tid; i < r; i += 256)
+    if (idx[i] == my) flag[0] = 1;
+  __syncthreads();
+  if (flag[0]) return;           // (uniform) another workgroup owns this block row
+  if (tid < 64) {                // one wave compacts rows r.. with index `my`, in order
+    int cnt = 0;
+    for (int i0 = r; i0 < B; i0 += 64) {
+      const int i = i0 + tid;
+      const bool hit = i < B && idx[i] == my;
+      const unsigned long long m = __ballot(hit);
+      if (hit) list[cnt + __popcll(m & ((1ull << tid) - 1ull))] = i;
+      cnt += __popcll(m);
+    }
+    if (tid == 0) flag[1] = cnt;
+  }
+  __syncthreads();
+  const int cnt = flag[1];
+  float* w = jb.w + (size_t)my * jb.ldw;
+  constexpr int U = 4;           // independent columns in flight per thread
+  for (int o0 = tid; o0 < jb.n; o0 += 256 * U) {
+    float acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.f;
+    for (int q = 0; q < cnt; ++q) {
+      const float* src = jb.dy + (size_t)list[q] * jb.ldy;
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += src[min(o0 + 256 * u, jb.n - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (o0 + 256 * u < jb.n) w[o0 + 256 * u] = acc[u];
+  }
+}
+
+void launch_onehot_wgrad(const OnehotWBatch& bt0, int zero, hipStream_t stream) {
+  OnehotWBatch bt = bt0;
+  bt.n_jobs = std::min(bt.n_jobs, 4);
+  if (bt.n_jobs <= 0 || bt.B <= 0) return;
+  const ClientBatch cb = client_batch();
+  if (cb.k > 1) {
+    check_slabs("onehot_wgrad operand", bt.col, bt.opt, bt.cond_off);
+    for (int j = 0; j < bt.n_jobs; ++j) check_slabs("onehot_wgrad job", bt.jobs[j].dy, bt.jobs[j].w);
+  }
+  const size_t lds = zero ? 0 : (size_t)(2 * bt.B + 2) * sizeof(int);
+  allow_big_lds(onehot_wgrad_kernel<false>, lds);
+  allow_big_lds(onehot_wgrad_kernel<true>, lds);
+  hipLaunchKernelGGL((cb.xcd ? onehot_wgrad_kernel<true> : onehot_wgrad_kernel<false>), dim3(bt.B, bt.n_jobs, cb.k),
+                     dim3(256), lds, stream, bt, zero, cb);
 }
 
 // one wave per row: y = d.v + e ; a = coef * v * ms ; loss += wloss * y

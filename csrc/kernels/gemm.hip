@@ -1026,6 +1026,7 @@ constexpr int GEMM_MAX_SPLITS = 64;
 int g_gemm_xcd_remap = 1;
 int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
 int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)
+int g_gemm_pair_max_wg = 0;   // pairs whose two grids together exceed this many workgroups launch separately (0: no limit)
 int g_gemm_splitk_inlaunch = 1;   // 1: split-K reduced by the last-arriving slice (GemmArgs::tile_cnt)
 
 // the reduced, epilogue-applied value of output idx = m * N + n (stored to C by the caller)
@@ -1352,7 +1353,9 @@ void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
   const dim3 d1 = gemm_prepare(g1), d2 = gemm_prepare(g2);
   const Grid3 a{(int)d1.x, (int)d1.y, (int)d1.z}, b{(int)d2.x, (int)d2.y, (int)d2.z};
   bool fused = false;
-  if (!g1.f32 && !g2.f32 && !g1.bin && !g2.bin && !g1.c16 && !g2.c16 && g_gemm_pairs) {
+  const int64_t pair_wg = (int64_t)a.x * a.y * a.z + (int64_t)b.x * b.y * b.z;
+  if (!g1.f32 && !g2.f32 && !g1.bin && !g2.bin && !g1.c16 && !g2.c16 && g_gemm_pairs &&
+      (g_gemm_pair_max_wg <= 0 || pair_wg <= g_gemm_pair_max_wg)) {
     if (g1.vec && g2.vec) fused = gemm_pair_vec<true, true>(g1, a, g2, b, stream);
     else if (g1.vec) fused = gemm_pair_vec<true, false>(g1, a, g2, b, stream);
     else if (g2.vec) fused = gemm_pair_vec<false, true>(g1, a, g2, b, stream);

@@ -128,6 +128,7 @@ unsigned check_status_vgm();
 // two independent GEMMs in one launch where the pair is instantiated, else two launches
 void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream);
 extern int g_gemm_pairs;
+extern int g_gemm_pair_max_wg;
 
 struct SampleArgs {
   int B, E, C, Dd, n_col, maxw, n_rows;
@@ -199,6 +200,24 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
 
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
                      int loss_per_row, hipStream_t stream);
+
+// Weight gradient of a one-hot conditional input block (generator layers, input-major weights): row k of the
+// block's gradient is the sum of the upstream-gradient rows whose condition index is k (rows in batch order, so
+// the result is deterministic); every other row stays zero.  zero != 0 clears the rows the batch touched (after
+// the optimizer has read them), restoring the all-zero block for the next step.
+struct OnehotWJob {
+  const float* dy;   // [B, n] upstream gradient rows
+  float* w;          // row k of the block's gradient at w + k * ldw
+  int ldy, ldw, n;
+};
+struct OnehotWBatch {
+  OnehotWJob jobs[4];
+  int n_jobs, B;
+  const int* col;        // [B] conditioned column
+  const int* opt;        // [B] its option
+  const int* cond_off;   // [n_col] first block row of each column
+};
+void launch_onehot_wgrad(const OnehotWBatch& bt, int zero, hipStream_t stream);
 
 void launch_d_head(const float* d, int ldd, const float* ms, int ldms, const float* v, const float* e,
                    const float* coef, const float* wloss, float* y, float* a, int lda, int rows, int cols, float* loss,

@@ -38,7 +38,7 @@ from __future__ import annotations
 
 import contextlib
 import dataclasses
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -133,6 +133,12 @@ class EngineConfig:
     # initial weights drawn from a generator of the engine's own, seeded by the engine seed ("engine": reproducible
     # whatever other threads do), or from torch's process-wide generator ("global", the reference modules' init)
     init_rng: str = "engine"
+    # HIP, one-hot conditions: a generator weight gradient whose condition block (C rows of the input-major
+    # weight x out) has at least this many elements is not a dense GEMM over the one-hot columns: its block rows
+    # are the sums of the batch rows' upstream gradients per condition index (ops.onehot_wgrad; the block stays
+    # zero between steps).  The wide table's G.out gradient: 7,018 x 7,402 dense (228 us) -> 7,018 x 640 + 500
+    # scattered rows.  0 = always dense.
+    onehot_wgrad_min: int = 1 << 20
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -185,6 +191,7 @@ class CTGANEngine:
         self.spans = [(int(s), int(w), int(k)) for s, w, k in zip(layout.start, layout.width, layout.kind)]
         self.cond_spans = [(int(s), int(w)) for s, w in zip(layout.cond_start, layout.cond_width)]
         self.use_onehot = bool(cfg.onehot) and self.C > 0
+        self._oh_pending = None   # one-hot block gradient rows written this step (cleared after the G Adam)
         self._cond_off = self.mem.tensor(np.asarray(layout.cond_offset, dtype=np.int32))
         self._build_params()
         self._build_buffers()
@@ -783,7 +790,7 @@ class CTGANEngine:
     def _g_update(self):
         """D forward on the fake rows, backward through D, activation, cond loss and G; G Adam step."""
         self._g_dlogits()
-        self._g_adam(self._g_backward(fold_colsum=True))
+        self._g_adam(self._g_backward(fold_colsum=True, onehot_w=True))
 
     def _g_dlogits(self):
         """G loss (-mean D(fake) + cond CE) back to the generator's logits: self.dlogits."""
@@ -797,17 +804,42 @@ class CTGANEngine:
         o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,
                      self.opt, self.dlogits, self.ce_rows, self.cfg.tau)
 
-    def _g_backward(self, fold_colsum: bool = False):
+    def _onehot_w_ok(self, W: torch.Tensor) -> bool:
+        """Is the condition block of G weight gradient W (logical [out, in]) a scattered one (onehot_wgrad_min)?"""
+        lim = int(self.cfg.onehot_wgrad_min)
+        return lim > 0 and self.use_onehot and bool(self.cfg.g_wt) and hasattr(self.ops, "onehot_wgrad") and \
+            self.lanes is None and self.C * W.shape[0] >= lim
+
+    def _wgrad_operands(self, a: int, W: torch.Tensor, oh: Optional[list]):
+        """(x, dW) of a generator weight-gradient GEMM over H[:, a:]; with ``oh`` (a list) a large one-hot
+        condition block is left out of the GEMM and queued as an (upstream-gradient slot, block rows) job."""
+        if oh is not None and self._onehot_w_ok(W):
+            kd = self.c_cols[0] - a
+            oh.append(W[:, kd:].t())               # [C, out]: the input-major storage's condition rows
+            return self.H[:, a:self.c_cols[0]], W[:, :kd]
+        return self._kpad(self.H, a, W)
+
+    def _g_backward(self, fold_colsum: bool = False, onehot_w: bool = False):
         """self.dlogits -> G parameter gradients (self.gradG), through the saved forward buffers.
         fold_colsum: return the G.out bias / metrics column-sum jobs for the Adam launch instead of
-        launching them (the gradient is then complete only after _g_adam(jobs))."""
+        launching them (the gradient is then complete only after _g_adam(jobs)).
+        onehot_w: large one-hot condition blocks of the weight gradients by ops.onehot_wgrad (see
+        EngineConfig.onehot_wgrad_min; _g_adam clears their rows again)."""
         o = self.ops
         # generator backward: the dH chain on the main lane, weight gradients on side lanes
         Lg = len(self.gdims)
         pair = self.lanes is None and Lg > 0   # weight gradient + dX product of a layer: one launch
         top = self.off[0]
+        oh_w, oh_dy = ([], []) if onehot_w else (None, None)
+
+        def wgrad(dy, a, W):
+            n0 = len(oh_w) if oh_w is not None else 0
+            x, dW = self._wgrad_operands(a, W, oh_w)
+            if oh_w is not None and len(oh_w) > n0:
+                oh_dy.append(dy)
+            return x, dW
         with self._lane(1):
-            x, dW = self._kpad(self.H, 0, self.g["G.out.W"])
+            x, dW = wgrad(self.dlogits, 0, self.g["G.out.W"])
             o.gemm(self.dlogits, x, dW, ta=True, group=1 if pair else 0)
             if pair:
                 o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top], group=2)
@@ -824,16 +856,20 @@ class CTGANEngine:
             if i > 0:
                 pair = self.lanes is None
                 with self._lane(2 + i % 2):
-                    x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
+                    x, dW = wgrad(self.da[i], a, self.g[f"G.{i}.W"])
                     o.gemm(self.da[i], x, dW, ta=True, group=1 if pair else 0)
                 o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0,
                        group=2 if pair else 0)
             else:
-                x, dW = self._kpad(self.H, a, self.g[f"G.{i}.W"])
+                x, dW = wgrad(self.da[i], a, self.g[f"G.{i}.W"])
                 # held for the Adam launch that follows (fold_colsum: _g_adam(jobs) is next on this stream)
                 fuse = fold_colsum and self.lanes is None and self.cfg.fuse_g_adam and self._adam_fusable(self.nG) and \
                     getattr(o, "gemm_adam", False)
                 o.gemm(self.da[i], x, dW, ta=True, group=3 if fuse else 0)
+        if oh_w:
+            # (issued before a GEMM held for the Adam launch: that launch reads these rows)
+            o.onehot_wgrad(oh_dy, oh_w, self.col, self.opt, self._cond_off)
+            self._oh_pending = (oh_dy, oh_w)
         self._join(1, 2, 3)
         return jobs if fold_colsum else None
 
@@ -846,6 +882,10 @@ class CTGANEngine:
         b1, b2 = self.cfg.betas
         self.ops.adam(self.flatG, self.gradG, self.mG, self.vG, self.stepG, self.cfg.lr, b1, b2, self.cfg.adam_eps,
                       self.cfg.l2scale, last_in_step=True, jobs=jobs)
+        if self._oh_pending is not None:   # the one-hot block rows back to zero for the next step
+            dys, ws = self._oh_pending
+            self.ops.onehot_wgrad(dys, ws, self.col, self.opt, self._cond_off, zero=True)
+            self._oh_pending = None
 
     # ================================================================= split roles (MD-GAN)
     G_BUFFERS = ("H", "abuf", "nhat", "bn_mean", "bn_invstd", "da", "logits", "dlogits", "dH")

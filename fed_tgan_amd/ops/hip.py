@@ -401,6 +401,12 @@ class HipOps:
     def gp_scale(self, g, out, lam, loss_out):
         self.L.gp_scale(g, out, float(lam), loss_out)
 
+    # ------------------------------------------------------------------ one-hot input block weight gradients
+    def onehot_wgrad(self, dys, ws, col, opt, cond_off, zero: bool = False):
+        """ws[j][k] = sum of dys[j] rows r with cond_off[col[r]] + opt[r] == k (batch order); the other rows of
+        ws[j] must be zero and stay untouched.  zero=True clears the rows this batch touched instead."""
+        self.L.onehot_wgrad(list(dys), list(ws), col, opt, cond_off, 1 if zero else 0)
+
     def d_head(self, d_last, ms_last, v, e, coef, wloss, y, a_last, loss_out):
         self.L.d_head(d_last, ms_last, v, e, coef, wloss, y, a_last, loss_out)
 

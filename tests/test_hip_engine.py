@@ -350,3 +350,42 @@ def test_interrupted_hold_does_not_poison_next_step():
     eng.train_steps(8)                  # and graph capture still works
     ld, lg = eng.losses()
     assert np.isfinite(ld) and np.isfinite(lg)
+
+
+def test_onehot_wgrad_matches_dense_gemm():
+    """EngineConfig.onehot_wgrad_min: the generator weight gradients' one-hot condition blocks as scattered
+    rows (ops.onehot_wgrad) train like the dense GEMMs over the one-hot columns (fp32: same gradients up to
+    summation order), and the blocks are all-zero again after every step (the invariant the scatter relies on)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    engs = []
+    for lim in (0, 1):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32", g_wt=True, onehot_wgrad_min=lim),
+                          DEV, backend="hip", seed=12)
+        eng.set_training_data(X)
+        engs.append(eng)
+    a, b = engs
+    b.flat.copy_(a.flat)
+    assert not a._onehot_w_ok(a.g["G.out.W"]) and b._onehot_w_ok(b.g["G.out.W"])
+    for e in engs:
+        e.train_steps(1, use_graph=False)
+    torch.cuda.synchronize()
+    C, c0 = b.C, b.c_cols[0]
+    for i, n in enumerate(("G.out.W", "G.0.W", "G.1.W")):
+        a_ = 0 if n == "G.out.W" else b.off[int(n[2])]
+        kd = c0 - a_
+        assert b.g[n][:, kd:].abs().max().item() == 0.0, n          # cleared after the Adam step
+        assert torch.allclose(b.g[n][:, :kd], a.g[n][:, :kd], atol=1e-6, rtol=1e-4), n
+    lr = a.cfg.lr
+    for n in a.p:
+        assert (a.p[n] - b.p[n]).abs().max() <= 8 * lr + 1e-6, n
+    for e in engs:
+        e.train_steps(8, use_graph=True)
+    torch.cuda.synchronize()
+    for n in ("G.out.W", "G.0.W", "G.1.W", "D.0.W"):
+        assert _rel(b.p[n], a.p[n]) < 2e-2, (n, _rel(b.p[n], a.p[n]))
+    for n in ("G.out.W", "G.0.W", "G.1.W"):
+        a_ = 0 if n == "G.out.W" else b.off[int(n[2])]
+        assert b.g[n][:, c0 - a_:].abs().max().item() == 0.0, n

@@ -633,17 +633,19 @@ def test_adam_with_folded_colsum_matches_two_launches(hip, aux):
     assert torch.allclose(res[1][1][8000:8037], src0.sum(0), atol=1e-4, rtol=1e-5)
 
 
-def test_wide_row_kernels_match_per_wave_kernels(hip):
-    """Rows wider than 512: the one-workgroup-per-row kernels draw the same Philox words as the
-    per-wave kernels, so activation (+ fused slerp) and its backward agree element for element."""
-    spans, cond, D = _wide_spans(D_min=2300, seed=4)
+@pytest.mark.parametrize("d_min", [2300, 7000])
+def test_wide_row_kernels_match_per_wave_kernels(hip, d_min):
+    """Rows wider than 512: the one-workgroup-per-row kernels (LDS row image, and register-resident with 2 or 4
+    groups per wave) draw the same Philox words as the per-wave kernels, so activation (+ fused slerp) and its
+    backward agree element for element."""
+    spans, cond, D = _wide_spans(D_min=d_min, seed=4)
     rows, nc = 600, 45
     Din = D + nc
     logits = mat(rows, D, seed=52) * 2
     real = mat(rows, Din, seed=53)
     cond_cols = mat(rows, nc, seed=54)
     res = []
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         fake = torch.zeros(rows, Din, device=DEV)
         fake[:, D:] = cond_cols
         interp = torch.zeros(rows // 3, Din, device=DEV)
@@ -661,9 +663,10 @@ def test_wide_row_kernels_match_per_wave_kernels(hip):
             torch.ops.fedtgan.set_tuning("act_row_mode", prev)
         torch.cuda.synchronize()
         res.append((fake, interp, d, loss))
-    for name, a, b in zip(("act", "slerp", "dlogits", "ce"), *res):
-        err = (a - b).abs().max().item()
-        assert torch.allclose(a, b, atol=2e-5, rtol=1e-4), (name, err)
+    for other in res[1:]:
+        for name, a, b in zip(("act", "slerp", "dlogits", "ce"), res[0], other):
+            err = (a - b).abs().max().item()
+            assert torch.allclose(a, b, atol=2e-5, rtol=1e-4), (name, err)
 
 
 
@@ -852,3 +855,27 @@ def test_gemm_splitk_inlaunch_matches_epilogue_kernel(hip, hip32, case):
     ref_g = run(False, graph=True)
     for r, o in zip(ref_g, got_g):
         assert torch.equal(r, o)
+
+
+def test_onehot_wgrad_scatter_and_clear(hip):
+    """ops.onehot_wgrad: block row k = sum of the dy rows whose condition index is k (duplicates summed in batch
+    order), the other rows untouched; zero=True clears exactly the touched rows."""
+    B, n, ncol = 500, 301, 7
+    widths = torch.tensor([3, 1, 40, 5, 9, 2, 60])
+    cond_off = torch.cat([torch.zeros(1, dtype=torch.int64), widths.cumsum(0)[:-1]]).to(torch.int32).to(DEV)
+    C = int(widths.sum())
+    g = torch.Generator().manual_seed(3)
+    col = torch.randint(0, ncol, (B,), generator=g)
+    opt = (torch.rand(B, generator=g) * widths[col]).floor().long()
+    col, opt = col.to(torch.int32).to(DEV), opt.to(torch.int32).to(DEV)
+    dy = mat(B, n, seed=120)
+    w = torch.zeros(C + 5, n + 3, device=DEV)[2:C + 2, :n]        # a strided view inside a larger buffer
+    hip.onehot_wgrad([dy], [w], col, opt, cond_off)
+    torch.cuda.synchronize()
+    idx = (cond_off.long()[col.long()] + opt.long())
+    ref = torch.zeros(C, n, dtype=torch.float64, device=DEV).index_add_(0, idx, dy.double())
+    assert torch.allclose(w.double(), ref, atol=1e-5, rtol=1e-5)
+    assert len(torch.unique(idx)) < B          # (duplicates were exercised)
+    hip.onehot_wgrad([dy], [w], col, opt, cond_off, zero=True)
+    torch.cuda.synchronize()
+    assert w.abs().max().item() == 0.0

@@ -11,5 +11,7 @@ done
 cd /tmp
 (cd $R/_basetree && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_base -o run -- python3 bench.py --steps 10 --warmup 3 > $OUT/prof_base.log 2>&1) || exit 1
 (cd $R && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_head -o run -- python3 bench.py --steps 10 --warmup 3 > $OUT/prof_head.log 2>&1) || exit 1
+du -ah $OUT | sort -h | tail -12
 find $OUT -name "*kernel_trace.csv" -delete
+find $OUT -type f -size +4M -delete
 echo done

@@ -50,6 +50,8 @@ def main():
                     help="emulated clients as one batched engine (FedConfig.batched_clients) or one engine per thread")
     ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
                     help="EngineConfig override for A/B runs, e.g. --engine g_wt=1")
+    ap.add_argument("--fed", action="append", default=[], metavar="KEY=VALUE",
+                    help="FedConfig override for A/B runs, e.g. --fed label_encoders_early=0")
     ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
                     help="native set_tuning knob for A/B runs, e.g. --tuning gemm_pairs=0")
     args = ap.parse_args()
@@ -75,6 +77,7 @@ def main():
                     gmm_backend="torch", aggregation=args.aggregation, seed=args.seed,
                     engine=_engine_cfg(EngineConfig(precision=args.precision), args.engine), verbose=True,
                     client_streams=not args.one_stream, batched_clients=args.batched)
+    _engine_cfg(cfg, args.fed)
     t0 = time.time()
     if args.clients == 1:
         rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=dev), dev)
@@ -111,6 +114,8 @@ def main():
         summ["engine_overrides"] = args.engine
     if args.tuning:
         summ["tuning"] = args.tuning
+    if args.fed:
+        summ["fed_overrides"] = args.fed
     print(json.dumps(summ), flush=True)
     if args.json:
         with open(args.json, "a") as f:
