@@ -26,7 +26,8 @@ def _engine_cfg(ecfg, overrides):
     for kv in overrides:
         k, v = kv.split("=", 1)
         cur = getattr(ecfg, k)
-        setattr(ecfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+        setattr(ecfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else
+                v if cur is None else type(cur)(v))
     return ecfg
 
 
