@@ -653,11 +653,12 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
 }
 
 // ---- wide rows, register-resident (act_row_mode 2): the same element -> (wave, lane, Philox word) map as
-// activate_row_kernel, but every element a lane owns (GPW groups of 4 blocks) stays in its registers across
-// the three passes, and the span map and the slerp's real row are requested with the logits in ONE burst.
-// The LDS-image kernel above pays a global round trip per pass and loop trip (the span map re-read from L2
-// in the exp and normalise passes, the real row twice in the slerp): ~100 us for the wide table's 1,000 rows
-// of 7,018 columns, where the bytes take ~25 us.  LDS holds only the span statistics, so more rows fit a CU.
+// activate_row_kernel, but every element a lane owns (GPW groups of 4 blocks) stays in its registers, and the
+// span map and the slerp's real row are requested with the logits in ONE burst.  The per-span max / sum are
+// span-parallel: the perturbed logits go to an LDS row image and each thread folds whole spans of it (spans are
+// contiguous column ranges).  Per-element LDS atomics (the LDS-image kernel above) serialise the lanes of a wave
+// that hit one span: on the wide table (7,018 columns, spans ~17 wide) the LDS pipe was busy ~40 us per CU per
+// launch (rocprofv3 SQ_LDS_IDX_ACTIVE, profiles/wide_pmc_r4.txt).
 template <int GPW, bool BT_ = false>
 __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const float* __restrict__ logits, int ldl,
                                                                          float* __restrict__ out, int ldo, int rows,
@@ -675,14 +676,19 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
     client_off(sl, co);
     seed += (uint64_t)bi_.z * cb.seed_step;
   }
+  constexpr int NTH = ROW_WAVES * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = bi_.x;
   const int D = sp.dim, S = sp.n_span;
   const float* x = logits + (size_t)r * ldl;
   const int* einfo = sp.packed;
-  uint32_t* smax = reinterpret_cast<uint32_t*>(act_smem);
-  float* ssum = act_smem + S;
-  float* red = act_smem + 2 * S;   // [ROW_WAVES * 3] slerp partial sums
+  const int* kind = einfo + D;
+  const int* start = kind + S;
+  const int* width = start + S;
+  float* vs = act_smem;          // [D] perturbed logits (softmax elements)
+  float* smax = vs + D;          // [S] span max, then 1 / span sum
+  float* ssum = smax + S;        // [S]
+  float* red = ssum + S;         // [ROW_WAVES * 3] slerp partial sums
   float* y = out + (size_t)r * ldo;
   const bool do_sl = sl.real != nullptr && r < sl.rows;   // (uniform over the workgroup)
   const float* a = do_sl ? sl.real + (size_t)r * sl.ld : x;
@@ -697,14 +703,9 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
       ic[g][q] = einfo[j];
       ar[g][q] = a[j];
     }
-  for (int s2 = tid; s2 < S; s2 += blockDim.x) {
-    smax[s2] = 0u;
-    ssum[s2] = 0.f;
-  }
   const uint64_t step = ctr ? *ctr : 0ull;
   RngArgs rng{seed, ctr, stream_id};
   const uint64_t base = (uint64_t)r << 20;
-  __syncthreads();
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
     const int gi = wv + ROW_WAVES * g;
@@ -722,9 +723,29 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
       } else {
         const float gv = (xv[g][q] + gumbel(u)) * inv_tau;
         xv[g][q] = gv;
-        atomicMax(&smax[ic[g][q] & (EI_SOFTMAX - 1)], f2ord(gv));
+        vs[j] = gv;
       }
     }
+  }
+  __syncthreads();
+  // span-parallel statistics: max, then sum of exp(v - max); spans of one thread are independent loops
+  for (int s2 = tid; s2 < S; s2 += NTH) {
+    if (kind[s2] == 0) continue;
+    const int st = start[s2], w = width[s2];
+    const float* v = vs + st;
+    float m = -INFINITY;
+    int i = 0;
+    for (; i + 4 <= w; i += 4) m = fmaxf(fmaxf(m, fmaxf(v[i], v[i + 1])), fmaxf(v[i + 2], v[i + 3]));
+    for (; i < w; ++i) m = fmaxf(m, v[i]);
+    float e0 = 0.f, e1 = 0.f;
+    i = 0;
+    for (; i + 2 <= w; i += 2) {
+      e0 += __expf(v[i] - m);
+      e1 += __expf(v[i + 1] - m);
+    }
+    if (i < w) e0 += __expf(v[i] - m);
+    smax[s2] = m;
+    ssum[s2] = 1.f / (e0 + e1);
   }
   __syncthreads();
 #pragma unroll
@@ -734,19 +755,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
       const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
       if (j < D && (ic[g][q] & EI_SOFTMAX)) {
         const int s2 = ic[g][q] & (EI_SOFTMAX - 1);
-        const float e = __expf(xv[g][q] - ord2f(smax[s2]));
-        xv[g][q] = e;
-        atomicAdd(&ssum[s2], e);
-      }
-    }
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < GPW; ++g)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
-      if (j < D && (ic[g][q] & EI_SOFTMAX)) {
-        const float o = xv[g][q] / ssum[ic[g][q] & (EI_SOFTMAX - 1)];
+        const float o = __expf(xv[g][q] - smax[s2]) * ssum[s2];
         y[j] = o;
         xv[g][q] = o;
       }
@@ -767,17 +776,17 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
       }
     }
   constexpr int TU = 4;   // tail loads in flight per thread
-  for (int j0 = D; j0 < sl.cols; j0 += TU * ROW_WAVES * 64) {
+  for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
     float ra[TU], fb[TU];
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
-      const int j = min(j0 + u * ROW_WAVES * 64 + tid, sl.cols - 1);
+      const int j = min(j0 + u * NTH + tid, sl.cols - 1);
       ra[u] = a[j];
       fb[u] = y[j];
     }
 #pragma unroll
     for (int u = 0; u < TU; ++u)
-      if (j0 + u * ROW_WAVES * 64 + tid < sl.cols) {
+      if (j0 + u * NTH + tid < sl.cols) {
         saa += ra[u] * ra[u];
         sbb += fb[u] * fb[u];
         sab += ra[u] * fb[u];
@@ -796,17 +805,17 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
       const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
       if (j < D) o[j] = wa * ar[g][q] + wb * xv[g][q];
     }
-  for (int j0 = D; j0 < sl.cols; j0 += TU * ROW_WAVES * 64) {
+  for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
     float ra[TU], fb[TU];
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
-      const int j = min(j0 + u * ROW_WAVES * 64 + tid, sl.cols - 1);
+      const int j = min(j0 + u * NTH + tid, sl.cols - 1);
       ra[u] = a[j];
       fb[u] = y[j];
     }
 #pragma unroll
     for (int u = 0; u < TU; ++u) {
-      const int j = j0 + u * ROW_WAVES * 64 + tid;
+      const int j = j0 + u * NTH + tid;
       if (j < sl.cols) o[j] = wa * ra[u] + wb * fb[u];
     }
   }
@@ -978,17 +987,30 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_rowreg_kernel(const
   }
   const int cr = col[r];
   const int orow = opt[r];
-  float* stat = act_smem;                                   // [S] per-span sum of g*y
+  float* gy = act_smem;                                     // [D] g*y of the softmax elements
+  float* stat = gy + D;                                     // [S] per-span sum of g*y
   int* cspan = reinterpret_cast<int*>(stat + S);            // the conditioned span
   float* lse_sh = stat + S + 1;
-  for (int s2 = tid; s2 < S; s2 += NTH) stat[s2] = 0.f;
   if (tid == 0) *cspan = -1;
-  __syncthreads();
-  for (int s2 = tid; s2 < S; s2 += NTH)
-    if (kind[s2] != 0 && cidx[s2] == cr) *cspan = s2;       // exactly one span matches
 #pragma unroll
   for (int e = 0; e < E; ++e)
-    if (tid + NTH * e < D && (ic[e] & EI_SOFTMAX)) atomicAdd(&stat[ic[e] & (EI_SOFTMAX - 1)], gc[e] * yc[e]);
+    if (tid + NTH * e < D && (ic[e] & EI_SOFTMAX)) gy[tid + NTH * e] = gc[e] * yc[e];
+  __syncthreads();
+  // span-parallel sums (no per-element LDS atomics, see activate_rowreg_kernel)
+  for (int s2 = tid; s2 < S; s2 += NTH) {
+    if (kind[s2] == 0) continue;
+    if (cidx[s2] == cr) *cspan = s2;                        // exactly one span matches
+    const float* v = gy + start[s2];
+    const int w = width[s2];
+    float t0 = 0.f, t1 = 0.f;
+    int i = 0;
+    for (; i + 2 <= w; i += 2) {
+      t0 += v[i];
+      t1 += v[i + 1];
+    }
+    if (i < w) t0 += v[i];
+    stat[s2] = t0 + t1;
+  }
   __syncthreads();
   const int cs = *cspan;
   int cst = 0, cw = 0;
@@ -1077,7 +1099,7 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
   if (act_row_mode(sp) && g_act_row_mode == 2) {
     // register-resident row kernel: GPW groups of 4 x 64 columns per wave
     const int ng = ((sp.dim + 63) / 64 + 3) / 4, gpw = (ng + ROW_WAVES - 1) / ROW_WAVES;
-    const size_t lds = (size_t)(2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
+    const size_t lds = (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
     const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
     const bool xcd = cb.xcd != 0;
 #define FEDTGAN_ACT_REG(G)                                                                                          \
@@ -1262,7 +1284,7 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
   }
   if (act_row_mode(sp) && g_act_row_mode == 2) {
     const int ept = (sp.dim + ROW_WAVES * 64 - 1) / (ROW_WAVES * 64);   // elements per thread
-    const size_t lds = (size_t)(sp.n_span + 2) * sizeof(float);
+    const size_t lds = (size_t)(sp.dim + sp.n_span + 2) * sizeof(float);
     const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
     const bool xcd = cb.xcd != 0;
 #define FEDTGAN_BWD_REG(E)                                                                                             \
