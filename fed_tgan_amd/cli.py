@@ -93,6 +93,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="write each epoch CSV inside its round (reference timing) instead of in the background")
     p.add_argument("-init", type=str, default="independent", choices=["independent", "broadcast"],
                    help="initial G/D weights: each client its own random init (reference) or client 0's on every rank")
+    p.add_argument("-batched_clients", default="auto", choices=["auto", "on", "off"],
+                   help="-local_clients K: the K clients as one batched launch sequence (on) or one engine and HIP "
+                        "stream per client thread (off; what auto picks, see FedConfig.batched_clients)")
     p.add_argument("-quiet", action="store_true")
     return p
 
@@ -124,7 +127,8 @@ def fed_config_from_args(args):
                      metrics_log=args.metrics_log, drop_client_prob=args.drop_client_prob, mode=args.mode,
                      e_interval=args.E_interval, grad_flow=args.grad_flow, profile_dir=args.profile_dir,
                      heartbeat_s=args.heartbeat,
-                     dump_real=args.dump_real, async_csv=not args.sync_csv, init=args.init)
+                     dump_real=args.dump_real, async_csv=not args.sync_csv, init=args.init,
+                     batched_clients=args.batched_clients)
 
 
 def pick_device(rank: int, colocated: bool, backend: str, mode: str = "fedavg") -> torch.device:

@@ -117,14 +117,16 @@ class FedConfig:
     train_sync: bool = True
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
-    # several clients on one GPU (in-process emulation): "auto" runs their training steps as ONE batched
-    # launch sequence (models/batched.py) when they allow it (HIP backend, equal row counts, no fault
-    # injection) and there are at most batched_max_auto of them; "on" always when allowed; "off" keeps one
-    # engine, stream and step graph per client thread.  Measured round times, 40k-row Intrusion clients
-    # (profiles/batched_r3.md): 2 clients 23.9 ms batched vs 27.2 ms threads, 4 clients 35.3 vs 35.7,
-    # 8 clients 58.4 vs 48.8 -- the batched kernels are throughput-bound at 8 clients' work
+    # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
+    # sequence (models/batched.py) when they allow it (HIP backend, no fault injection); "off" keeps one engine,
+    # stream and step graph per client thread; "auto" batches up to batched_max_auto clients.  Round 4 made the
+    # thread path's aggregation event-ordered (no device sync), so client threads start the next epoch while the
+    # federator samples and writes: 12-epoch runs, 40k-row Intrusion clients, sum of rounds 1-11
+    # (profiles/multiclient_r4.txt): 2 clients 337 ms batched vs 311 ms threads, 4 clients 416 vs 325, 8 clients
+    # 609 vs 525 -- the threads are faster at every K (with 3-4x the round-to-round variance), so "auto" keeps
+    # them (batched_max_auto = 1); the batched engine stays available ("on": one arena, lower variance).
     batched_clients: str = "auto"
-    batched_max_auto: int = 4
+    batched_max_auto: int = 1
     batched_arena_mb: float = 0.0           # per-client arena slab of the batched engine (0: estimated)
     # write models/label_encoders_{name}.pickle during initialisation (a helper process, as the reference writes it
     # there) instead of after the last round
@@ -685,22 +687,31 @@ class FedRuntime:
         t0 = time.time()
         self._round_start[epoch] = t0
         alive = round_alive_mask(self.cfg, epoch, c.n_clients)
+        h0 = time.perf_counter()
+        hw = hi = 0.0
         with self.timer.phase("train", self.device):
             if getattr(self, "batched", False):
                 # every client's epoch in one batched launch sequence, issued by the process' thread 0 (host
                 # barriers over the process' threads only; the device work is on thread 0's stream)
                 c.g.wait()
+                hw = time.perf_counter()
                 if self._local_t == 0:
                     self.batch_clients.train_epoch(self.cfg.use_graph)
                     if self.gradflow is not None:
                         self.gradflow.update(self.engine)
+                hi = time.perf_counter()
                 c.g.wait()
             elif self.is_client and alive[c.client_index]:
+                hw = time.perf_counter()
                 self.engine.train_epoch(self.cfg.use_graph)
+                hi = time.perf_counter()
                 if self.gradflow is not None:
                     self.gradflow.update(self.engine)
             if self.cfg.train_sync and self.device.type == "cuda":
                 stream_sync(self.device)
+        # host-side seconds of the train phase: waiting at the entry barrier, issuing the epoch, until its end
+        self._host_train = {"h_wait": (hw - h0) if hw else 0.0, "h_issue": (hi - hw) if hi else 0.0,
+                            "h_total": time.perf_counter() - h0}
         self._epoch_done = epoch + 1
         with self.timer.phase("aggregate", self.device):
             # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
@@ -752,7 +763,8 @@ class FedRuntime:
     def fit(self):
         cfg = self.cfg
         for ep in range(self.start_epoch, cfg.epochs):
-            if cfg.profile_dir and ep == cfg.profile_epoch:
+            # (one profiler per process: in a threaded emulation only the federator's thread profiles)
+            if cfg.profile_dir and ep == cfg.profile_epoch and (self.is_fed or getattr(self.comm, "g", None) is None):
                 dt = self._profiled_round(ep)
             else:
                 dt = self.run_round(ep)
@@ -767,7 +779,7 @@ class FedRuntime:
                 _log(cfg, self.rank, f"EPOCH {ep}: loss_d:{ld:>6.2f}   loss_g:{lg:>6.2f}   round time: {dt:.3f} sec")
                 if self.metrics is not None:
                     self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,
-                                        **self.timer.last()})
+                                        **self.timer.last(), **getattr(self, "_host_train", {})})
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
                 self.flush_writes()      # the checkpoint's per-round stamps include every CSV so far
                 self.save_checkpoint(ep + 1)

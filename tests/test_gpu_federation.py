@@ -176,7 +176,7 @@ def test_gpu_emulated_clients_batched(tmp_path):
     holding the same aggregate, and the federator writes every epoch table."""
     from fed_tgan_amd.ops import native
     native.require()
-    rt = run_local_emulation(_cfg(tmp_path, epochs=3), 3, backend="hip", device=DEV)
+    rt = run_local_emulation(_cfg(tmp_path, epochs=3, batched_clients="on"), 3, backend="hip", device=DEV)
     assert rt.batched and rt.engine.batch is not None
     b = rt.batch_clients
     torch.cuda.synchronize()
@@ -194,7 +194,8 @@ def test_gpu_emulated_clients_batched_off_and_unequal_rows(tmp_path):
     native.require()
     rt = run_local_emulation(_cfg(tmp_path, epochs=1, batched_clients="off"), 2, backend="hip", device=DEV)
     assert not rt.batched and rt.engine.batch is None
-    rt = run_local_emulation(_cfg(tmp_path / "u", epochs=2, shard_mode="dirichlet"), 3, backend="hip", device=DEV)
+    rt = run_local_emulation(_cfg(tmp_path / "u", epochs=2, shard_mode="dirichlet", batched_clients="on"), 3,
+                             backend="hip", device=DEV)
     assert len(set(rt.rows)) > 1 and rt.batched
     b = rt.batch_clients
     steps = [n // 500 for n in rt.rows]
