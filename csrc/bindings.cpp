@@ -448,13 +448,20 @@ void slerp(const Tensor& real, const Tensor& fake, const Tensor& out, int64_t se
                         (uint64_t)seed, ctr_ptr(rng_ctr), (uint32_t)stream, cur_stream());
 }
 
-void gp_scale(const Tensor& g, const Tensor& out, double lam, const Tensor& loss) {
+void gp_scale(const Tensor& g, const Tensor& out, double lam, const Tensor& loss, const optional<Tensor>& ws) {
   check_f32_2d(g, "g");
   check_f32_2d(out, "out");
   TORCH_CHECK(g.sizes() == out.sizes(), "gp_scale: shapes");
   const bool per_row = g.size(0) > 1 && loss.numel() == g.size(0);   // per-pack terms, summed later
+  float* wsp = nullptr;
+  int64_t wsn = 0;
+  if (ws.has_value()) {
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "gp_scale: float32 workspace");
+    wsp = fp(*ws);
+    wsn = ws->numel();
+  }
   fedtgan::launch_gp_scale(cfp(g), ld_of(g), fp(out), ld_of(out), (int)g.size(0), (int)g.size(1), (float)lam,
-                           fp(loss), per_row ? 1 : 0, cur_stream());
+                           fp(loss), per_row ? 1 : 0, wsp, wsn, cur_stream());
 }
 
 void onehot_wgrad(const std::vector<Tensor>& dy, const std::vector<Tensor>& w, const Tensor& col, const Tensor& opt,
@@ -1035,6 +1042,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "gp_split") {   // gradient-penalty scale of rows wider than 8,192: chunk-split (1) or one workgroup per row (0)
+    const int prev = fedtgan::g_gp_split;
+    fedtgan::g_gp_split = value ? 1 : 0;
+    return prev;
+  }
   if (key == "act_row_mode") {
     TORCH_CHECK(value >= 0 && value <= 2, "act_row_mode: 0 per-wave, 1 row (LDS image), 2 row (registers; forward)");
     const int prev = fedtgan::g_act_row_mode;
@@ -1113,7 +1125,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "act_bwd_ce(Tensor dact, Tensor act, Tensor logits, Tensor start, Tensor width, Tensor kind, Tensor cidx, "
       "Tensor elem, Tensor col, Tensor opt, Tensor(a!) dlogits, Tensor(b!) loss, float tau) -> ()");
   m.def("slerp(Tensor real, Tensor fake, Tensor(a!) out, int seed, Tensor rng_ctr, int stream) -> ()");
-  m.def("gp_scale(Tensor g, Tensor(a!) out, float lam, Tensor(b!) loss) -> ()");
+  m.def("gp_scale(Tensor g, Tensor(a!) out, float lam, Tensor(b!) loss, Tensor(c!)? ws=None) -> ()");
   m.def("onehot_wgrad(Tensor[] dy, Tensor(a!)[] w, Tensor col, Tensor opt, Tensor cond_off, int zero) -> ()");
   m.def(
       "d_head(Tensor d, Tensor ms, Tensor v, Tensor e, Tensor coef, Tensor wloss, Tensor(a!) y, Tensor(b!) a, "

@@ -123,6 +123,28 @@ __device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint32_t n, uint4 k
   return x;
 }
 
+// p[0, C) = one-hot(hot) written by one wave: scalar stores up to the first 16-B boundary, then 16-B stores
+// (the wide table's condition blocks are 6,762 floats per row, three of them per D-phase row: a plain
+// per-float loop was 3 x 106 store instructions per wave)
+__device__ __forceinline__ void onehot_row(float* __restrict__ p, int C, int hot, int lane) {
+  const int head = min((int)(((16u - (uint32_t)(reinterpret_cast<uintptr_t>(p) & 15u)) & 15u) >> 2), C);
+  if (lane < head) p[lane] = lane == hot ? 1.f : 0.f;
+  const int n4 = (C - head) >> 2;
+  float4* q = reinterpret_cast<float4*>(p + head);
+  for (int k = lane; k < n4; k += 64) {
+    const int i0 = head + 4 * k;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (hot >= i0 && hot < i0 + 4) {
+      v.x = hot == i0 ? 1.f : 0.f;
+      v.y = hot == i0 + 1 ? 1.f : 0.f;
+      v.z = hot == i0 + 2 ? 1.f : 0.f;
+      v.w = hot == i0 + 3 ? 1.f : 0.f;
+    }
+    q[k] = v;
+  }
+  for (int i = head + 4 * n4 + lane; i < C; i += 64) p[i] = i == hot ? 1.f : 0.f;
+}
+
 template <bool BT_ = false>
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const BIdx bi_ = batch_bidx<BT_>(a.cb.xcd);
@@ -214,11 +236,8 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   }
   const int hot = a.n_col > 0 ? a.cond_off[col] + opt : -1;
   float* xf = a.xf ? a.xf + (size_t)b * a.ldx + a.Dd : nullptr;
-  for (int i = lane; i < a.C; i += 64) {
-    const float v = (i == hot) ? 1.f : 0.f;
-    hrow[a.cc + i] = v;
-    if (xf) xf[i] = v;
-  }
+  onehot_row(hrow + a.cc, a.C, hot, lane);
+  if (xf) onehot_row(xf, a.C, hot, lane);
   if (lane == 0 && a.col) { a.col[b] = col; a.opt[b] = opt; }
   if (!real) return;
   // (4) real row for the permuted condition: count -> CSR entry -> row copy
@@ -251,7 +270,7 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
 #pragma unroll
   for (int u = 0; u < CP; ++u) v[u] = src[min(lane + 64 * u, a.Dd - 1)];
   const int phot = a.cond_off[pc] + po;
-  for (int i = lane; i < a.C; i += 64) dst[a.Dd + i] = (i == phot) ? 1.f : 0.f;
+  onehot_row(dst + a.Dd, a.C, phot, lane);
   for (int i0 = 0; i0 < a.Dd; i0 += 64 * CP) {
     float nx[CP];
     const int n0 = i0 + 64 * CP;
@@ -1369,6 +1388,7 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
 // GP_V4 float4 per thread, loaded in one burst), so the row is read once: norm, then scale.
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int GP_V4 = 8;    // rows up to 8 * 256 * 4 = 8192 wide stay in registers
+int g_gp_split = 1;         // wider rows: chunk-split two-launch path when given a workspace (set_tuning("gp_split"))
 
 __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, float* loss, int loss_per_row,
                                           float* sh, float& coef) {
@@ -1479,8 +1499,69 @@ __global__ __launch_bounds__(256) void gp_scale_v4_wide_kernel(const float* __re
   }
 }
 
+// rows wider than the register-resident variant, split over chunks of GP_V4 * 256 float4 (the wide table's 50
+// packed rows of 137,800: 17 chunks each -> 850 workgroups instead of 50): partial sums of squares per chunk into a
+// workspace, then every chunk's workgroup sums its row's partials in chunk order (deterministic) and scales.
+constexpr int GP_CH4 = GP_V4 * 256;   // float4 per chunk
+
+template <bool BT_ = false>
+__global__ __launch_bounds__(256) void gp_partial_kernel(const float* __restrict__ g, int ldg, int cols,
+                                                         float* __restrict__ part, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    g = cptr(g, co);
+    part = cptr(part, co);
+  }
+  __shared__ float sh[8];
+  const int c = bi_.x, r = bi_.y, nch = gridDim.x;
+  const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
+  const int n4 = cols / 4, c0 = c * GP_CH4;
+  f32x4 v[GP_V4];
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i) v[i] = x[min(c0 + (int)threadIdx.x + 256 * i, n4 - 1)];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i)
+    if (c0 + (int)threadIdx.x + 256 * i < n4) s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) part[(size_t)r * nch + c] = s;
+}
+
+template <bool BT_ = false>
+__global__ __launch_bounds__(256) void gp_apply_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
+                                                       int ldo, int rows, int cols, float lam, float* loss,
+                                                       int loss_per_row, const float* __restrict__ part, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    g = cptr(g, co);
+    out = cptr(out, co);
+    loss = cptr(loss, co);
+    part = cptr(part, co);
+  }
+  const int c = bi_.x, r = bi_.y, nch = gridDim.x;
+  const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
+  const int n4 = cols / 4, c0 = c * GP_CH4;
+  f32x4 v[GP_V4];
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i) v[i] = x[min(c0 + (int)threadIdx.x + 256 * i, n4 - 1)];
+  float s = 0.f;
+  for (int k = 0; k < nch; ++k) s += part[(size_t)r * nch + k];   // (uniform: every thread, chunk order)
+  const float nrm = sqrtf(s);
+  const float coef = lam * 2.f * (nrm - 1.f) / (fmaxf(nrm, 1e-30f) * (float)rows);
+  if (c == 0 && threadIdx.x == 0) {
+    const float term = lam * (nrm - 1.f) * (nrm - 1.f) / (float)rows;
+    if (loss_per_row) loss[r] = term; else atomicAdd(loss, term);
+  }
+  f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)r * ldo);
+#pragma unroll
+  for (int i = 0; i < GP_V4; ++i)
+    if (c0 + (int)threadIdx.x + 256 * i < n4) o[c0 + threadIdx.x + 256 * i] = v[i] * coef;
+}
+
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
-                     int loss_per_row, hipStream_t stream) {
+                     int loss_per_row, float* ws, int64_t ws_n, hipStream_t stream) {
   if (rows == 0) return;
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("gp_scale operand", g, out, loss);
@@ -1489,7 +1570,15 @@ void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int
                   reinterpret_cast<uintptr_t>(out) % 16 == 0;
   const bool v4 = al && cols <= GP_V4 * 256 * 4;
   const dim3 grid(rows, 1, cb.k);
-  if (al && !v4)
+  const int nch = (cols / 4 + GP_CH4 - 1) / GP_CH4;
+  if (al && !v4 && ws != nullptr && ws_n >= (int64_t)rows * nch && g_gp_split) {
+    if (cb.k > 1) check_slabs("gp_scale workspace", ws);
+    const dim3 g2(nch, rows, cb.k);
+    hipLaunchKernelGGL((cb.xcd ? gp_partial_kernel<true> : gp_partial_kernel<false>), g2, dim3(256), 0, stream, g, ldg,
+                       cols, ws, cb);
+    hipLaunchKernelGGL((cb.xcd ? gp_apply_kernel<true> : gp_apply_kernel<false>), g2, dim3(256), 0, stream, g, ldg, out,
+                       ldo, rows, cols, lam, loss, loss_per_row, ws, cb);
+  } else if (al && !v4)
     hipLaunchKernelGGL((client_batch().xcd ? gp_scale_v4_wide_kernel<true> : gp_scale_v4_wide_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
   else if (v4)

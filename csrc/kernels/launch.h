@@ -198,8 +198,11 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
 void launch_slerp(const float* real, const float* fake, float* out, int rows, int cols, int ld, uint64_t seed,
                   const uint64_t* ctr, uint32_t stream_id, hipStream_t stream);
 
+// ws (nullable, >= rows * ceil(cols / 8192) floats): rows wider than 8,192 run as a chunk-split partial-sum
+// launch + a scale launch (g_gp_split) instead of one workgroup per row
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
-                     int loss_per_row, hipStream_t stream);
+                     int loss_per_row, float* ws, int64_t ws_n, hipStream_t stream);
+extern int g_gp_split;
 
 // Weight gradient of a one-hot conditional input block (generator layers, input-major weights): row k of the
 // block's gradient is the sum of the upstream-gradient rows whose condition index is k (rows in batch order, so

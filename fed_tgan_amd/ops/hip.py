@@ -399,7 +399,15 @@ class HipOps:
         self.L.slerp(real, fake, out, self.seed, self.ctr, int(stream_id) * 16)
 
     def gp_scale(self, g, out, lam, loss_out):
-        self.L.gp_scale(g, out, float(lam), loss_out)
+        ws = None
+        if g.shape[1] > 8192:      # chunk partials of the split launch (csrc launch_gp_scale)
+            n = g.shape[0] * -(-g.shape[1] // 8192)
+            ws = self._gpws if getattr(self, "_gpws", None) is not None and self._gpws.numel() >= n else None
+            if ws is None:
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("gp_scale workspace must be sized before graph capture")
+                ws = self._gpws = self.mem.zeros(n, dtype=torch.float32)
+        self.L.gp_scale(g, out, float(lam), loss_out, ws)
 
     # ------------------------------------------------------------------ one-hot input block weight gradients
     def onehot_wgrad(self, dys, ws, col, opt, cond_off, zero: bool = False):
