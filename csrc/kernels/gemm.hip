@@ -1023,7 +1023,12 @@ struct GemmShape {
 };
 
 constexpr int GEMM_MAX_SPLITS = 64;
-int g_gemm_xcd_remap = 1;
+// 2: every GEMM launch deals its tiles to the XCDs in contiguous runs.  Round 4, same box, two passes of
+// tools/microbench.py --step-only: rule-based (1) 207.3-208.1 us per step, always (2) 204.6-205.5 us, off (0)
+// 207.6-208.2 us (profiles/knobs_step_r4.txt): the remap's index math is cheaper than the L2 sharing it buys
+// even on the short-K step GEMMs (the round-2 measurement that kept it off there predates the pair / chain
+// launches)
+int g_gemm_xcd_remap = 2;
 int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
 int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)
 int g_gemm_pair_max_wg = 0;   // pairs whose two grids together exceed this many workgroups launch separately (0: no limit)

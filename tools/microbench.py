@@ -261,6 +261,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--init-rng", default=None, help="EngineConfig.init_rng (engine | global)")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
+                    help="native set_tuning knob for A/B runs, e.g. --tuning bn_cols=16")
     ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
     ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
     ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
@@ -279,6 +281,11 @@ def main():
     ap.add_argument("--cfg-ab", default=None, metavar="FIELD", help="step + generation: a boolean EngineConfig field off / on")
     ap.add_argument("--fork-probe", action="store_true", help="step: cost of a forked side-stream branch in the graph")
     args = ap.parse_args()
+    if args.tuning:
+        from fed_tgan_amd.ops import native as _nat
+        for kv in args.tuning:
+            k_, v_ = kv.split("=", 1)
+            _nat.require().set_tuning(k_, int(v_))
     from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
     from helpers import small_table
     dev = torch.device("cuda:0")
