@@ -261,6 +261,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--init-rng", default=None, help="EngineConfig.init_rng (engine | global)")
+    ap.add_argument("--engine", action="append", default=[], metavar="KEY=VALUE",
+                    help="EngineConfig override for A/B runs, e.g. --engine chain_d1=0")
     ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
                     help="native set_tuning knob for A/B runs, e.g. --tuning bn_cols=16")
     ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
@@ -291,6 +293,10 @@ def main():
     dev = torch.device("cuda:0")
     _, _, _, _, _, _, tr, X = small_table(40000, 0)
     cfg = EngineConfig(precision=args.precision)
+    for kv in args.engine:
+        k_, v_ = kv.split("=", 1)
+        cur = getattr(cfg, k_)
+        setattr(cfg, k_, (v_.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v_))
     if args.init_rng:
         cfg.init_rng = args.init_rng
     eng = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=1)
