@@ -1042,6 +1042,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "act_rowreg_narrow") {   // rows <= 512 wide also on the register-resident row kernels (1)
+    const int prev = fedtgan::g_act_rowreg_narrow;
+    fedtgan::g_act_rowreg_narrow = value ? 1 : 0;
+    return prev;
+  }
   if (key == "gp_split") {   // gradient-penalty scale of rows wider than 8,192: chunk-split (1) or one workgroup per row (0)
     const int prev = fedtgan::g_gp_split;
     fedtgan::g_gp_split = value ? 1 : 0;

@@ -548,6 +548,7 @@ __global__ __launch_bounds__(ACT_WAVES * 64) void activate_kernel(const float* _
 // (counter (row, block / 4, lane), component block % 4): the two kernels are interchangeable.
 constexpr int ROW_WAVES = 8;
 
+template <int NW = ROW_WAVES>
 __device__ __forceinline__ float3 block_sum3(float a, float b, float c, float* sh) {
   a = wave_sum(a);
   b = wave_sum(b);
@@ -561,7 +562,7 @@ __device__ __forceinline__ float3 block_sum3(float a, float b, float c, float* s
   __syncthreads();
   float3 r = make_float3(0.f, 0.f, 0.f);
 #pragma unroll
-  for (int w = 0; w < ROW_WAVES; ++w) {
+  for (int w = 0; w < NW; ++w) {
     r.x += sh[3 * w];
     r.y += sh[3 * w + 1];
     r.z += sh[3 * w + 2];
@@ -678,8 +679,8 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
 // contiguous column ranges).  Per-element LDS atomics (the LDS-image kernel above) serialise the lanes of a wave
 // that hit one span: on the wide table (7,018 columns, spans ~17 wide) the LDS pipe was busy ~40 us per CU per
 // launch (rocprofv3 SQ_LDS_IDX_ACTIVE, profiles/wide_pmc_r4.txt).
-template <int GPW, bool BT_ = false>
-__global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const float* __restrict__ logits, int ldl,
+template <int GPW, int NW = ROW_WAVES, bool BT_ = false>
+__global__ __launch_bounds__(NW * 64) void activate_rowreg_kernel(const float* __restrict__ logits, int ldl,
                                                                          float* __restrict__ out, int ldo, int rows,
                                                                          SpanTables sp, float inv_tau, uint64_t seed,
                                                                          const uint64_t* ctr, uint32_t stream_id,
@@ -695,7 +696,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
     client_off(sl, co);
     seed += (uint64_t)bi_.z * cb.seed_step;
   }
-  constexpr int NTH = ROW_WAVES * 64;
+  constexpr int NTH = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = bi_.x;
   const int D = sp.dim, S = sp.n_span;
@@ -717,7 +718,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = min((4 * (wv + ROW_WAVES * g) + q) * 64 + lane, D - 1);
+      const int j = min((4 * (wv + NW * g) + q) * 64 + lane, D - 1);
       xv[g][q] = x[j];
       ic[g][q] = einfo[j];
       ar[g][q] = a[j];
@@ -727,7 +728,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
   const uint64_t base = (uint64_t)r << 20;
 #pragma unroll
   for (int g = 0; g < GPW; ++g) {
-    const int gi = wv + ROW_WAVES * g;
+    const int gi = wv + NW * g;
     if (4 * gi * 64 >= D) break;   // (uniform over the wave)
     const uint4 u4 = rng4(rng, step, base + (uint64_t)gi * 64u + (uint64_t)lane);
 #pragma unroll
@@ -771,7 +772,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      const int j = (4 * (wv + NW * g) + q) * 64 + lane;
       if (j < D && (ic[g][q] & EI_SOFTMAX)) {
         const int s2 = ic[g][q] & (EI_SOFTMAX - 1);
         const float o = __expf(xv[g][q] - smax[s2]) * ssum[s2];
@@ -787,7 +788,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      const int j = (4 * (wv + NW * g) + q) * 64 + lane;
       if (j < D) {
         saa += ar[g][q] * ar[g][q];
         sbb += xv[g][q] * xv[g][q];
@@ -811,7 +812,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
         sab += ra[u] * fb[u];
       }
   }
-  const float3 tot = block_sum3(saa, sbb, sab, red);
+  const float3 tot = block_sum3<NW>(saa, sbb, sab, red);
   RngArgs srng{seed, ctr, sl.stream};
   const float alpha = u01(rng4(srng, step, (uint64_t)r).x);
   float wa, wb;
@@ -821,7 +822,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_rowreg_kernel(const f
   for (int g = 0; g < GPW; ++g)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = (4 * (wv + ROW_WAVES * g) + q) * 64 + lane;
+      const int j = (4 * (wv + NW * g) + q) * 64 + lane;
       if (j < D) o[j] = wa * ar[g][q] + wb * xv[g][q];
     }
   for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
@@ -961,8 +962,8 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const fl
 // upstream gradient, the activation and the span map in registers from ONE burst of loads; the conditioned
 // span's logits are read straight from global memory by one wave (a few dozen values, L2-resident).  The LDS
 // kernel above stages the whole span table (D + 4S words, 44 KB on the wide table) per row and reads g / y twice.
-template <int E, bool BT_ = false>
-__global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_rowreg_kernel(const float* __restrict__ dact, int ldd,
+template <int E, int NW = ROW_WAVES, bool BT_ = false>
+__global__ __launch_bounds__(NW * 64) void act_bwd_ce_rowreg_kernel(const float* __restrict__ dact, int ldd,
                                                                            const float* __restrict__ act, int lda,
                                                                            const float* __restrict__ logits, int ldl,
                                                                            SpanTables sp, const int* __restrict__ col,
@@ -983,7 +984,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_rowreg_kernel(const
     loss = cptr(loss, co);
     client_off(sp, co);
   }
-  constexpr int NTH = ROW_WAVES * 64;
+  constexpr int NTH = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = bi_.x;
   const int D = sp.dim, S = sp.n_span;
@@ -1086,6 +1087,12 @@ static size_t act_row_fwd_smem_bytes(const SpanTables& sp) {   // activate_row_k
   return (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
 }
 static bool act_row_mode(const SpanTables& sp) { return sp.dim > ACT_PF * 64 && g_act_row_mode; }
+// the register-resident row kernels: wide rows in act_row_mode 2, and -- g_act_rowreg_narrow -- narrow ones too
+// (a row then gets 2-4 waves instead of the per-wave kernels' one; same Philox words, so the same draws)
+int g_act_rowreg_narrow = 1;   // measured: one-client step 204.7 -> 201.0 us, bench 17.0 -> 16.7 ms (profiles/knobs_step_r4.txt)
+static bool act_rowreg(const SpanTables& sp) {
+  return g_act_row_mode == 2 && (sp.dim > ACT_PF * 64 || g_act_rowreg_narrow);
+}
 
 static size_t act_smem_bytes(const SpanTables& sp, int waves) {
   return (size_t)span_packed_len(sp.dim, sp.n_span) * sizeof(int) +
@@ -1115,23 +1122,26 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
     check_slabs("activate operand", logits, out, ctr, sl.real, sl.out);
     check_slab(sp);
   }
-  if (act_row_mode(sp) && g_act_row_mode == 2) {
-    // register-resident row kernel: GPW groups of 4 x 64 columns per wave
-    const int ng = ((sp.dim + 63) / 64 + 3) / 4, gpw = (ng + ROW_WAVES - 1) / ROW_WAVES;
+  if (act_rowreg(sp)) {
+    // register-resident row kernel: NW waves per row, GPW groups of 4 x 64 columns per wave
+    const int ng = ((sp.dim + 63) / 64 + 3) / 4;
+    const int nw = ng <= 2 ? 2 : (ng <= 4 ? 4 : ROW_WAVES), gpw = (ng + nw - 1) / nw;
     const size_t lds = (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
-    const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
+    const dim3 grid(rows, 1, cb.k), block(nw * 64);
     const bool xcd = cb.xcd != 0;
-#define FEDTGAN_ACT_REG(G)                                                                                          \
+#define FEDTGAN_ACT_REG(G, W)                                                                                       \
   do {                                                                                                             \
-    allow_big_lds(activate_rowreg_kernel<G, false>, lds);                                                          \
-    allow_big_lds(activate_rowreg_kernel<G, true>, lds);                                                           \
-    hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, true> : activate_rowreg_kernel<G, false>), grid, block, lds, \
-                       stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);          \
+    allow_big_lds(activate_rowreg_kernel<G, W, false>, lds);                                                       \
+    allow_big_lds(activate_rowreg_kernel<G, W, true>, lds);                                                        \
+    hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, W, true> : activate_rowreg_kernel<G, W, false>), grid, block, \
+                       lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);     \
     return;                                                                                                        \
   } while (0)
-    if (gpw <= 2) FEDTGAN_ACT_REG(2);
-    if (gpw <= 4) FEDTGAN_ACT_REG(4);
-    if (gpw <= 8) FEDTGAN_ACT_REG(8);
+    if (nw == 2 && gpw <= 1) FEDTGAN_ACT_REG(1, 2);
+    if (nw == 4 && gpw <= 1) FEDTGAN_ACT_REG(1, 4);
+    if (nw == ROW_WAVES && gpw <= 2) FEDTGAN_ACT_REG(2, ROW_WAVES);
+    if (nw == ROW_WAVES && gpw <= 4) FEDTGAN_ACT_REG(4, ROW_WAVES);
+    if (nw == ROW_WAVES && gpw <= 8) FEDTGAN_ACT_REG(8, ROW_WAVES);
 #undef FEDTGAN_ACT_REG
     // (wider rows: the LDS-image row kernel)
   }
@@ -1301,23 +1311,27 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
     check_slabs("act_bwd_ce operand", dact, act, logits, col, opt, dlogits, loss);
     check_slab(sp);
   }
-  if (act_row_mode(sp) && g_act_row_mode == 2) {
-    const int ept = (sp.dim + ROW_WAVES * 64 - 1) / (ROW_WAVES * 64);   // elements per thread
+  if (act_rowreg(sp)) {
+    const int ng = ((sp.dim + 63) / 64 + 3) / 4;
+    const int nw = ng <= 2 ? 2 : (ng <= 4 ? 4 : ROW_WAVES);
+    const int ept = (sp.dim + nw * 64 - 1) / (nw * 64);   // elements per thread
     const size_t lds = (size_t)(sp.dim + sp.n_span + 2) * sizeof(float);
-    const dim3 grid(rows, 1, cb.k), block(ROW_WAVES * 64);
+    const dim3 grid(rows, 1, cb.k), block(nw * 64);
     const bool xcd = cb.xcd != 0;
-#define FEDTGAN_BWD_REG(E)                                                                                             \
+#define FEDTGAN_BWD_REG(E, W)                                                                                          \
   do {                                                                                                                \
-    allow_big_lds(act_bwd_ce_rowreg_kernel<E, false>, lds);                                                           \
-    allow_big_lds(act_bwd_ce_rowreg_kernel<E, true>, lds);                                                            \
-    hipLaunchKernelGGL((xcd ? act_bwd_ce_rowreg_kernel<E, true> : act_bwd_ce_rowreg_kernel<E, false>), grid, block, lds, \
-                       stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss,      \
+    allow_big_lds(act_bwd_ce_rowreg_kernel<E, W, false>, lds);                                                        \
+    allow_big_lds(act_bwd_ce_rowreg_kernel<E, W, true>, lds);                                                         \
+    hipLaunchKernelGGL((xcd ? act_bwd_ce_rowreg_kernel<E, W, true> : act_bwd_ce_rowreg_kernel<E, W, false>), grid, block, \
+                       lds, stream, dact, ldd, act, lda, logits, ldl, sp, col, opt, dlogits, ldg, rows, 1.f / tau, loss, \
                        loss_per_row, cb);                                                                             \
     return;                                                                                                           \
   } while (0)
-    if (ept <= 8) FEDTGAN_BWD_REG(8);
-    if (ept <= 16) FEDTGAN_BWD_REG(16);
-    if (ept <= 32) FEDTGAN_BWD_REG(32);
+    if (nw == 2 && ept <= 4) FEDTGAN_BWD_REG(4, 2);
+    if (nw == 4 && ept <= 4) FEDTGAN_BWD_REG(4, 4);
+    if (nw == ROW_WAVES && ept <= 8) FEDTGAN_BWD_REG(8, ROW_WAVES);
+    if (nw == ROW_WAVES && ept <= 16) FEDTGAN_BWD_REG(16, ROW_WAVES);
+    if (nw == ROW_WAVES && ept <= 32) FEDTGAN_BWD_REG(32, ROW_WAVES);
 #undef FEDTGAN_BWD_REG
   }
   if (act_row_mode(sp)) {

@@ -638,7 +638,7 @@ def test_adam_with_folded_colsum_matches_two_launches(hip, aux):
     assert torch.allclose(res[1][1][8000:8037], src0.sum(0), atol=1e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("d_min", [2300, 7000])
+@pytest.mark.parametrize("d_min", [300, 2300, 7000])
 def test_wide_row_kernels_match_per_wave_kernels(hip, d_min):
     """Rows wider than 512: the one-workgroup-per-row kernels (LDS row image, and register-resident with 2 or 4
     groups per wave) draw the same Philox words as the per-wave kernels, so activation (+ fused slerp) and its
@@ -655,6 +655,7 @@ def test_wide_row_kernels_match_per_wave_kernels(hip, d_min):
         fake[:, D:] = cond_cols
         interp = torch.zeros(rows // 3, Din, device=DEV)
         prev = torch.ops.fedtgan.set_tuning("act_row_mode", mode)
+        prev_n = torch.ops.fedtgan.set_tuning("act_rowreg_narrow", 1)     # (rows <= 512: 2-wave row kernels)
         try:
             hip.activate(logits, fake[:, :D], spans, 0.2, stream_id=2, slerp=(real[:rows // 3], fake, interp, 3))
             dact = mat(rows, D, seed=55)
@@ -666,6 +667,7 @@ def test_wide_row_kernels_match_per_wave_kernels(hip, d_min):
             hip.act_bwd_ce(dact, fake[:, :D], logits, spans, cond, col, opt, d, loss, 0.2)
         finally:
             torch.ops.fedtgan.set_tuning("act_row_mode", prev)
+            torch.ops.fedtgan.set_tuning("act_rowreg_narrow", prev_n)
         torch.cuda.synchronize()
         res.append((fake, interp, d, loss))
     for other in res[1:]:
