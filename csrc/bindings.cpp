@@ -1042,6 +1042,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "bn_threads") {
+    TORCH_CHECK(value == 512 || value == 1024, "bn_threads: 512 or 1024");
+    const int prev = fedtgan::g_bn_threads;
+    fedtgan::g_bn_threads = (int)value;
+    return prev;
+  }
   if (key == "act_rowreg_narrow") {   // rows <= 512 wide also on the register-resident row kernels (1)
     const int prev = fedtgan::g_act_rowreg_narrow;
     fedtgan::g_act_rowreg_narrow = value ? 1 : 0;

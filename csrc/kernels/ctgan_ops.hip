@@ -1796,6 +1796,7 @@ void launch_colsum(const ColsumJob* jobs, int n_jobs, hipStream_t stream) {
 // Loads use clamped (always valid) addresses and are masked afterwards (no predicated loads).
 constexpr int BN_THREADS = 512, BN_WAVES = BN_THREADS / 64;
 int g_bn_cols = 8;    // columns per workgroup (tuning knob, see set_tuning)
+int g_bn_threads = 512;   // threads per BN workgroup: 512, or 1024 (half the rows per thread; set_tuning("bn_threads"))
 // (16 columns for batched launches measured +1.0 ms per 8-client epoch once the clients sit on their own XCDs:
 // 47.7 vs 48.7 ms, profiles/batched_r4.md; 8 everywhere)
 static int bn_cols_for_launch() { return g_bn_cols; }
@@ -1808,28 +1809,29 @@ constexpr int BN_MAXG = 2;
 
 // sum over every row-group of the workgroup for this thread's column; NV values at once.
 // sh: [NV][BN_WAVES][COLS] LDS; ends with a barrier so sh can be reused right away.
-template <int COLS, int NV>
+template <int COLS, int NV, int NTH = BN_THREADS>
 __device__ __forceinline__ void bn_colsum(float (&v)[NV], float* sh) {
+  constexpr int NWV = NTH / 64;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, lc = threadIdx.x % COLS;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
 #pragma unroll
     for (int o = COLS; o < 64; o <<= 1) v[k] += __shfl_xor(v[k], o, 64);
-    if (lane < COLS) sh[(k * BN_WAVES + wv) * COLS + lc] = v[k];
+    if (lane < COLS) sh[(k * NWV + wv) * COLS + lc] = v[k];
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < BN_WAVES; ++w) t += sh[(k * BN_WAVES + w) * COLS + lc];
+    for (int w = 0; w < NWV; ++w) t += sh[(k * NWV + w) * COLS + lc];
     v[k] = t;
   }
   __syncthreads();
 }
 
-template <int COLS, int MAXR, bool BT_ = false>
-__global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
+template <int COLS, int MAXR, bool BT_ = false, int NTH = BN_THREADS>
+__global__ __launch_bounds__(NTH) void bn_relu_train_kernel(
     const float* __restrict__ a, int lda, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ out, int ldo, float* __restrict__ nhat, int ldn, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rm, float* __restrict__ rv, int rows, int cols, int groups,
@@ -1848,8 +1850,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     rv = cptr(rv, co);
   }
 
-  constexpr int GROUPS = BN_THREADS / COLS;
-  __shared__ float sh[2 * BN_MAXG * BN_WAVES * COLS];
+  constexpr int GROUPS = NTH / COLS;
+  __shared__ float sh[2 * BN_MAXG * (NTH / 64) * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
   const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
@@ -1873,7 +1875,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_train_kernel(
     const float d = (r < rows) ? v - (g1 ? sh1 : sh0) : 0.f;
     if (g1) { s[1] += d; s[3] += d * d; } else { s[0] += d; s[2] += d * d; }
   }
-  bn_colsum<COLS, 2 * BN_MAXG>(s, sh);
+  bn_colsum<COLS, 2 * BN_MAXG, NTH>(s, sh);
   const float m0 = s[0] / (float)rpg, m1 = s[1] / (float)rpg;
   const float mu0 = sh0 + m0, mu1 = sh1 + m1;
   const float var0 = fmaxf(s[2] / (float)rpg - m0 * m0, 0.f);   // biased batch variances
@@ -2108,6 +2110,12 @@ static void bn_train_cols(const float* a, int lda, const float* gamma, const flo
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("bn_relu_train operand", a, gamma, beta, out, nhat, mean, invstd, rm, rv);
   const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
+  if (g_bn_threads == 1024 && rows <= 8 * (1024 / COLS)) {   // twice the row groups, half the rows per thread
+    hipLaunchKernelGGL((client_batch().xcd ? bn_relu_train_kernel<COLS, 8, true, 1024> : bn_relu_train_kernel<COLS, 8, false, 1024>),
+                       grid, dim3(1024), 0, stream, a, lda, gamma, beta, out, ldo, nhat, ldn, mean, invstd, rm, rv, rows,
+                       cols, groups, momentum, eps, cb);
+    return;
+  }
 #define BN_TRAIN_LAUNCH(R)                                                                                          \
   hipLaunchKernelGGL((client_batch().xcd ? bn_relu_train_kernel<COLS, R, true> : bn_relu_train_kernel<COLS, R, false>), grid, block, 0, stream, a, lda, gamma, beta, out, ldo, nhat, \
                      ldn, mean, invstd, rm, rv, rows, cols, groups, momentum, eps, cb)
@@ -2137,8 +2145,8 @@ void launch_bn_relu_train(const float* a, int lda, const float* gamma, const flo
                      stream);
 }
 
-template <int COLS, int MAXR, bool BT_ = false>
-__global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
+template <int COLS, int MAXR, bool BT_ = false, int NTH = BN_THREADS>
+__global__ __launch_bounds__(NTH) void bn_relu_bwd_kernel(
     const float* __restrict__ dr, int lddr, const float* __restrict__ r_, int ldr, const float* __restrict__ nhat,
     int ldn, const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ da, int ldda,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, int rows, int cols, ClientBatch cb) {
@@ -2156,8 +2164,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     dbias = cptr(dbias, co);
   }
 
-  constexpr int GROUPS = BN_THREADS / COLS;
-  __shared__ float sh[3 * BN_WAVES * COLS];
+  constexpr int GROUPS = NTH / COLS;
+  __shared__ float sh[3 * (NTH / 64) * COLS];
   const int lc = threadIdx.x % COLS, grp = threadIdx.x / COLS;
   const int c = bi_.x * COLS + lc;
   const bool ok = c < cols;
@@ -2182,7 +2190,7 @@ __global__ __launch_bounds__(BN_THREADS) void bn_relu_bwd_kernel(
     st[1] += d * n;
     st[2] += n;
   }
-  bn_colsum<COLS, 3>(st, sh);
+  bn_colsum<COLS, 3, NTH>(st, sh);
   const float sdy = st[0], sdyn = st[1], snh = st[2];
   const float invn = 1.f / (float)rows;
   // the preceding Linear's bias gradient sum_r da_r, in closed form from the same single
@@ -2259,6 +2267,12 @@ static void bn_bwd_cols(const float* dr, int lddr, const float* r, int ldr, cons
   const ClientBatch cb = client_batch();
   if (cb.k > 1) check_slabs("bn_relu_bwd operand", dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias);
   const dim3 grid((cols + COLS - 1) / COLS, 1, cb.k), block(BN_THREADS);
+  if (g_bn_threads == 1024 && rows <= 8 * (1024 / COLS)) {
+    hipLaunchKernelGGL((client_batch().xcd ? bn_relu_bwd_kernel<COLS, 8, true, 1024> : bn_relu_bwd_kernel<COLS, 8, false, 1024>),
+                       grid, dim3(1024), 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, invstd, da, ldda, dgamma, dbeta,
+                       dbias, rows, cols, cb);
+    return;
+  }
 #define BN_BWD_LAUNCH(R)                                                                                          \
   hipLaunchKernelGGL((client_batch().xcd ? bn_relu_bwd_kernel<COLS, R, true> : bn_relu_bwd_kernel<COLS, R, false>), grid, block, 0, stream, dr, lddr, r, ldr, nhat, ldn, gamma, \
                      invstd, da, ldda, dgamma, dbeta, dbias, rows, cols, cb)

@@ -111,10 +111,19 @@ def test_gemm_bn_eval_relu(hip):
     assert torch.allclose(out, ref, atol=2e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("rows,scale,offset", [(500, 3.0, 1.0), (37, 3.0, 1.0), (500, 0.05, 50.0), (5000, 3.0, 1.0)])
-def test_bn_relu_train_and_bwd(hip, rows, scale, offset):
+@pytest.mark.parametrize("rows,scale,offset,threads", [(500, 3.0, 1.0, 512), (37, 3.0, 1.0, 512), (500, 0.05, 50.0, 512),
+                                                      (5000, 3.0, 1.0, 512), (1000, 3.0, 1.0, 1024), (500, 0.05, 50.0, 1024)])
+def test_bn_relu_train_and_bwd(hip, rows, scale, offset, threads):
     # the (0.05, 50) case: tiny spread around a large mean -- the one-pass shifted statistics
-    # must not lose the variance to cancellation
+    # must not lose the variance to cancellation.  threads: the BN workgroup size (set_tuning("bn_threads"))
+    prev_t = torch.ops.fedtgan.set_tuning("bn_threads", threads)
+    try:
+        _bn_train_and_bwd(hip, rows, scale, offset)
+    finally:
+        torch.ops.fedtgan.set_tuning("bn_threads", prev_t)
+
+
+def _bn_train_and_bwd(hip, rows, scale, offset):
     a = mat(rows, 300, seed=15) * scale + offset
     gamma, beta = torch.rand(300, device=DEV) + 0.5, mat(300, seed=16)
     fwd = {}
