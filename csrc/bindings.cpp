@@ -1048,9 +1048,10 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_bn_threads = (int)value;
     return prev;
   }
-  if (key == "act_rowreg_narrow") {   // rows <= 512 wide also on the register-resident row kernels (1)
+  if (key == "act_rowreg_narrow") {   // rows <= 512 wide: per-wave kernels (0), row kernels 2-4 waves (1), a block per wave (2)
+    TORCH_CHECK(value >= 0 && value <= 2, "act_rowreg_narrow: 0, 1 or 2");
     const int prev = fedtgan::g_act_rowreg_narrow;
-    fedtgan::g_act_rowreg_narrow = value ? 1 : 0;
+    fedtgan::g_act_rowreg_narrow = (int)value;
     return prev;
   }
   if (key == "gp_split") {   // gradient-penalty scale of rows wider than 8,192: chunk-split (1) or one workgroup per row (0)

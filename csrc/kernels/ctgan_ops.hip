@@ -841,6 +841,131 @@ __global__ __launch_bounds__(NW * 64) void activate_rowreg_kernel(const float* _
   }
 }
 
+// ---- narrow rows (<= 64 NW columns), one 64-column block per wave (act_rowreg_narrow 2): the same Philox words
+// as every other activation kernel -- block b uses component b % 4 of the call for group b / 4, so the waves of
+// a group each evaluate that call (4x the RNG arithmetic of activate_rowreg_kernel) -- in exchange for one
+// element per lane: the per-wave dependent chain (load, Philox, Gumbel, softmax, slerp) is a quarter as long.
+template <int NW, bool BT_ = false>
+__global__ __launch_bounds__(NW * 64) void activate_rowblk_kernel(const float* __restrict__ logits, int ldl,
+                                                                  float* __restrict__ out, int ldo, int rows,
+                                                                  SpanTables sp, float inv_tau, uint64_t seed,
+                                                                  const uint64_t* ctr, uint32_t stream_id,
+                                                                  SlerpFuse sl, ClientBatch cb) {
+  const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
+  extern __shared__ float act_smem[];
+  if (bi_.z) {
+    const int64_t co = (int64_t)bi_.z * cb.stride;
+    logits = cptr(logits, co);
+    out = cptr(out, co);
+    ctr = cptr(ctr, co);
+    client_off(sp, co);
+    client_off(sl, co);
+    seed += (uint64_t)bi_.z * cb.seed_step;
+  }
+  constexpr int NTH = NW * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = bi_.x;
+  const int D = sp.dim, S = sp.n_span;
+  const float* x = logits + (size_t)r * ldl;
+  const int* einfo = sp.packed;
+  const int* kind = einfo + D;
+  const int* start = kind + S;
+  const int* width = start + S;
+  float* vs = act_smem;          // [D] perturbed logits (softmax elements)
+  float* smax = vs + D;          // [S]
+  float* ssum = smax + S;        // [S] 1 / span sum
+  float* red = ssum + S;         // [NW * 3]
+  float* y = out + (size_t)r * ldo;
+  const bool do_sl = sl.real != nullptr && r < sl.rows;
+  const float* a = do_sl ? sl.real + (size_t)r * sl.ld : x;
+  const int j = wv * 64 + lane;          // this lane's element (block wv)
+  const bool in = j < D;
+  const int jc = min(j, D - 1);
+  float xv = x[jc];
+  const int ic = einfo[jc];
+  const float ar = a[jc];
+  const uint64_t step = ctr ? *ctr : 0ull;
+  if (in) {
+    RngArgs rng{seed, ctr, stream_id};
+    const uint4 u4 = rng4(rng, step, ((uint64_t)r << 20) + (uint64_t)(wv >> 2) * 64u + (uint64_t)lane);
+    const int q = wv & 3;
+    const uint32_t u = q == 0 ? u4.x : q == 1 ? u4.y : q == 2 ? u4.z : u4.w;
+    if (!(ic & EI_SOFTMAX)) {
+      xv = tanhf(xv);
+      y[j] = xv;
+    } else {
+      xv = (xv + gumbel(u)) * inv_tau;
+      vs[j] = xv;
+    }
+  }
+  __syncthreads();
+  for (int s2 = tid; s2 < S; s2 += NTH) {
+    if (kind[s2] == 0) continue;
+    const int st = start[s2], w = width[s2];
+    const float* v = vs + st;
+    float m = -INFINITY;
+    int i = 0;
+    for (; i + 4 <= w; i += 4) m = fmaxf(fmaxf(m, fmaxf(v[i], v[i + 1])), fmaxf(v[i + 2], v[i + 3]));
+    for (; i < w; ++i) m = fmaxf(m, v[i]);
+    float e0 = 0.f, e1 = 0.f;
+    i = 0;
+    for (; i + 2 <= w; i += 2) {
+      e0 += __expf(v[i] - m);
+      e1 += __expf(v[i + 1] - m);
+    }
+    if (i < w) e0 += __expf(v[i] - m);
+    smax[s2] = m;
+    ssum[s2] = 1.f / (e0 + e1);
+  }
+  __syncthreads();
+  if (in && (ic & EI_SOFTMAX)) {
+    const int s2 = ic & (EI_SOFTMAX - 1);
+    xv = __expf(xv - smax[s2]) * ssum[s2];
+    y[j] = xv;
+  }
+  if (!do_sl) return;
+  float saa = 0.f, sbb = 0.f, sab = 0.f;
+  if (in) {
+    saa = ar * ar;
+    sbb = xv * xv;
+    sab = ar * xv;
+  }
+  constexpr int TU = 2;
+  float ra[TU], fb[TU];
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {     // the condition columns (j >= D) of the real and fake rows
+    const int jt = min(D + u * NTH + tid, sl.cols - 1);
+    ra[u] = a[jt];
+    fb[u] = y[jt];
+  }
+#pragma unroll
+  for (int u = 0; u < TU; ++u)
+    if (D + u * NTH + tid < sl.cols) {
+      saa += ra[u] * ra[u];
+      sbb += fb[u] * fb[u];
+      sab += ra[u] * fb[u];
+    }
+  for (int jt = D + TU * NTH + tid; jt < sl.cols; jt += NTH) {   // (rare: condition blocks wider than TU * NTH)
+    const float ra2 = a[jt], fb2 = y[jt];
+    saa += ra2 * ra2;
+    sbb += fb2 * fb2;
+    sab += ra2 * fb2;
+  }
+  const float3 tot = block_sum3<NW>(saa, sbb, sab, red);
+  RngArgs srng{seed, ctr, sl.stream};
+  const float alpha = u01(rng4(srng, step, (uint64_t)r).x);
+  float wa, wb;
+  slerp_weights(tot.x, tot.y, tot.z, alpha, wa, wb);
+  float* o = sl.out + (size_t)r * sl.ld;
+  if (in) o[j] = wa * ar + wb * xv;
+#pragma unroll
+  for (int u = 0; u < TU; ++u) {
+    const int jt = D + u * NTH + tid;
+    if (jt < sl.cols) o[jt] = wa * ra[u] + wb * fb[u];
+  }
+  for (int jt = D + TU * NTH + tid; jt < sl.cols; jt += NTH) o[jt] = wa * a[jt] + wb * y[jt];
+}
+
 template <bool BT_ = false>
 __global__ __launch_bounds__(ROW_WAVES * 64) void act_bwd_ce_row_kernel(const float* __restrict__ dact, int ldd,
                                                                         const float* __restrict__ act, int lda,
@@ -1089,7 +1214,7 @@ static size_t act_row_fwd_smem_bytes(const SpanTables& sp) {   // activate_row_k
 static bool act_row_mode(const SpanTables& sp) { return sp.dim > ACT_PF * 64 && g_act_row_mode; }
 // the register-resident row kernels: wide rows in act_row_mode 2, and -- g_act_rowreg_narrow -- narrow ones too
 // (a row then gets 2-4 waves instead of the per-wave kernels' one; same Philox words, so the same draws)
-int g_act_rowreg_narrow = 1;   // measured: one-client step 204.7 -> 201.0 us, bench 17.0 -> 16.7 ms (profiles/knobs_step_r4.txt)
+int g_act_rowreg_narrow = 2;   // measured (profiles/knobs_step_r4.txt): 1: step 204.7 -> 201.0 us; 2: 200.7 -> 199.7 us, bench 16.62 -> 16.51 ms
 static bool act_rowreg(const SpanTables& sp) {
   return g_act_row_mode == 2 && (sp.dim > ACT_PF * 64 || g_act_rowreg_narrow);
 }
@@ -1121,6 +1246,21 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
   if (cb.k > 1) {
     check_slabs("activate operand", logits, out, ctr, sl.real, sl.out);
     check_slab(sp);
+  }
+  if (g_act_row_mode == 2 && g_act_rowreg_narrow == 2 && sp.dim <= ROW_WAVES * 64) {
+    const int nb = (sp.dim + 63) / 64;
+    const size_t lds = (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
+    const dim3 grid(rows, 1, cb.k);
+    const bool xcd = cb.xcd != 0;
+    if (nb <= 4) {
+      hipLaunchKernelGGL((xcd ? activate_rowblk_kernel<4, true> : activate_rowblk_kernel<4, false>), grid, dim3(256), lds,
+                         stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);
+    } else {
+      hipLaunchKernelGGL((xcd ? activate_rowblk_kernel<ROW_WAVES, true> : activate_rowblk_kernel<ROW_WAVES, false>), grid,
+                         dim3(ROW_WAVES * 64), lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr,
+                         stream_id, sl, cb);
+    }
+    return;
   }
   if (act_rowreg(sp)) {
     // register-resident row kernel: NW waves per row, GPW groups of 4 x 64 columns per wave
@@ -1313,7 +1453,7 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
   }
   if (act_rowreg(sp)) {
     const int ng = ((sp.dim + 63) / 64 + 3) / 4;
-    const int nw = ng <= 2 ? 2 : (ng <= 4 ? 4 : ROW_WAVES);
+    const int nw = (g_act_rowreg_narrow == 2 || ng > 4) ? ROW_WAVES : (ng <= 2 ? 2 : 4);
     const int ept = (sp.dim + nw * 64 - 1) / (nw * 64);   // elements per thread
     const size_t lds = (size_t)(sp.dim + sp.n_span + 2) * sizeof(float);
     const dim3 grid(rows, 1, cb.k), block(nw * 64);
@@ -1329,6 +1469,7 @@ void launch_act_bwd_ce(const float* dact, int ldd, const float* act, int lda, co
   } while (0)
     if (nw == 2 && ept <= 4) FEDTGAN_BWD_REG(4, 2);
     if (nw == 4 && ept <= 4) FEDTGAN_BWD_REG(4, 4);
+    if (nw == ROW_WAVES && ept <= 1) FEDTGAN_BWD_REG(1, ROW_WAVES);
     if (nw == ROW_WAVES && ept <= 8) FEDTGAN_BWD_REG(8, ROW_WAVES);
     if (nw == ROW_WAVES && ept <= 16) FEDTGAN_BWD_REG(16, ROW_WAVES);
     if (nw == ROW_WAVES && ept <= 32) FEDTGAN_BWD_REG(32, ROW_WAVES);

@@ -659,12 +659,13 @@ def test_wide_row_kernels_match_per_wave_kernels(hip, d_min):
     real = mat(rows, Din, seed=53)
     cond_cols = mat(rows, nc, seed=54)
     res = []
-    for mode in (0, 1, 2):
+    # (act_rowreg_narrow: rows <= 512 on the row kernels with 2 waves (1) or one 64-column block per wave (2))
+    for mode, narrow in ((0, 0), (1, 1), (2, 1), (2, 2)):
         fake = torch.zeros(rows, Din, device=DEV)
         fake[:, D:] = cond_cols
         interp = torch.zeros(rows // 3, Din, device=DEV)
         prev = torch.ops.fedtgan.set_tuning("act_row_mode", mode)
-        prev_n = torch.ops.fedtgan.set_tuning("act_rowreg_narrow", 1)     # (rows <= 512: 2-wave row kernels)
+        prev_n = torch.ops.fedtgan.set_tuning("act_rowreg_narrow", narrow)
         try:
             hip.activate(logits, fake[:, :D], spans, 0.2, stream_id=2, slerp=(real[:rows // 3], fake, interp, 3))
             dact = mat(rows, D, seed=55)
