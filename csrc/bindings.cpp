@@ -1042,6 +1042,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "gp_threads") {
+    TORCH_CHECK(value == 256 || value == 1024, "gp_threads: 256 or 1024");
+    const int prev = fedtgan::g_gp_threads;
+    fedtgan::g_gp_threads = (int)value;
+    return prev;
+  }
   if (key == "bn_threads") {
     TORCH_CHECK(value == 512 || value == 1024, "bn_threads: 512 or 1024");
     const int prev = fedtgan::g_bn_threads;

@@ -1547,7 +1547,8 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
 // GP_V4 float4 per thread, loaded in one burst), so the row is read once: norm, then scale.
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 constexpr int GP_V4 = 8;    // rows up to 8 * 256 * 4 = 8192 wide stay in registers
-int g_gp_split = 1;         // wider rows: chunk-split two-launch path when given a workspace (set_tuning("gp_split"))
+int g_gp_split = 1;          // wider rows: chunk-split two-launch path when given a workspace (set_tuning("gp_split"))
+int g_gp_threads = 256;      // workgroup size of the register-resident gp_scale (256, or 1024 for rows <= 8192; A/B knob)
 
 __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, float* loss, int loss_per_row,
                                           float* sh, float& coef) {
@@ -1560,8 +1561,8 @@ __device__ __forceinline__ void gp_finish(int r, float s, int rows, float lam, f
   }
 }
 
-template <bool BT_ = false>
-__global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
+template <bool BT_ = false, int NTH = 256, int V = GP_V4>
+__global__ __launch_bounds__(NTH) void gp_scale_v4_kernel(const float* __restrict__ g, int ldg, float* __restrict__ out,
                                                           int ldo, int rows, int cols, float lam, float* loss,
                                                           int loss_per_row, ClientBatch cb) {
   const BIdx bi_ = batch_bidx<BT_>(cb.xcd);
@@ -1571,23 +1572,23 @@ __global__ __launch_bounds__(256) void gp_scale_v4_kernel(const float* __restric
     out = cptr(out, co);
     loss = cptr(loss, co);
   }
-  __shared__ float sh[8];
+  __shared__ float sh[NTH / 64];
   const int r = bi_.x;
   const f32x4* x = reinterpret_cast<const f32x4*>(g + (size_t)r * ldg);
   const int n4 = cols / 4;
-  f32x4 v[GP_V4];
+  f32x4 v[V];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < GP_V4; ++i) v[i] = x[min((int)threadIdx.x + 256 * i, n4 - 1)];
+  for (int i = 0; i < V; ++i) v[i] = x[min((int)threadIdx.x + NTH * i, n4 - 1)];
 #pragma unroll
-  for (int i = 0; i < GP_V4; ++i)
-    if ((int)threadIdx.x + 256 * i < n4) s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
+  for (int i = 0; i < V; ++i)
+    if ((int)threadIdx.x + NTH * i < n4) s += v[i][0] * v[i][0] + v[i][1] * v[i][1] + v[i][2] * v[i][2] + v[i][3] * v[i][3];
   float coef;
   gp_finish(r, s, rows, lam, loss, loss_per_row, sh, coef);
   f32x4* o = reinterpret_cast<f32x4*>(out + (size_t)r * ldo);
 #pragma unroll
-  for (int i = 0; i < GP_V4; ++i)
-    if ((int)threadIdx.x + 256 * i < n4) o[threadIdx.x + 256 * i] = v[i] * coef;
+  for (int i = 0; i < V; ++i)
+    if ((int)threadIdx.x + NTH * i < n4) o[threadIdx.x + NTH * i] = v[i] * coef;
 }
 
 template <bool BT_ = false>
@@ -1740,6 +1741,9 @@ void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int
   } else if (al && !v4)
     hipLaunchKernelGGL((client_batch().xcd ? gp_scale_v4_wide_kernel<true> : gp_scale_v4_wide_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);
+  else if (v4 && g_gp_threads == 1024 && cols / 4 <= 2 * 1024)
+    hipLaunchKernelGGL((cb.xcd ? gp_scale_v4_kernel<true, 1024, 2> : gp_scale_v4_kernel<false, 1024, 2>), grid, dim3(1024), 0,
+                       stream, g, ldg, out, ldo, rows, cols, lam, loss, loss_per_row, cb);
   else if (v4)
     hipLaunchKernelGGL((client_batch().xcd ? gp_scale_v4_kernel<true> : gp_scale_v4_kernel<false>), grid, dim3(256), 0, stream, g, ldg, out, ldo, rows, cols, lam, loss,
                        loss_per_row, cb);

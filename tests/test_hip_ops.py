@@ -456,8 +456,9 @@ def test_gemm_padded_views_use_vector_loads(hip, ta, tb, M, N, K):
     hip.tile_override = None
 
 
-@pytest.mark.parametrize("cols,split", [(6260, 1), (6259, 1), (40, 1), (137800, 1), (137800, 0), (20004, 1)])
-def test_gp_scale_per_row_terms(hip, cols, split):
+@pytest.mark.parametrize("cols,split,threads", [(6260, 1, 256), (6259, 1, 256), (40, 1, 256), (137800, 1, 256),
+                                               (137800, 0, 256), (20004, 1, 256), (6280, 1, 1024), (40, 1, 1024)])
+def test_gp_scale_per_row_terms(hip, cols, split, threads):
     """Vector (16-B, register-resident), scalar, one-workgroup-per-row wide and chunk-split wide (two launches,
     set_tuning("gp_split")) variants; per-pack loss terms sum to the penalty."""
     g = mat(50, cols, seed=30) * (0.02 if cols < 10000 else 0.004)
@@ -465,10 +466,12 @@ def test_gp_scale_per_row_terms(hip, cols, split):
     rows1 = torch.zeros(50, device=DEV)
     l2 = torch.zeros(1, device=DEV)
     prev = torch.ops.fedtgan.set_tuning("gp_split", split)
+    prev_t = torch.ops.fedtgan.set_tuning("gp_threads", threads)
     try:
         hip.gp_scale(g, o1, 10.0, rows1)
     finally:
         torch.ops.fedtgan.set_tuning("gp_split", prev)
+        torch.ops.fedtgan.set_tuning("gp_threads", prev_t)
     REF.gp_scale(g, o2, 10.0, l2)
     torch.cuda.synchronize()
     assert torch.allclose(o1, o2, atol=1e-6, rtol=1e-4)
