@@ -368,8 +368,6 @@ class FedRuntime:
             # threads): a failure falls back to per-thread engines instead of aborting round 0
             self._prepare_batched()
         self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
-        if self.is_fed and cfg.write_csv and cfg.async_csv and self.csv_cols is not None:
-            self._warm_csv_writer(len(merged["columns"]))
         self.init_times["engine"] = time.time() - t0
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
         c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
@@ -438,24 +436,6 @@ class FedRuntime:
         self.batched = False
         self.batch_clients = None
         g.wait()
-
-    def _warm_csv_writer(self, n_col: int):   # n_col: columns of the decoded value matrix
-        """The background writer's first table pays one-time costs (thread start, the formatter's first call)
-        while holding the GIL in places; measured on 8 batched clients, round 1 (whose launches overlap the
-        first CSV) took 116-126 ms against 49 ms steady.  A 2-row table written to os.devnull now, in the
-        background, moves that cost into initialisation."""
-        from ..utils.csvio import AsyncTableWriter
-        if self._writer is None:
-            self._writer = AsyncTableWriter()
-        from ..utils import csvio
-        width = max([n_col] + [int(j) + 1 for j in self.csv_cols.src])
-
-        def warm():
-            try:
-                csvio.write_layout(os.devnull, np.zeros((2, width)), self.csv_cols, threads=self.cfg.csv_threads)
-            except Exception:      # (a warm-up only: the real tables report their own errors)
-                pass
-        self._writer.submit(warm)
 
     def _prepare_batched(self):
         """Collective over the process' client threads: thread 0 freezes the arena (one device sync: every
