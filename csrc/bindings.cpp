@@ -1042,6 +1042,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "chain_coalesced") {   // chained tail GEMM: lane-contiguous weight rows + wave sums (1)
+    const int prev = fedtgan::g_chain_coalesced;
+    fedtgan::g_chain_coalesced = value ? 1 : 0;
+    return prev;
+  }
   if (key == "gp_threads") {
     TORCH_CHECK(value == 256 || value == 1024, "gp_threads: 256 or 1024");
     const int prev = fedtgan::g_gp_threads;

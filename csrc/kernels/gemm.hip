@@ -1077,6 +1077,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
 // The discriminator's second layer (150 or 50 x 256 x 256) and its R-chain link R1 = (R0 W1^T) . MS1
 // were launches of their own after D0's / R0's reduction.
 constexpr int CH_MAXK = 1024, CH_COLS = 64;
+int g_chain_coalesced = 0;   // chain tail: per-column weight rows read lane-contiguous + wave sums (1) or one row per lane (0)
 // MASK: head and tail both EPI_MASK (the R chain) -- the launch carries no Philox / BN epilogue code
 template <int SMAX, bool MASK = false, bool BT_ = false>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
@@ -1102,6 +1103,44 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
   __syncthreads();
   const int jl = threadIdx.x & (CH_COLS - 1), kq = threadIdx.x >> 6;
   const int j = s * CH_COLS + jl;
+  if (t.chain_co) {
+    // wave kq owns 16 of the block's 64 output columns; for each, the 64 lanes read the column's weight row as
+    // consecutive float4 (one coalesced 1 KB request per 256 K values, instead of 64 rows 1 KB apart per
+    // request) and a wave sum finishes the dot product
+    constexpr int JW = CH_COLS / 4;
+    const int lane = threadIdx.x & 63;
+    float p[JW];
+#pragma unroll
+    for (int jj = 0; jj < JW; ++jj) p[jj] = 0.f;
+    for (int k0 = 0; k0 < g.N; k0 += 256) {
+      const int k = k0 + 4 * lane;
+      const bool kin = k < g.N;
+      const float4 x = kin ? *reinterpret_cast<const float4*>(row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 w[JW];
+#pragma unroll
+      for (int jj = 0; jj < JW; ++jj) {
+        const int jc = min(s * CH_COLS + kq * JW + jj, t.N - 1);
+        w[jj] = *reinterpret_cast<const float4*>(t.b + (size_t)jc * t.ldb + min(k, g.N - 4));
+      }
+#pragma unroll
+      for (int jj = 0; jj < JW; ++jj)
+        if (kin) p[jj] += (w[jj].x * x.x + w[jj].y * x.y) + (w[jj].z * x.z + w[jj].w * x.w);
+    }
+#pragma unroll
+    for (int jj = 0; jj < JW; ++jj) {
+      const float tsum = wave_sum(p[jj]);
+      if (lane == 0) part[0][kq * JW + jj] = tsum;
+    }
+    __syncthreads();
+    if (kq == 0 && j < t.N) {
+      float v = t.alpha * part[0][jl];
+      if (t.bias) v += t.bias[j];
+      const uint64_t st = (t.epi == EPI_LRELU_DROPOUT && t.rng_ctr) ? *t.rng_ctr : 0ull;
+      if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
+      else t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+    }
+    return;
+  }
   const int q4 = g.N / 16;                       // float4 per K-quarter (host: N % 16 == 0)
   float a0 = 0.f, a1 = 0.f;
   if (j < t.N) {
@@ -1276,6 +1315,7 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     t.cstride = g.cstride;      // (the tail was never prepared: it shares the head's client layout)
     t.seed_step = g.seed_step;
     t.nclient = g.nclient;
+    t.chain_co = g_chain_coalesced && (g.N % 4 == 0);
     const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS, g.nclient), block(256);
     const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
 #define FEDTGAN_CHAIN(S)                                                                                 \

@@ -118,6 +118,7 @@ struct GemmArgs {
   uint64_t seed_step;
   int nclient;
   int xcd_cl;   // ClientBatch::xcd
+  int chain_co;   // chained tail (chain_epilogue_kernel): lane-contiguous weight rows + wave sums (g_chain_coalesced)
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);
@@ -203,6 +204,7 @@ void launch_slerp(const float* real, const float* fake, float* out, int rows, in
 void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int cols, float lam, float* loss,
                      int loss_per_row, float* ws, int64_t ws_n, hipStream_t stream);
 extern int g_gp_split;
+extern int g_chain_coalesced;   // set_tuning("chain_coalesced")
 extern int g_gp_threads;   // register-resident gp_scale workgroup size (set_tuning("gp_threads"))
 extern int g_bn_threads;   // BN workgroup size (set_tuning("bn_threads"))
 extern int g_act_rowreg_narrow;   // narrow rows on the register-resident row kernels (set_tuning("act_rowreg_narrow"))

@@ -389,3 +389,30 @@ def test_onehot_wgrad_matches_dense_gemm():
     for n in ("G.out.W", "G.0.W", "G.1.W"):
         a_ = 0 if n == "G.out.W" else b.off[int(n[2])]
         assert b.g[n][:, c0 - a_:].abs().max().item() == 0.0, n
+
+
+def test_chain_tail_coalesced_matches_row_per_lane():
+    """set_tuning("chain_coalesced"): the chained tail GEMM (D1 forward / R1 link in D0's / R0's reduction launch)
+    with lane-contiguous weight rows + wave sums gives the same outputs as one weight row per lane (fp32 dot
+    products in a different order: close), and a step with it trains the same parameters within rounding."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    res = []
+    for co in (0, 1):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32"), DEV, backend="hip", seed=14)
+        eng.set_training_data(X)
+        prev = torch.ops.fedtgan.set_tuning("chain_coalesced", co)
+        try:
+            eng.train_steps(1, use_graph=False)
+            torch.cuda.synchronize()
+            res.append((eng.dl[1].clone(), eng.flat.clone()))
+            eng.train_steps(8, use_graph=True)
+            torch.cuda.synchronize()
+            assert bool(torch.isfinite(eng.flat).all())
+        finally:
+            torch.ops.fedtgan.set_tuning("chain_coalesced", prev)
+    (d0, f0), (d1, f1) = res
+    assert torch.allclose(d0, d1, atol=1e-5, rtol=1e-4), float((d0 - d1).abs().max())
+    assert (f0 - f1).abs().max().item() <= 2 * 2e-4 + 1e-6
