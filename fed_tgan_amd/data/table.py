@@ -56,20 +56,65 @@ def dump_meta_json(meta: dict, path: str) -> None:
         json.dump(meta, f, sort_keys=True, indent=4, separators=(",", ": "), cls=NumpyJSONEncoder)
 
 
+def _is_missing(v) -> bool:
+    """pd.isna for one object value (None, NaN, NaT, pd.NA), never raising on a non-scalar."""
+    try:
+        return bool(pd.isna(v))
+    except (TypeError, ValueError):
+        return False
+
+
+def _first_appearance(codes: np.ndarray, labels: np.ndarray):
+    """(codes, labels) with the labels renumbered in order of first appearance in ``codes`` -- the order
+    pd.factorize gives the column itself (its hash pass, which ``value_counts`` ties follow)."""
+    u, pos = np.unique(codes, return_index=True)
+    order = u[np.argsort(pos, kind="stable")]
+    remap = np.empty(len(labels), dtype=np.int64)
+    remap[order] = np.arange(len(order))
+    return remap[codes], labels[order]
+
+
+def _categorical_strings(col: pd.Series):
+    """(codes, labels) of a pandas categorical column as the object path would see it: blank (" ") and
+    missing cells become "empty", labels are the categories' ``str`` forms (equal strings merge), and both
+    are in order of first appearance; categories no row holds are dropped (``value_counts`` of the raw
+    column does not list them)."""
+    cats = np.asarray(col.cat.categories, dtype=object)
+    codes = col.cat.codes.to_numpy().astype(np.int64)
+    bad = np.asarray([(isinstance(u, str) and u == " ") or _is_missing(u) for u in cats], dtype=bool)
+    strs = [str(u) for u in cats[~bad]]
+    kmap, labels = pd.factorize(pd.Index(strs, dtype=object)) if strs else (np.zeros(0, np.int64), [])
+    labels = list(labels)
+    e = labels.index(EMPTY) if EMPTY in labels else len(labels)
+    if e == len(labels):
+        labels.append(EMPTY)
+    m = np.empty(len(cats) + 1, dtype=np.int64)     # m[-1]: the missing code -1
+    m[np.nonzero(~bad)[0]] = kmap
+    m[np.nonzero(bad)[0]] = e
+    m[-1] = e
+    return _first_appearance(m[codes], np.asarray(labels, dtype=object))
+
+
 def timestamp_token() -> str:
     """The reference's folder/file timestamp token (`file_generator.py:97`)."""
     return str(datetime.datetime.now().timestamp()).replace(".", "")
 
 
 def detect_integer_columns(df: pd.DataFrame) -> List[str]:
+    """Integer columns of the raw frame (`file_generator.py:104-110`): an int dtype, or a float dtype whose
+    non-null values are all finite whole numbers.  Object columns never qualify (their non-null values
+    keep the object dtype), so they are not scanned."""
     out = []
     for c in df.columns:
-        s = df[c].dropna()
-        kind = s.dtype.kind
+        col = df[c]
+        kind = col.dtype.kind
         if kind in "iu":
             out.append(c)
         elif kind == "f":
-            v = s.to_numpy()
+            v = col.to_numpy()
+            nan = np.isnan(v)
+            if nan.any():
+                v = v[~nan]
             if np.all(np.isfinite(v)) and np.array_equal(v, np.trunc(v)):
                 out.append(c)
     return out
@@ -90,18 +135,43 @@ class TablePreprocessor:
         self.output_name = f"{self.file_name}_{self.synthesizer_used}-{timestamp_token()}"
 
         self.integer_columns = detect_integer_columns(frame)
+        self._cat_cache: Dict[str, tuple] = {}
         # blanks -> NaN -> "empty" (`file_generator.py:115-116`), column by column: numeric columns
-        # without NaNs are untouched, so only object columns and NaN-holding ones are rewritten
-        df = frame.copy()
+        # without NaNs are untouched, so only object columns and NaN-holding ones are rewritten.  An
+        # object column is factorised once: the blank / missing test runs on its distinct values, and a
+        # column of plain strings keeps the factorisation for the categorical pass (_cat_strings)
+        df = frame.copy(deep=False)       # columns are replaced, never written in place
+        categorical = list(categorical_list) + [d for d in self.date_columns if d not in categorical_list]
+        cat_set = set(categorical) - set(self.date_columns)
         for c in df.columns:
             col = df[c]
-            if col.dtype == object:
-                col = col.where(col != " ", np.nan)
-            if col.isna().any():
-                df[c] = col.astype(object).where(col.notna(), EMPTY)
-            elif col is not df[c]:
+            if isinstance(col.dtype, pd.CategoricalDtype):
+                if c in cat_set:      # codes + categories are already a factorisation: no per-row objects
+                    codes, labels = _categorical_strings(col)
+                    self._cat_cache[c] = (codes, labels)
+                    df[c] = pd.Categorical.from_codes(codes, categories=labels)
+                    continue
+                col = col.astype(object)
                 df[c] = col
-        categorical = list(categorical_list) + [d for d in self.date_columns if d not in categorical_list]
+            if col.dtype == object:
+                codes, uniq = pd.factorize(col, use_na_sentinel=False)
+                uniq = np.asarray(uniq, dtype=object)
+                bad = np.asarray([(isinstance(u, str) and u == " ") or _is_missing(u) for u in uniq], dtype=bool)
+                if bad.any():
+                    df[c] = col.where(~bad[codes], EMPTY)
+                    if all(isinstance(u, str) for u in uniq[~bad]):
+                        # "empty" joins the distinct values (once, even if the literal was already there)
+                        labels = list(uniq[~bad])
+                        e = labels.index(EMPTY) if EMPTY in labels else len(labels)
+                        if e == len(labels):
+                            labels.append(EMPTY)
+                        remap = np.cumsum(~bad) - 1
+                        remap[bad] = e
+                        self._cat_cache[c] = _first_appearance(remap[codes], np.asarray(labels, dtype=object))
+                elif all(isinstance(u, str) for u in uniq):
+                    self._cat_cache[c] = (codes.astype(np.int64, copy=False), uniq)
+            elif col.isna().any():
+                df[c] = col.astype(object).where(col.notna(), EMPTY)
         untouched = set(categorical) | set(self.date_columns)
         for c in df.columns:
             if c not in untouched and c in self.non_negative_columns:
@@ -109,8 +179,10 @@ class TablePreprocessor:
         if self.date_columns:
             df, categorical = split_dates(df, self.date_columns, categorical)
         self.categorical_list = categorical
+        # (a date column is replaced by its parts: its factorisation is stale)
+        self._cat_cache = {k: v for k, v in self._cat_cache.items() if k in set(categorical) and
+                           k not in self.date_columns}
         self.df = df
-        self._cat_cache: Dict[str, tuple] = {}
 
     def _cat_strings(self, c: str):
         """Column ``c`` as ``(codes, labels)`` with ``labels[codes]`` == ``df[c].astype(str)``.
@@ -124,7 +196,8 @@ class TablePreprocessor:
             if col.dtype == object and pd.api.types.infer_dtype(col, skipna=False) != "string":
                 # factorize merges objects that hash and compare equal (1, 1.0, True) although they print
                 # differently ('1', '1.0', 'True'): key a mixed object column by (type, value)
-                keys = pd.Series([(type(v).__name__, v if v == v else None) for v in col.tolist()], dtype=object)
+                keys = pd.Series([(type(v).__name__, None if _is_missing(v) else v) for v in col.tolist()],
+                                 dtype=object)
                 codes, _ = pd.factorize(keys, use_na_sentinel=False)
                 first = pd.Series(np.arange(len(codes))).groupby(codes).first().to_numpy()
                 uniq = col.to_numpy()[first]
@@ -168,8 +241,9 @@ class TablePreprocessor:
 
     # ------------------------------------------------------------------ encode
     def encode(self, vocabs: Sequence[CategoryVocab]) -> np.ndarray:
-        """Label-encode with the global vocabularies; returns float64 [rows, cols]."""
-        out = np.empty((len(self.df), self.df.shape[1]), dtype=np.float64)
+        """Label-encode with the global vocabularies; returns float64 [rows, cols] in column-major
+        (Fortran) order: every column is written and later read (VGM fits, device upload) contiguously."""
+        out = np.empty((self.df.shape[1], len(self.df)), dtype=np.float64).T
         cursor = 0
         for j, c in enumerate(self.df.columns):
             if c in self.categorical_list:

@@ -118,15 +118,24 @@ def encode_on_device(tr: VGMTransformer, data: np.ndarray, device, seed: int = 0
     from ..ops import native
     L = native.require()
     t = _tables(tr, device)
-    data = np.ascontiguousarray(data, dtype=np.float64)
+    data = np.asarray(data, dtype=np.float64)
     if data.ndim != 2 or data.shape[1] != len(tr.meta):
         raise ValueError(f"expected a [rows, {len(tr.meta)}] table")
-    for j, n_codes in zip(t["cat_cols"], t["cat_n"]):   # every code must index its LUT row
-        col = data[:, j]
-        if len(col) and (not np.all(np.isfinite(col)) or col.min() < 0 or col.max() >= n_codes
-                         or not np.all(col == np.floor(col))):
-            raise ValueError(f"column {j}: category codes outside 0..{n_codes - 1}")
-    x = torch.as_tensor(data, device=device)
+    # a column-major table (TablePreprocessor.encode) is uploaded as its [cols, rows] transpose and
+    # turned row-major on the device: no host-side transposing copy of the (wide: 400 MB) matrix
+    if data.flags.f_contiguous and not data.flags.c_contiguous:
+        x = torch.as_tensor(data.T, device=device).t().contiguous()
+    else:
+        x = torch.as_tensor(np.ascontiguousarray(data), device=device)
+    if t["cat_cols"]:
+        # every code must index its LUT row (checked on the device: one host read of the verdict)
+        cc = torch.as_tensor(np.asarray(t["cat_cols"], dtype=np.int64), device=device)
+        nc = torch.as_tensor(np.asarray(t["cat_n"], dtype=np.float64), device=device)
+        v = x.index_select(1, cc)
+        bad = (~torch.isfinite(v)) | (v < 0) | (v >= nc) | (v != torch.floor(v))
+        if len(v) and bool(bad.any()):
+            j = int(cc[bad.any(0).nonzero()[0, 0]])
+            raise ValueError(f"column {j}: category codes outside 0..{int(t['cat_n'][t['cat_cols'].index(j)]) - 1}")
     n = x.shape[0]
     lay = tr.layout
     out = torch.zeros(n, lay.data_dim, dtype=torch.float32, device=device)

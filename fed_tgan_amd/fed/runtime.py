@@ -52,7 +52,7 @@ from ..features.transformer import VGMTransformer
 from ..models.engine import CTGANEngine, EngineConfig
 from ..models.samplers import CondTables
 from ..parallel.comm import Comm
-from ..utils.metrics import MetricsLog, PhaseTimer
+from ..utils.metrics import MetricsLog, PhaseTimer, cgroup_cpu_stat
 from ..utils.devsync import PendingHost, stream_sync
 from .stats import (aggregation_weights, continuous_client_distances, continuous_client_distances_device,
                     merge_categorical_metas, uniform_weights)
@@ -233,9 +233,9 @@ class FedRuntime:
             print(f"[data] rank {self.rank}: {path} not found; using the synthetic {cfg.spec.name}-schema "
                   f"generator ({cfg.synthetic_rows} rows, shard mode {cfg.shard_mode})", flush=True)
         if cfg.shard_mode == "independent":
-            df = generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx)
+            df = generate(cfg.spec, cfg.synthetic_rows, seed=cfg.seed * 1000 + idx, as_category=True)
         else:
-            full = generate(cfg.spec, cfg.synthetic_rows * k, seed=cfg.seed)
+            full = generate(cfg.spec, cfg.synthetic_rows * k, seed=cfg.seed, as_category=True)
             df = shard(full, k, cfg.shard_mode, seed=cfg.seed, target=cfg.spec.target_column,
                        alpha=cfg.dirichlet_alpha)[idx]
         if cfg.dump_real:
@@ -267,7 +267,9 @@ class FedRuntime:
         self.table = None
         if self.is_client:
             df = self._local_frame()
-            self.table = TablePreprocessor(df[spec.selected_variables], f"{self.name}_train", spec.problem_type,
+            if list(df.columns) != list(spec.selected_variables):
+                df = df[spec.selected_variables]
+            self.table = TablePreprocessor(df, f"{self.name}_train", spec.problem_type,
                                            "" if spec.target_column == "none" else spec.target_column,
                                            spec.categorical_list, spec.nonnegative_list, spec.date_dic)
         metas = c.all_gather_object(self.table.local_meta() if self.is_client else None)
@@ -368,12 +370,44 @@ class FedRuntime:
             # threads): a failure falls back to per-thread engines instead of aborting round 0
             self._prepare_batched()
         self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
+        self._prepare_round_zero()
         self.init_times["engine"] = time.time() - t0
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
         c.warmup(dst=self.federator, gather=self.federator in c.client_ranks)
         self.init_times["total"] = time.time() - t0     # cumulative seconds at the end of each stage
         _log(cfg, self.rank, f"[init] done in {time.time() - t0:.2f}s: data_dim={lay.data_dim} n_opt={lay.n_opt} "
                              f"steps/epoch={self.steps}")
+
+    def _prepare_round_zero(self):
+        """Everything round 0 would otherwise do for the first time, done at initialisation: capture the
+        local epoch's step graphs and the generation graph of this rank's share of the epoch table, create
+        the table's copy stream and background writer, and page in one pinned host buffer of the table's
+        size (torch's caching host allocator hands it back in round 0).  Round 0 then costs what every
+        later round costs (`Server/dtds/distributed.py:790-829` times every round the same way)."""
+        cfg, c = self.cfg, self.comm
+        if self.device.type != "cuda" or cfg.mode != "fedavg" or cfg.use_graph is False:
+            return
+        gen = []
+        samplers = c.client_ranks if (self.federator in c.client_ranks and not getattr(self, "batched", False)) \
+            else [self.federator]
+        if self.rank in samplers:
+            i = samplers.index(self.rank)
+            gen.append(self.n_sample // len(samplers) + (1 if i < self.n_sample % len(samplers) else 0))
+        if self.is_fed and int(cfg.e_interval) > 1 and len(samplers) > 1:
+            gen.append(self.n_sample)           # rounds without aggregation: the federator's table alone
+        # (a batched engine's step graphs were captured by _prepare_batched)
+        train = 0 if getattr(self, "batched", False) or not self.is_client or not self.engine.tables \
+            else self.engine.steps_per_epoch
+        self.engine.prepare_graphs(train, gen)
+        if self.is_fed and cfg.write_csv and cfg.async_csv:
+            self._copy_stream = torch.cuda.Stream(self.device)
+            n_cols = len(self.global_meta["columns"])
+            torch.empty((self.n_sample, n_cols), dtype=torch.float64, pin_memory=True)   # back to the cache
+            from ..utils.csvio import AsyncTableWriter
+            if self._writer is None:
+                self._writer = AsyncTableWriter()
+            self._writer.submit(lambda: None)       # the writer thread starts now
+            self._writer.flush()
 
     def _batch_group(self, lay):
         """The batched multi-client engine's arena when this process' clients run as one (threads of an
@@ -668,6 +702,8 @@ class FedRuntime:
         self._round_start[epoch] = t0
         alive = round_alive_mask(self.cfg, epoch, c.n_clients)
         h0 = time.perf_counter()
+        cpu0 = time.process_time()
+        thr0 = cgroup_cpu_stat() if self.metrics is not None else {}
         hw = hi = 0.0
         with self.timer.phase("train", self.device):
             if getattr(self, "batched", False):
@@ -710,6 +746,13 @@ class FedRuntime:
         if self.device.type == "cuda":
             stream_sync(self.device)
         dt = time.time() - t0
+        if self.metrics is not None:
+            # process CPU seconds of the round (all threads) and the cgroup's CFS throttling during it
+            self._host_train["cpu_s"] = time.process_time() - cpu0
+            thr1 = cgroup_cpu_stat()
+            for k in ("throttled_usec", "nr_throttled", "usage_usec"):
+                if k in thr0 and k in thr1:
+                    self._host_train[k] = thr1[k] - thr0[k]
         self._sync_losses()
         return dt
 

@@ -38,7 +38,7 @@ from __future__ import annotations
 
 import contextlib
 import dataclasses
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -953,7 +953,7 @@ class CTGANEngine:
         if not self.tables:
             raise RuntimeError("set_training_data() first")
         if use_graph is None:
-            use_graph = self.device.type == "cuda"
+            use_graph = self._graphs_by_default()
         if use_graph:
             # U steps per graph launch (the per-launch gap between graphs is paid n/U times)
             U = max(1, int(self.cfg.graph_unroll))
@@ -976,6 +976,33 @@ class CTGANEngine:
 
     def train_epoch(self, use_graph: bool | None = None):
         self.train_steps(self.steps_per_epoch, use_graph)
+
+    def _graphs_by_default(self) -> bool:
+        """Step graphs unless asked otherwise: on a GPU with the HIP backend.  The eager torch oracle
+        (ops/ref.py) runs eagerly: on wide tables its step is tens of thousands of small ATen launches
+        (Python loops over ~770 spans), and capturing 8 of them into one graph crashed HIP's graph
+        instantiation (segfault in capture_end, 100k x 512 table, round 5)."""
+        return self.device.type == "cuda" and self.ops.name == "hip"
+
+    def prepare_graphs(self, steps: int | None = None, gen_rows: Sequence[int] = ()) -> None:
+        """Capture, ahead of the first round, every hipGraph that ``train_steps(steps)`` and
+        ``generate_decoded(n)`` for ``n`` in ``gen_rows`` will replay: the capture (one eager warm-up step
+        or pass plus the capture itself, ~40 ms for the Intrusion step graph) then happens at
+        initialisation instead of inside round 0's timed window.  Capturing never changes the training
+        state (``_capture_locked`` restores it).  No-op off the GPU / without graphs."""
+        if self.device.type != "cuda":
+            return
+        steps = self.steps_per_epoch if steps is None else int(steps)
+        if self.tables and steps > 0 and self._graphs_by_default():
+            U = max(1, int(self.cfg.graph_unroll))
+            if steps >= U and self._graph_key(U) not in self.graphs:
+                self._capture(U)
+            if steps % U and self._graph_key(1) not in self.graphs:
+                self._capture(1)
+        if self.gen_tables is not None and self.cfg.gen_graph and self.ops.name == "hip":
+            for n in gen_rows:
+                if n > 0 and n not in self._gen_graphs:
+                    self._capture_gen(int(n))
 
     def _graph_key(self, steps: int):
         """Captured step graphs are per (steps, clients): a batched engine whose clients hold different row

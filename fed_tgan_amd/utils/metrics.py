@@ -89,6 +89,56 @@ class PhaseTimer:
         return {f"t_{k}": v for k, v in self._last.items()}
 
 
+_CPU_STAT = None
+
+
+def cgroup_cpu_stat() -> Dict[str, int]:
+    """The process cgroup's CPU accounting: usage and CFS-bandwidth throttling counters (cgroup v2
+    ``cpu.stat``: usage_usec, nr_periods, nr_throttled, throttled_usec; v1 ``cpu.stat`` +
+    ``cpuacct.usage``).  Empty where the file is absent.  A round whose host issue time jumps while
+    ``throttled_usec`` grows was descheduled by the CPU quota, not slowed by the GPU."""
+    global _CPU_STAT
+    if _CPU_STAT is None:
+        _CPU_STAT = ""
+        for p in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"):
+            try:
+                with open(p):
+                    _CPU_STAT = p
+                    break
+            except OSError:
+                continue
+    if not _CPU_STAT:
+        return {}
+    out: Dict[str, int] = {}
+    try:
+        with open(_CPU_STAT) as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if v.strip().isdigit():
+                    out[k] = int(v)
+    except OSError:
+        return {}
+    if "throttled_time" in out and "throttled_usec" not in out:       # cgroup v1 (nanoseconds)
+        out["throttled_usec"] = out["throttled_time"] // 1000
+    return out
+
+
+def cpu_quota() -> Dict[str, float]:
+    """CPU quota of the process cgroup (cgroup v2 ``cpu.max`` / v1 cfs files) and the affinity size."""
+    import os
+    info: Dict[str, float] = {"affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 0,
+                              "cpu_count": os.cpu_count() or 0}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                info["quota_cpus"] = int(q) / int(per)
+                info["period_us"] = int(per)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
 class MetricsLog:
     def __init__(self, path: str):
         self.path = path

@@ -19,13 +19,22 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
 
 
-def _engine(precision="bf16", g_wt=False):
+def _engine(precision="bf16", g_wt=False, wide=False):
+    """wide: the reduced wide table (fed_tgan_amd.data.demo.wide_table) with the scattered one-hot weight
+    gradients forced on -- the step takes every kernel path that only the 100k x 512 config takes by
+    default (activation row kernels, chunk-split gradient-penalty scale, deep split-K D GEMMs)."""
     from fed_tgan_amd.ops import native
     native.require()
-    _, _, _, _, _, _, tr, X = small_table()
+    if wide:
+        from fed_tgan_amd.data.demo import wide_table
+        _, _, _, _, _, _, tr, X = wide_table(device="cuda:0")
+    else:
+        _, _, _, _, _, _, tr, X = small_table()
     torch.manual_seed(0)
-    eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, g_wt=g_wt), DEV, backend="hip",
-                      seed=11)
+    cfg = EngineConfig(batch_size=500, precision=precision, g_wt=g_wt or wide)
+    if wide:
+        cfg.onehot_wgrad_min = 1
+    eng = CTGANEngine(tr.layout, cfg, DEV, backend="hip", seed=11)
     eng.set_training_data(X)
     return eng, tr
 
@@ -48,9 +57,11 @@ def _rel(a, b):
 TOL = {"bf16": 5e-2, "fp32": 2e-3}
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
-def test_hip_d_update_matches_autograd(precision):
-    eng, tr = _engine(precision)
+@pytest.mark.parametrize("precision,wide", [("bf16", False), ("fp32", False), ("bf16", True), ("fp32", True)])
+def test_hip_d_update_matches_autograd(precision, wide):
+    eng, tr = _engine(precision, wide=wide)
+    if wide:
+        assert eng.K1 > 8192 and eng.Dd > 512       # chunk-split GP scale, activation row kernels
     B, nP = eng.B, eng.nP
     eng._d_prepare()
     torch.cuda.synchronize()
@@ -81,9 +92,22 @@ def test_hip_d_update_matches_autograd(precision):
         assert _rel(eng.g[n], t.grad) < TOL[precision], (n, _rel(eng.g[n], t.grad))
 
 
-@pytest.mark.parametrize("precision,g_wt", [("bf16", False), ("fp32", False), ("bf16", True), ("fp32", True)])
-def test_hip_g_update_matches_autograd(precision, g_wt):
-    eng, tr = _engine(precision, g_wt)
+@pytest.mark.parametrize("precision,g_wt,wide,row_mode", [
+    ("bf16", False, False, None), ("fp32", False, False, None), ("bf16", True, False, None), ("fp32", True, False, None),
+    ("bf16", True, True, None), ("fp32", True, True, None), ("fp32", True, True, 1)])
+def test_hip_g_update_matches_autograd(precision, g_wt, wide, row_mode):
+    prev = torch.ops.fedtgan.set_tuning("act_row_mode", row_mode) if row_mode is not None else None
+    try:
+        _g_update_vs_autograd(precision, g_wt, wide)
+    finally:
+        if prev is not None:
+            torch.ops.fedtgan.set_tuning("act_row_mode", prev)
+
+
+def _g_update_vs_autograd(precision, g_wt, wide):
+    eng, tr = _engine(precision, g_wt, wide)
+    if wide:
+        assert eng._onehot_w_ok(eng.p["G.out.W"])   # the scattered one-hot weight gradients run
     B, nP, Dd = eng.B, eng.nP, eng.Dd
     eng._d_step()
     before = {n: t.detach().clone() for n, t in eng.p.items()}
@@ -92,8 +116,25 @@ def test_hip_g_update_matches_autograd(precision, g_wt):
     x0 = eng.H[:, eng.off[0]:].clone()
     act_k = eng.Xg[:, :Dd].clone()
     logits_k = eng.logits.clone()
-    eng._g_update()
+    snap = []
+    if wide:
+        # the scattered one-hot gradient rows are cleared right after the Adam step: keep a copy to compare
+        real = eng.ops.onehot_wgrad
+
+        def spy(dys, ws, *a, zero=False, **k):
+            if zero:
+                snap.extend((w, w.clone()) for w in ws)
+            return real(dys, ws, *a, zero=zero, **k)
+        eng.ops.onehot_wgrad = spy
+    try:
+        eng._g_update()
+    finally:
+        if wide:
+            del eng.ops.onehot_wgrad
     torch.cuda.synchronize()
+    assert len(snap) == (len(eng.gdims) + 1 if wide else 0)
+    for w, saved in snap:
+        w.copy_(saved)
     G = Generator(eng.E + eng.C, eng.gdims, Dd).to(DEV)
     sd = {k: before[n] for k, n in eng.g_key_map()}
     for i in range(len(eng.gdims)):

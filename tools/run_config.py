@@ -69,6 +69,7 @@ def main():
     from fed_tgan_amd.fed.runtime import FedConfig, FedRuntime
     from fed_tgan_amd.models.engine import EngineConfig
     from fed_tgan_amd.parallel.comm import Comm
+    from fed_tgan_amd.utils.metrics import cpu_quota
 
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     spec = get_spec(args.spec)
@@ -110,7 +111,7 @@ def main():
             "mean_sec_per_epoch_after_first": round(sum(rt.round_times[1:]) / max(len(rt.round_times) - 1, 1), 4),
             "wall_s_incl_init": round(wall, 2),
             "init_s": {k: round(v, 3) for k, v in getattr(rt, "init_times", {}).items()},
-            "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"]}
+            "final_avg_jsd": lines[-1]["avg_jsd"], "final_avg_wd": lines[-1]["avg_wd"], "cpu": cpu_quota()}
     if args.engine:
         summ["engine_overrides"] = args.engine
     if args.tuning:
