@@ -90,12 +90,29 @@ struct ChainTail {
 thread_local ChainTail g_chain_tail{};
 thread_local fedtgan::GemmArgs g_chain_args{};
 
+// BatchNorm on load for the NEXT gemm() call of this thread (gemm_bnl_next): the ranges of op(A) that hold a
+// layer's pre-BatchNorm output, their statistics' source and where the consumer materialises relu(BN(a))
+struct BnlPending {
+  fedtgan::GemmArgs::BnLoad r[2];
+  int n, rpg;
+  float mom, eps;
+  float* out;
+  int ldo;
+  int64_t out_rows, out_cols;
+  int64_t nhat_rows[2];
+  int64_t part_numel[2];
+  bool active;
+};
+thread_local BnlPending g_bnl{};
+
 // drop every GEMM held by this thread (pairing, chain tail, Adam fusion) without launching it: called at
 // the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
 // (whose operand pointers may since have been freed) can never be launched or block the next step.
 // Returns the number of holds that were dropped.
 int64_t reset_held() {
-  const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0);
+  const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0) +
+                    (g_bnl.active ? 1 : 0);
+  g_bnl.active = false;
   has_held = false;
   held_stream = nullptr;
   g_adam_held.active = false;
@@ -119,6 +136,79 @@ int64_t set_client_batch(int64_t k, int64_t stride, int64_t seed_step, int64_t b
   cb.base = k > 1 ? reinterpret_cast<const char*>(base) : nullptr;
   cb.xcd = k > 1 ? fedtgan::g_xcd_clients : 0;
   return prev;
+}
+
+// The next gemm() of this thread stages relu(BatchNorm(a)) for op(A) columns [k0[j], k0[j] + width_j) (see
+// launch.h GemmArgs::bnl): part[j] = the producing GEMM's partials (None: mean / invstd are final), ptm[j] its
+// rows per tile; mean / invstd [2, width] (written by the consumer from partials); out (nullable): materialise
+// relu(BN(a)) (raw outside the ranges) as [M, K] rows, with nhat[j] [M, width_j] alongside.
+void gemm_bnl_next(const std::vector<optional<Tensor>>& part, const std::vector<Tensor>& mean,
+                   const std::vector<Tensor>& invstd, const std::vector<Tensor>& gamma, const std::vector<Tensor>& beta,
+                   const std::vector<Tensor>& rm, const std::vector<Tensor>& rv, const std::vector<optional<Tensor>>& nhat,
+                   const std::vector<int64_t>& k0, const std::vector<int64_t>& ptm, int64_t rpg, double momentum,
+                   double eps, const optional<Tensor>& out) {
+  const size_t n = k0.size();
+  TORCH_CHECK(n >= 1 && n <= 2 && part.size() == n && mean.size() == n && invstd.size() == n && gamma.size() == n &&
+                  beta.size() == n && rm.size() == n && rv.size() == n && nhat.size() == n && ptm.size() == n,
+              "gemm_bnl_next: one entry per range (1 or 2 ranges)");
+  TORCH_CHECK(!g_bnl.active, "gemm_bnl_next: a BatchNorm-on-load configuration is already pending");
+  BnlPending p{};
+  p.n = (int)n;
+  p.rpg = (int)rpg;
+  p.mom = (float)momentum;
+  p.eps = (float)eps;
+  for (size_t j = 0; j < n; ++j) {
+    fedtgan::GemmArgs::BnLoad& r = p.r[j];
+    const int64_t w = gamma[j].numel();
+    TORCH_CHECK(w >= 4 && w <= 256 && w % 4 == 0 && k0[j] >= 0 && k0[j] % 4 == 0, "gemm_bnl_next: width 4..256, multiple of 4; k0 % 4 == 0");
+    for (const Tensor* t : {&mean[j], &invstd[j]})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() >= 2 * w,
+                  "gemm_bnl_next: mean / invstd [2, width] fp32");
+    for (const Tensor* t : {&gamma[j], &beta[j], &rm[j], &rv[j]})
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == w,
+                  "gemm_bnl_next: gamma / beta / running stats [width] fp32");
+    r.part = nullptr;
+    p.part_numel[j] = 0;
+    if (part[j].has_value() && part[j]->defined()) {
+      TORCH_CHECK(part[j]->is_cuda() && part[j]->scalar_type() == at::kFloat && part[j]->is_contiguous() && ptm[j] >= 1,
+                  "gemm_bnl_next: partials");
+      r.part = part[j]->data_ptr<float>();
+      p.part_numel[j] = part[j]->numel();
+    }
+    r.mean = mean[j].data_ptr<float>();
+    r.invstd = invstd[j].data_ptr<float>();
+    r.gamma = gamma[j].data_ptr<float>();
+    r.beta = beta[j].data_ptr<float>();
+    r.rm = rm[j].data_ptr<float>();
+    r.rv = rv[j].data_ptr<float>();
+    r.k0 = (int)k0[j];
+    r.width = (int)w;
+    r.ptm = (int)ptm[j];
+    r.nhat = nullptr;
+    p.nhat_rows[j] = 0;
+    if (nhat[j].has_value() && nhat[j]->defined()) {
+      check_f32_2d(*nhat[j], "nhat");
+      TORCH_CHECK(nhat[j]->size(1) == w && ld_of(*nhat[j]) % 4 == 0 &&
+                      (reinterpret_cast<uintptr_t>(nhat[j]->data_ptr()) & 15) == 0,
+                  "gemm_bnl_next: nhat [M, width], 16-B aligned rows");
+      r.nhat = nhat[j]->data_ptr<float>();
+      r.ldn = ld_of(*nhat[j]);
+      p.nhat_rows[j] = nhat[j]->size(0);
+    }
+  }
+  p.out = nullptr;
+  if (out.has_value() && out->defined()) {
+    check_f32_2d(*out, "out");
+    TORCH_CHECK(ld_of(*out) % 4 == 0 && (reinterpret_cast<uintptr_t>(out->data_ptr()) & 15) == 0,
+                "gemm_bnl_next: out rows 16-B aligned");
+    for (size_t j = 0; j < n; ++j) TORCH_CHECK(p.r[j].nhat, "gemm_bnl_next: materialising needs nhat for every range");
+    p.out = out->data_ptr<float>();
+    p.ldo = ld_of(*out);
+    p.out_rows = out->size(0);
+    p.out_cols = out->size(1);
+  }
+  p.active = true;
+  g_bnl = p;
 }
 
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
@@ -232,15 +322,40 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     g.oh_off = oh_off->data_ptr<int>();
   }
   if (bn_part.has_value() && bn_part->defined()) {
-    TORCH_CHECK(tb && !ta && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && g.splitk == 1 &&
-                    (tile == 32 || tile == 64) && group == 0,
-                "gemm: BN partials need a plain unsplit C = A B^T + bias on 32/64 tiles");
+    TORCH_CHECK(!ta && !bin && !cbf && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && g.splitk == 1 &&
+                    (tile == 32 || tile == 64) && group == 0 && g.vec,
+                "gemm: BN partials need a plain unsplit C = A op(B) + bias on 32/64 tiles with 16-B operands");
     const int64_t tiles = (M + tile - 1) / tile;
     TORCH_CHECK(bn_part->is_cuda() && bn_part->scalar_type() == at::kFloat && bn_part->is_contiguous() &&
                     bn_part->numel() >= tiles * 6 * N, "gemm: bn_part must hold [m_tiles, 2, 3, N] floats");
     TORCH_CHECK(bn_rpg >= 1 && bn_rpg <= M, "gemm: bn_rpg");
     g.bn_part = fp(*bn_part);
     g.bn_rpg = (int)bn_rpg;
+  }
+  if (g_bnl.active) {
+    BnlPending& p = g_bnl;
+    p.active = false;      // consumed by this call whatever happens below
+    TORCH_CHECK(!ta && !bin && !cbf && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && g.splitk == 1 &&
+                    (tile == 32 || tile == 64) && group == 0 && !chain && g.vec && fedtgan::client_batch().k == 1,
+                "gemm: BatchNorm on load needs a plain unsplit C = A op(B) + bias (row-major fp32 A, 32/64 tiles, 16-B "
+                "operands, one client, unpaired)");
+    TORCH_CHECK(p.rpg >= 1 && p.rpg <= M && (!g.bn_part || g.bn_rpg == p.rpg), "gemm: BatchNorm on load rows per batch");
+    for (int j = 0; j < p.n; ++j) {
+      const fedtgan::GemmArgs::BnLoad& r = p.r[j];
+      TORCH_CHECK(r.k0 + r.width <= K, "gemm: BatchNorm-on-load range beyond K");
+      if (r.part) TORCH_CHECK(p.part_numel[j] >= ((M + r.ptm - 1) / r.ptm) * 6 * r.width, "gemm: partials too small");
+      if (p.out) TORCH_CHECK(p.nhat_rows[j] >= M, "gemm: nhat rows");
+      g.bnl[j] = r;
+    }
+    if (p.n == 2) TORCH_CHECK(p.r[0].k0 + p.r[0].width <= p.r[1].k0 || p.r[1].k0 + p.r[1].width <= p.r[0].k0,
+                              "gemm: BatchNorm-on-load ranges overlap");
+    if (p.out) TORCH_CHECK(p.out_rows >= M && p.out_cols >= K, "gemm: materialised rows [M, K]");
+    g.nbnl = p.n;
+    g.bn_rpg = p.rpg;
+    g.bnl_mom = p.mom;
+    g.bnl_eps = p.eps;
+    g.bnl_out = p.out;
+    g.bnl_ldo = p.ldo;
   }
   if (tile_cnt.has_value() && tile_cnt->defined() && g.splitk > 1) {
     // one arrival counter per output tile, all zero (the reducing workgroup re-zeroes its tile's)
@@ -1200,6 +1315,9 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("py_float(float x) -> str", &py_float);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
+  m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "
+        "Tensor[] rv, Tensor?[] nhat, int[] k0, int[] ptm, int rpg, float momentum, float eps, Tensor? out) -> ()",
+        &gemm_bnl_next);
   m.def("set_client_batch(int k, int stride, int seed_step, int base) -> int", &set_client_batch);
   m.def("check_status() -> int", &check_status);
   m.def("is_checked() -> bool", &is_checked);

@@ -156,6 +156,64 @@ __device__ __forceinline__ int lds_swz(int row) {
   return (3 * (row >> 4)) & (KC / 8 - 1);
 }
 
+// ----------------------------------------------------------------------------- BatchNorm on load (EK 5 / 6)
+// A generator layer's BatchNorm(train) + ReLU folded into its consumers (GemmArgs::bnl): the producing GEMM
+// stores the layer's pre-BN output a plus per-tile partial statistics (EK 4 / 5, bn_tile_partials), and every
+// GEMM that reads the layer's output stages relu(BN(a)) from a into LDS.  The per-column (mean, invstd, gamma,
+// beta) of both batches sit in an LDS table behind the stage buffers.  No BatchNorm launch and no extra pass
+// over the activations remain in the forward (the bn_relu_train launches were 2 x 7.7 us of the one-client step).
+constexpr int BNL_W = 256;                                    // widest range (host-checked)
+constexpr size_t BNL_TAB_BYTES = 2 * 2 * BNL_W * sizeof(float) * 4;   // [range][batch][column] float4
+
+struct BnlCtx {
+  const f32x4* tab;   // [(j * 2 + b) * BNL_W + c] = (mean, invstd, gamma, beta)
+  int nr, rpg;
+  int k0[2], w[2];
+  float* out;         // materialise this burst (nullptr: not this workgroup's burst)
+  int ldo;
+  float* nhat[2];
+  int ldn[2];
+};
+
+// 4 consecutive k of row m (k % 4 == 0; a range never splits a float4: k0 and width are multiples of 4).
+// ok[e]: element in range (others stay 0 and are not materialised).
+__device__ __forceinline__ void bnl_apply4(const BnlCtx& c, int m, int k, float (&x)[4], const bool (&ok)[4]) {
+  int j = -1, kk = 0;
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+    if (jj < c.nr && k >= c.k0[jj] && k < c.k0[jj] + c.w[jj]) {
+      j = jj;
+      kk = k - c.k0[jj];
+    }
+  const int b = m >= c.rpg ? 1 : 0;
+  if (j >= 0) {
+    float n[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 t = c.tab[(j * 2 + b) * BNL_W + kk + e];
+      n[e] = (x[e] - t[0]) * t[1];            // the bn_relu_train expressions
+      const float y = n[e] * t[2] + t[3];
+      x[e] = ok[e] ? (y > 0.f ? y : 0.f) : 0.f;
+    }
+    if (c.out && ok[0]) {
+      float* dst = c.nhat[j] + (size_t)m * c.ldn[j] + kk;
+      if (ok[3]) *reinterpret_cast<f32x4*>(dst) = f32x4{n[0], n[1], n[2], n[3]};
+      else
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (ok[e]) dst[e] = n[e];
+    }
+  }
+  if (c.out && ok[0]) {
+    float* dst = c.out + (size_t)m * c.ldo + k;
+    if (ok[3]) *reinterpret_cast<f32x4*>(dst) = f32x4{x[0], x[1], x[2], x[3]};
+    else
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (ok[e]) dst[e] = x[e];
+  }
+}
+
 template <int KC, bool ROWMAJ, int R>
 struct Chunk {
   static constexpr int NV = R * KC / (4 * NT);   // float4 per thread
@@ -254,6 +312,33 @@ struct Chunk {
           *reinterpret_cast<uint32_t*>(&s[row * (KC + 8) + pk]) =
               pack_bf16x2(ok_cm(i, 0, e) ? v[2 * i][e] : 0.f, ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f);
         }
+      }
+    }
+  }
+
+  // BatchNorm on load (row-major operand only): relu(BN(a)) of the ranges in bc, staged as bf16 / fp32
+  template <bool BF16>
+  __device__ __forceinline__ void store_bnl(void* s_, const BnlCtx& bc) const {
+    static_assert(ROWMAJ, "BatchNorm on load stages a row-major A");
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
+      float x[4];
+      bool ok[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ok[e] = ok_rm(i, e);
+        x[e] = ok[e] ? v[i][e] : 0.f;
+      }
+      bnl_apply4(bc, r0 + r, k0 + 4 * q, x, ok);
+      if constexpr (BF16) {
+        uint16_t* s = reinterpret_cast<uint16_t*>(s_);
+        *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+      } else {
+        float* s = reinterpret_cast<float*>(s_);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[r * (KC + 1) + 4 * q + e] = x[e];
       }
     }
   }
@@ -436,6 +521,68 @@ __device__ __forceinline__ void bn_tile_partials(const GemmArgs& g, const f32x4 
   }
 }
 
+__device__ __forceinline__ void bnl_merge(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
+  const float nt = n + nb;
+  if (nt > 0.f) {
+    const float d = mub - mu;
+    mu += d * (nb / nt);
+    m2 += m2b + d * d * (n * nb / nt);
+    n = nt;
+  }
+}
+
+// Prologue of a BatchNorm-on-load GEMM (EK 5 / 6): the (mean, invstd, gamma, beta) table of every range for the
+// batches of this tile's rows.  From partials: merged in producer-tile order (every workgroup gets the same
+// bits); tile (0, 0, 0) merges both batches, publishes mean / invstd and advances the running statistics
+// batch after batch, as bn_relu_train does (biased batch variance; running variance unbiased).
+template <int TM>
+__device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin, f32x4* tab) {
+  const int rpg = g.bn_rpg, M = g.M;
+  const int ng = M > rpg ? 2 : 1;
+  const int blo = m0 >= rpg ? 1 : 0, bhi = (min(m0 + TM, M) - 1) >= rpg ? 1 : 0;
+  for (int j = 0; j < g.nbnl; ++j) {
+    const GemmArgs::BnLoad& L = g.bnl[j];
+    for (int c = threadIdx.x; c < L.width; c += NT) {
+      const float gm = L.gamma[c], bt = L.beta[c];
+      if (L.part) {
+        float mu[2] = {0.f, 0.f}, var[2] = {0.f, 0.f};
+        for (int b = 0; b < ng; ++b) {
+          if (!fin && (b < blo || b > bhi)) continue;
+          const int t0 = b ? rpg / L.ptm : 0, t1 = b ? (M - 1) / L.ptm : (min(rpg, M) - 1) / L.ptm;
+          float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll 8
+          for (int t = t0; t <= t1; ++t) {
+            const float* p = L.part + ((size_t)(t * 2 + b) * 3) * L.width + c;
+            bnl_merge(n, mean, m2, p[0], p[L.width], p[2 * (size_t)L.width]);
+          }
+          mu[b] = mean;
+          var[b] = n > 0.f ? m2 / n : 0.f;
+          const float is = rsqrtf(var[b] + g.bnl_eps);
+          tab[(j * 2 + b) * BNL_W + c] = f32x4{mean, is, gm, bt};
+          if (fin) {
+            L.mean[(size_t)b * L.width + c] = mean;
+            L.invstd[(size_t)b * L.width + c] = is;
+          }
+        }
+        if (fin) {
+          const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnl_mom;
+          float rm = L.rm[c], rv = L.rv[c];
+          for (int b = 0; b < ng; ++b) {
+            rm = (1.f - mom) * rm + mom * mu[b];
+            rv = (1.f - mom) * rv + mom * var[b] * unb;
+          }
+          L.rm[c] = rm;
+          L.rv[c] = rv;
+        }
+      } else {
+        for (int b = blo; b <= bhi; ++b)
+          tab[(j * 2 + b) * BNL_W + c] = f32x4{L.mean[(size_t)b * L.width + c], L.invstd[(size_t)b * L.width + c], gm, bt};
+      }
+    }
+  }
+  __syncthreads();
+}
+
 template <bool F32, int TM, int TN, bool BIN = false>
 struct Cfg {
   // K values per burst: (64 + 64) rows x KC fp32 = 64 KB in flight per workgroup.  (KC = 256
@@ -591,9 +738,32 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       b_.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
     }
   };
+  // BatchNorm on load (EK 5 / 6): the stats table behind the two stage buffers; burst i of A is materialised
+  // (GemmArgs::bnl_out) by the workgroups of N tile i % gx
+  constexpr bool BNL = (EK == 5 || EK == 6);
+  BnlCtx bc{};
+  if constexpr (BNL) {
+    static_assert(!TA && !BIN, "BatchNorm on load: row-major fp32 A");
+    bc.tab = reinterpret_cast<const f32x4*>(smem + 2 * C::STAGE);
+    bc.nr = g.nbnl;
+    bc.rpg = g.bn_rpg;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bc.k0[j] = g.bnl[j].k0;
+      bc.w[j] = j < g.nbnl ? g.bnl[j].width : 0;
+      bc.nhat[j] = g.bnl[j].nhat;
+      bc.ldn[j] = g.bnl[j].ldn;
+    }
+    bc.ldo = g.bnl_ldo;
+  }
   auto stage_ab = [&](const CA& a_, const CB& b_, int st) {
     unsigned char* base = smem + st * C::STAGE;
-    if constexpr (F32) {
+    if constexpr (BNL) {
+      bc.out = (g.bnl_out && ((a_.k0 - kb) / KC) % gx == bx) ? g.bnl_out : nullptr;
+      a_.template store_bnl<!F32>(base, bc);
+      if constexpr (F32) b_.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
+      else b_.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
+    } else if constexpr (F32) {
       a_.store_f32(reinterpret_cast<float*>(base));
       b_.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
     } else if constexpr (BIN) {
@@ -665,6 +835,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     auto stage2 = [&](int s) { stage_ab(ca2, cb2, s); };
     issue(kb);
     if (kb + KC < ke) issue2(kb + KC);
+    if constexpr (BNL) bnl_prologue<TM>(g, m0, bx == 0 && by == 0 && bz == 0, reinterpret_cast<f32x4*>(smem + 2 * C::STAGE));
     for (int k0 = kb; k0 < ke; k0 += 2 * KC) {
       stage(st);
       __syncthreads();
@@ -681,6 +852,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
   } else {
     issue(kb);
+    if constexpr (BNL) bnl_prologue<TM>(g, m0, bx == 0 && by == 0 && bz == 0, reinterpret_cast<f32x4*>(smem + 2 * C::STAGE));
     for (int k0 = kb; k0 < ke; k0 += KC) {
       stage(st);
       __syncthreads();
@@ -732,7 +904,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       }
   }
   // weight-gradient instantiations (op(A) = A^T) have a plain epilogue (host-checked): no epilogue code at all
-  constexpr bool PLAIN = TA || EK == 1;
+  constexpr bool PLAIN = TA || EK == 1 || EK >= 4;   // (EK 4-6: BatchNorm producers / consumers, plain C + bias)
   constexpr bool MASKED = !TA && EK == 3;
   const uint64_t step = (!PLAIN && g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   if constexpr (BIN && TM <= 64) if (g.c16) {
@@ -898,8 +1070,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
                PLAIN ? v : (MASKED ? v * g.ms[(size_t)m * g.ldms + n] : apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n)),
                g.wt);
       }
-  if constexpr (!TA && TB) {   // (host: BN partials need C = A B^T)
-    if (g.bn_part && gz == 1) bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
+  if constexpr (EK == 4 || EK == 5) {   // (host: BN partials need a plain unsplit C = A op(B) + bias)
+    bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
   }
 }
 
@@ -982,6 +1154,7 @@ static size_t gemm_smem_bytes(const GemmArgs& g) {
   else stage = T == 32 ? Cfg<false, 32, 32>::STAGE : (T == 128 ? Cfg<false, 128, 128>::STAGE : Cfg<false, 64, 64>::STAGE);
   const int KC = g.f32 ? Cfg<true, 64, 64>::KC / (T >= 128 ? 2 : 1) : Cfg<false, 64, 64>::KC / (T >= 128 ? 2 : 1);
   const bool one_burst = g.kchunk <= KC;
+  if (g.nbnl > 0) return 2 * stage + BNL_TAB_BYTES;   // the BatchNorm-on-load table sits behind two stages
   return (one_burst && T <= 64) ? stage : 2 * stage;
 }
 
@@ -1239,6 +1412,8 @@ static dim3 gemm_prepare(GemmArgs& g) {
 
 // epilogue kind of a launch (gemm_tile's EK): a split-K slice reduced by its own launch, a plain epilogue, or any
 static int gemm_ek(const GemmArgs& g) {
+  if (g.nbnl > 0) return g.bn_part ? 5 : 6;    // BatchNorm on load (+ partials of this GEMM's own output)
+  if (g.bn_part) return 4;                     // BatchNorm partials of the output
   if (g.splitk > 1 && !g.red_inl) return 2;
   if (g.splitk > 1) return 0;   // (in-launch reduction: the generic body)
   return g.epi == EPI_NONE ? 1 : (g.epi == EPI_MASK ? 3 : 0);
@@ -1254,6 +1429,30 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
     return;
   }
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
+  if constexpr (!BATCH) {
+    const int ek = gemm_ek(g);
+    if (ek >= 4) {   // BatchNorm producers / consumers: row-major A, 32 / 64 tiles, 16-B operands (host-checked)
+#define FEDTGAN_GEMM_BN(F, TT, EKV)                                                                              \
+  if (g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, true, TT, TT, false, false, EKV>), grid, block, lds, stream, g); \
+  else hipLaunchKernelGGL((gemm_kernel<false, false, F, true, TT, TT, false, false, EKV>), grid, block, lds, stream, g);
+#define FEDTGAN_GEMM_BN_EK(F, TT) \
+  if (ek == 4) {                  \
+    FEDTGAN_GEMM_BN(F, TT, 4)     \
+  } else if (ek == 5) {           \
+    FEDTGAN_GEMM_BN(F, TT, 5)     \
+  } else {                        \
+    FEDTGAN_GEMM_BN(F, TT, 6)     \
+  }
+      if (g.f32) {
+        if (T == 32) { FEDTGAN_GEMM_BN_EK(true, 32) } else { FEDTGAN_GEMM_BN_EK(true, 64) }
+      } else {
+        if (T == 32) { FEDTGAN_GEMM_BN_EK(false, 32) } else { FEDTGAN_GEMM_BN_EK(false, 64) }
+      }
+#undef FEDTGAN_GEMM_BN_EK
+#undef FEDTGAN_GEMM_BN
+      return;
+    }
+  }
 // (op(A) = A^T layouts are plain whatever EK says; a split one keeps the generic body)
 #define FEDTGAN_GEMM_LAYOUTS(F, V, TT, EK)                                                                        \
   if (!g.ta && g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, V, TT, TT, false, BATCH, EK>), grid, block, lds, stream, g);       \
@@ -1315,7 +1514,9 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     t.cstride = g.cstride;      // (the tail was never prepared: it shares the head's client layout)
     t.seed_step = g.seed_step;
     t.nclient = g.nclient;
-    t.chain_co = g_chain_coalesced && (g.N % 4 == 0);
+    // float4 loads from t.b + jc * t.ldb + k: the row stride and the base must keep them 16-B aligned
+    t.chain_co = g_chain_coalesced && (g.N % 4 == 0) && (t.ldb % 4 == 0) &&
+                 ((reinterpret_cast<uintptr_t>(t.b) & 15) == 0);
     const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS, g.nclient), block(256);
     const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
 #define FEDTGAN_CHAIN(S)                                                                                 \

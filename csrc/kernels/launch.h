@@ -86,6 +86,30 @@ struct GemmArgs {
   float* bn_part;
   int bn_rpg;
   int oh_c;       // width of the one-hot block (checked build: gather index bound)
+  // BatchNorm(train) + ReLU of earlier generator layers applied to op(A) while it is staged (gemm_tile EK 5 / 6;
+  // nbnl = 0: none).  op(A) = A row-major, unsplit, C = A op(B) + bias.  Range j covers A's columns
+  // [k0, k0 + width) -- a layer's PRE-BatchNorm output a -- and the GEMM multiplies relu(BN(a)) instead:
+  //   nhat = (a - mean_b) * invstd_b,  y = relu(nhat * gamma + beta)      (b: the row's batch, bn_rpg rows each)
+  // With `part` (the producing GEMM's per-tile partials, bn_part layout, ptiles row tiles of ptm rows) every
+  // workgroup merges the batch statistics itself (Chan, tile order) and tile (0, 0) writes mean / invstd
+  // [2][width] and updates the running statistics (batch after batch); without it mean / invstd are final.
+  // bnl_out (nullable): the workgroups materialise relu(BN(a)) (and the raw columns outside the ranges) at
+  // bnl_out[m * bnl_ldo + k] and nhat at nhat[m * ldn + c] -- burst i by the workgroups of N tile i % gx.
+  struct BnLoad {
+    const float* part;
+    float* mean;
+    float* invstd;
+    const float* gamma;
+    const float* beta;
+    float* rm;
+    float* rv;
+    float* nhat;
+    int ldn, k0, width, ptiles, ptm;
+  } bnl[2];
+  int nbnl;
+  float bnl_mom, bnl_eps;
+  float* bnl_out;
+  int bnl_ldo;
   // Split-K reduced inside the GEMM launch (nullable): one arrival counter per output tile, zero
   // between launches.  Every K-slice workgroup publishes its slab write-through and takes a ticket;
   // the one that completes a tile sums the tile's slabs and applies the epilogue (no

@@ -148,17 +148,6 @@ def device_index(local: int, ngpu: int, colocated: bool, mode: str = "fedavg") -
     return local % ngpu if (colocated or mode == "mdgan") else max(local - 1, 0) % ngpu
 
 
-def clients_own_gpus(world: int, colocated: bool) -> bool:
-    """Does every client rank of this node get a GPU no other client uses (RCCL: one rank per device)?
-    A dedicated federator (rank 0, not a client) may share one."""
-    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
-    if not n:
-        return False
-    clients = range(world) if colocated else range(1, world)
-    idx = [device_index(r, n, colocated) for r in clients]
-    return len(set(idx)) == len(idx)
-
-
 def gpus_shared(world: int, colocated: bool, mode: str = "fedavg") -> bool:
     """Will several ranks of this node run on one GPU (a dedicated federator next to client 1, or
     more clients than GPUs)?"""
@@ -213,16 +202,14 @@ def run_rank(rank: int, args, on_done=None) -> None:
     client_ranks = list(range(world)) if colocated else list(range(1, world))
     data_backend = args.data_backend
     if data_backend == "auto":
-        if args.mode == "mdgan":
-            data_backend = "nccl" if (device.type == "cuda" and world <= torch.cuda.device_count()) else "gloo"
-        else:
-            # RCCL among the client ranks whenever every client has a GPU of its own; a dedicated federator
-            # stays outside the RCCL group and receives the aggregate from the first client
-            # (Comm.share_with_federator)
-            data_backend = "nccl" if (device.type == "cuda" and clients_own_gpus(world, colocated)) else "gloo"
-    if not args.quiet:
-        print(f"[rank {rank}] data plane {data_backend} over client ranks {client_ranks}", flush=True)
+        # agreed by every rank over the gloo control plane (Comm._vote_data_backend): RCCL among the client
+        # ranks (MD-GAN: among all ranks) when each of them has a GPU of its own, gloo everywhere otherwise.  A
+        # dedicated federator stays outside the RCCL group and receives the aggregate from the first client
+        # (Comm.share_with_federator)
+        data_backend = "auto_all" if args.mode == "mdgan" else "auto"
     comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
+    if not args.quiet:
+        print(f"[rank {rank}] data plane {comm.data_backend} over client ranks {client_ranks}", flush=True)
     try:
         if args.local_clients:      # K clients as threads of this rank: clients rank*K .. rank*K+K-1
             from .fed.local import run_local_emulation

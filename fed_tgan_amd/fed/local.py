@@ -24,7 +24,6 @@ from typing import Any, List, Optional
 import torch
 
 from ..parallel.comm import Comm
-from ..utils.devsync import device_sync
 
 
 class LocalGroup:
@@ -172,11 +171,25 @@ class ThreadComm(Comm):
         self.g.wait()
 
     def gather_rows(self, t, counts, ranks, dst: int = 0, to_host: bool = True):
-        # (threads share host memory: the rows always come back as host tensors)
-        parts = self.all_gather_object(t.cpu())
-        if self.rank != dst:
-            return None
-        return torch.cat([parts[r][:n] for r, n in zip(ranks, counts)])
+        """The threads' row blocks concatenated on ``dst``'s stream: ``dst`` waits for each thread's rows
+        through an event (no host synchronisation), marks them in use by its stream (they are freed by
+        their own threads later), and copies the result to the host once if ``to_host``."""
+        self.g.slots[self.rank] = (t, _stream_event(t))
+        self.g.wait()
+        out = None
+        if self.rank == dst:
+            parts = list(self.g.slots)
+            if t.is_cuda:
+                cur = torch.cuda.current_stream(t.device)
+                for p, ev in parts:
+                    if ev is not None:
+                        cur.wait_event(ev)
+                    p.record_stream(cur)
+            out = torch.cat([parts[r][0][:n] for r, n in zip(ranks, counts)])
+            if to_host:
+                out = out.cpu()
+        self.g.wait()           # every thread keeps its rows referenced until dst has enqueued its reads
+        return out
 
     def gather_bytes(self, payload, dst: int = 0):
         out = self.all_gather_object(payload)
@@ -237,10 +250,6 @@ class HierComm(Comm):
         self.g.wait()
         return out
 
-    def _sync(self):
-        if self.device.type == "cuda":
-            device_sync(self.device)
-
     # ---- control plane
     def all_gather_object(self, obj):
         local = self._tgather(obj)
@@ -261,17 +270,34 @@ class HierComm(Comm):
         self._lead(lambda: self.outer.heartbeat(timeout_s))
 
     def broadcast_tensor(self, t, src: int = 0):
-        self._sync()
+        """The source thread's copy is ordered to thread 0 and from thread 0 to every thread by stream
+        events; the process-level broadcast stages the tensor through host memory (gloo), which waits for
+        thread 0's stream only -- no device-wide synchronisation."""
         if self.t == src % self.k:
-            self.g.result = t.detach().clone()
+            c = t.detach().clone()
+            self.g.result = (c, _stream_event(c))
+        self.g.wait()
+        shared = self.g.result
         self.g.wait()
 
         def bcast():
-            v = self.outer.broadcast_tensor(self.g.result, src=src // self.k)
-            self._sync()
-            return v
-        t.copy_(self._lead(bcast))
-        self._sync()
+            c, ev = shared
+            if ev is not None and self.t != src % self.k:
+                torch.cuda.current_stream(t.device).wait_event(ev)
+                c.record_stream(torch.cuda.current_stream(t.device))
+            v = self.outer.broadcast_tensor(c, src=src // self.k)
+            return v, _stream_event(v)
+        v, ev = self._lead(bcast)
+        if ev is not None and self.t != 0:
+            torch.cuda.current_stream(t.device).wait_event(ev)
+            v.record_stream(torch.cuda.current_stream(t.device))   # (allocated on the source thread's stream)
+        t.copy_(v)
+        done = self._tgather(_stream_event(t))
+        if self.t == 0 and t.is_cuda:       # v stays alive until every thread's stream has read it
+            cur = torch.cuda.current_stream(t.device)
+            for e in done:
+                if e is not None:
+                    cur.wait_event(e)
         self.g.wait()
         return t
 
@@ -312,8 +338,8 @@ class HierComm(Comm):
             return flat
         return stream_reduce(self.g, self.t, flat, weight, outer=lambda acc: self.outer.weighted_all_reduce(acc, 1.0))
 
-    def share_with_federator(self, flat, federator: int = 0):
-        return flat         # co-located: the federator is a client and already holds the aggregate
+    def share_with_federator(self, flat, federator: int = 0, extra=None):
+        return False        # co-located: the federator is a client and already holds the aggregate
 
     def gather_rows(self, t, counts, ranks, dst: int = 0, to_host: bool = True):
         """The process' client shares are concatenated on its GPU, then one process-level gather."""

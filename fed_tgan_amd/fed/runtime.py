@@ -564,11 +564,18 @@ class FedRuntime:
                           "vocabs": [[v.column_name, v.tolist()] for v in self.vocabs]})
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        # the request goes through a file and the helper's stderr into another: no pipe that this process
+        # must write (the wide table's vocabularies are large) or drain (a chatty helper would block on a
+        # full pipe) while it initialises
+        import tempfile
         try:
-            p = subprocess.Popen([sys.executable, "-m", "fed_tgan_amd.data.vocab"], stdin=subprocess.PIPE,
-                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
-            p.stdin.write(req.encode())
-            p.stdin.close()
+            with tempfile.TemporaryFile() as f:
+                f.write(req.encode())
+                f.flush()
+                f.seek(0)
+                self._le_err = tempfile.TemporaryFile()
+                p = subprocess.Popen([sys.executable, "-m", "fed_tgan_amd.data.vocab"], stdin=f,
+                                     stdout=subprocess.DEVNULL, stderr=self._le_err, env=env)
             self._le_proc = p
         except OSError:
             self._le_proc = None
@@ -580,12 +587,16 @@ class FedRuntime:
         self._le_proc = None
         if p is not None:
             try:
-                _, err = p.communicate(timeout=120)
+                p.wait(timeout=120)
                 if p.returncode == 0 and os.path.exists(self._label_encoder_path()):
                     return self._label_encoder_path()
-                print(f"[init] label-encoder helper failed ({p.returncode}): {err.decode()[-300:]}", flush=True)
+                self._le_err.seek(0)
+                err = self._le_err.read().decode(errors="replace")
+                print(f"[init] label-encoder helper failed ({p.returncode}): {err[-300:]}", flush=True)
             except Exception:            # noqa: BLE001 - fall back to an in-process write
                 p.kill()
+            finally:
+                self._le_err.close()
         from ..data.vocab import write_label_encoders
         return write_label_encoders(self._label_encoder_path(), self.vocabs)
 
@@ -606,7 +617,18 @@ class FedRuntime:
         with self._sub("allreduce"):
             c.weighted_all_reduce(self.engine.flat, w)
         with self._sub("share"):
-            c.share_with_federator(self.engine.flat, self.federator)
+            # a dedicated federator (RCCL among the clients) gets the clients' mean last-step losses with the
+            # aggregate: one device all-reduce and the same message, no host round trip per client
+            m = None
+            if self.federator not in c.client_ranks and c.data_backend == "nccl" and c.dist_active:
+                m = self._loss_buf
+                if self.is_client:
+                    m.copy_(self.engine.metrics.detach().view(-1))
+                    c.client_mean(m)
+            shared = c.share_with_federator(self.engine.flat, self.federator, extra=m)
+            self._losses_shared = shared and m is not None
+            if self._losses_shared and self.is_fed:
+                self._losses = m.cpu()   # (the federator's stream was synchronised by the receive)
         # num_batches_tracked: weighted average of every client's counter, truncated (reference cast)
         ep = self.engine
         counts = np.asarray([2 * s for s in self.steps], dtype=np.float64) * (self._epoch_done)
@@ -756,11 +778,23 @@ class FedRuntime:
         self._sync_losses()
         return dt
 
+    @property
+    def _loss_buf(self) -> torch.Tensor:
+        """Device buffer of the four last-step loss terms (loss_d, pen, loss_g, cond CE), float32."""
+        if getattr(self, "_lbuf", None) is None:
+            self._lbuf = torch.zeros(4, dtype=torch.float32, device=self.engine.flat.device)
+        return self._lbuf
+
     def _sync_losses(self):
-        """Collective when the federator holds no data: the clients' last-step losses, averaged."""
+        """Collective when the federator holds no data: the clients' last-step losses, averaged.  With an
+        RCCL data plane they already travelled with the aggregate (``aggregate``); on gloo they take one
+        host all-reduce over the control plane."""
         c = self.comm
         if c.world_size == 1 or self.federator in c.client_ranks:
             self._losses = None
+            return
+        if getattr(self, "_losses_shared", False):
+            self._losses_shared = False
             return
         m = self.engine.metrics.detach().cpu().double() if self.is_client else torch.zeros(4, dtype=torch.float64)
         c.all_reduce_cpu(m)

@@ -139,6 +139,12 @@ class EngineConfig:
     # zero between steps).  The wide table's G.out gradient: 7,018 x 7,402 dense (228 us) -> 7,018 x 640 + 500
     # scattered rows.  0 = always dense.
     onehot_wgrad_min: int = 1 << 20
+    # HIP, paired step, one-hot conditions, <= 2 hidden generator layers of <= 256 units: each generator layer's
+    # BatchNorm(train) + ReLU is folded into the GEMMs around it instead of a launch of its own (K6).  The layer's
+    # GEMM stores its pre-BN output plus per-tile partial statistics; the next layer's GEMM and the output GEMM
+    # merge those statistics in their prologue and stage relu(BN(a)) from the pre-BN values as they load them;
+    # the output GEMM also writes relu(BN(a)) and nhat back for the backward.  Removes both bn_relu_train launches.
+    bn_fold: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -425,7 +431,23 @@ class CTGANEngine:
         # generator forward buffers hold two batches: rows [0, B) the D phase, [B, 2B) the G phase.
         # The paired prepare runs both through ONE M = 2B GEMM chain (BN statistics per batch);
         # the per-phase paths use the G-phase rows, which are also what the G backward reads.
-        self.H2 = _padded_rows(2 * B, self.Hw, dev)
+        # BatchNorm folded into the generator GEMMs (EngineConfig.bn_fold): the layers' pre-BN outputs and z live
+        # in Hp = [a_{L-1} | ... | a_0 | z], columns [Hw, Hw + c0) of the same rows as H (one row stride, so the
+        # sampler writes z there and the condition block into H in one launch); the output GEMM materialises
+        # relu(BN(a)) and z into H for the backward
+        c0 = self.c_cols[0]
+        self._fold_static = (self.ops.name == "hip" and self.use_onehot and bool(cfg.bn_fold) and
+                             1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
+                             all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
+        if self._fold_static:
+            hw4 = _ceil4(self.Hw)
+            big = _padded_rows(2 * B, hw4 + c0, dev)
+            self.H2 = big[:, :self.Hw]
+            self.Hp2 = big[:, hw4:hw4 + c0]
+            self._hp_off = hw4           # z's column in the big rows: hw4 + off[0]
+            self._bn_part = [z(-(-2 * B // 32) * 6 * g) for g in self.gdims]   # 32-row tiles at most
+        else:
+            self.H2 = _padded_rows(2 * B, self.Hw, dev)
         self.abuf2 = [z(2 * B, g) for g in self.gdims]
         self.nhat2 = [z(2 * B, g) for g in self.gdims]
         self.bn_mean2 = [z(2, g) for g in self.gdims]
@@ -583,6 +605,9 @@ class CTGANEngine:
         cond: the rows' (col, opt) int32 condition indices -- the conditional block of H is then
         applied as a one-hot gather instead of a dense K range (``EngineConfig.onehot``)."""
         o = self.ops
+        if training and paired and self._fold_on():
+            self._g_forward_fold(logits, act_out, stream_id, slerp, cond)
+            return
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
             x, W, oh = self._g_in(H, a, self.p[f"G.{i}.W"], cond)
@@ -599,6 +624,51 @@ class CTGANEngine:
         else:
             o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
                               slerp=slerp, onehot=oh)
+
+    def _fold_on(self) -> bool:
+        """EngineConfig.bn_fold applies to this launch sequence (one client, one stream, paired step)."""
+        return self._fold_static and self.lanes is None and self.batch is None and \
+            getattr(self.ops, "batch_k", 1) == 1 and bool(self.cfg.paired)
+
+    def _g_forward_fold(self, logits, act_out, stream_id, slerp, cond):
+        """The paired training forward with every BatchNorm folded into the generator GEMMs (EngineConfig.bn_fold):
+        layer i's GEMM reads Hp[:, off[i]:c0] -- layer i-1's pre-BN output staged as relu(BN(.)) from the partial
+        statistics its GEMM wrote -- and stores its own pre-BN output and partials; the output GEMM stages every
+        layer through its BatchNorm (the last from partials, the others from the statistics their first consumer
+        published) and materialises relu(BN(a)), z and nhat into H / nhat for the backward.  Same math as
+        linear_bn_relu + bn_relu_train (batch statistics per batch, running statistics batch after batch)."""
+        o, p = self.ops, self.p
+        Hp, c0, L = self.Hp2, self.c_cols[0], len(self.gdims)
+        rpg, mom, eps = self.B, self.cfg.bn_momentum, self.cfg.bn_eps
+        ptm = []
+
+        def bn_args(j, from_part):
+            return (self._bn_part[j] if from_part else None, self.bn_mean2[j], self.bn_invstd2[j], p[f"G.{j}.gamma"],
+                    p[f"G.{j}.beta"], p[f"G.{j}.rm"], p[f"G.{j}.rv"])
+
+        for i in range(L):
+            a, b_ = self.off[i], self.off[i + 1]
+            x, W, oh = self._g_in(Hp, a, p[f"G.{i}.W"], cond)
+            tile, _ = o.gemm_plan(x.shape[0], W.shape[0], x.shape[1])
+            tile = min(tile, 64)
+            if i > 0:       # layer i-1's BatchNorm, applied while this GEMM stages its output (its first consumer)
+                part, mean, istd, gm, bt, rm, rv = bn_args(i - 1, True)
+                o.gemm_bnl_next([part], [mean], [istd], [gm], [bt], [rm], [rv], [None], [0], [ptm[i - 1]], rpg, mom, eps)
+            o.gemm(x, W, Hp[:, b_:a], tb=True, bias=p[f"G.{i}.b"], onehot=oh, bn_part=self._bn_part[i], bn_rpg=rpg,
+                   tile=tile, splitk=1)
+            ptm.append(tile)
+        x, W, oh = self._g_in(Hp, 0, p["G.out.W"], cond)
+        cols = [bn_args(j, j == L - 1) for j in range(L)]
+        tile, _ = o.gemm_plan(x.shape[0], W.shape[0], x.shape[1])
+        o.gemm_bnl_next([c[0] for c in cols], [c[1] for c in cols], [c[2] for c in cols], [c[3] for c in cols],
+                        [c[4] for c in cols], [c[5] for c in cols], [c[6] for c in cols],
+                        [self.nhat2[j] for j in range(L)], [self.off[j + 1] for j in range(L)], ptm, rpg, mom, eps,
+                        out=self.H2[:, :c0])
+        if act_out is None:
+            o.gemm(x, W, logits, tb=True, bias=p["G.out.b"], onehot=oh, tile=min(tile, 64), splitk=1)
+        else:
+            o.linear_activate(x, W, p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
+                              slerp=slerp, onehot=oh, tile=min(tile, 64), splitk=1)
 
     def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None):
         """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
@@ -696,7 +766,11 @@ class CTGANEngine:
         updated D batch first, then G batch.  Halves the generator-side launches of a step and
         doubles their workgroups (M = 1000 fills the chip better than M = 500)."""
         o, B = self.ops, self.B
-        o.sample_train(self.tables, self.H2, self.z_cols, self.c_cols, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
+        h, zc = self.H2, self.z_cols
+        if self._fold_on():     # z goes to the pre-BN rows Hp (same row stride: one sampler launch)
+            h = self.H2.as_strided((2 * B, self._hp_off + self.c_cols[0]), self.H2.stride(), self.H2.storage_offset())
+            zc = (self._hp_off + self.z_cols[0], self._hp_off + self.z_cols[1])
+        o.sample_train(self.tables, h, zc, self.c_cols, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
                        self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
                        zero_metrics=True, stream_id=1)
         self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
@@ -1028,13 +1102,16 @@ class CTGANEngine:
         snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            self._one_step()
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        # restore state so the warm-up step does not count
-        for dst, src in zip(state, snap):
-            dst.copy_(src)
+        try:
+            with torch.cuda.stream(s):
+                self._one_step()
+        finally:
+            # restore the state so the warm-up step does not count -- also when it raised part-way (e.g. a
+            # batched arena slab overflow): the caller may fall back to other engines that copy this state
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            for dst, src in zip(state, snap):
+                dst.copy_(src)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
             for _ in range(steps):      # every step re-reads the device RNG/step counters

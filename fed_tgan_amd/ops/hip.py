@@ -254,7 +254,7 @@ class HipOps:
     # ------------------------------------------------------------------ GEMM
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
              slope=0.2, p_drop=0.5, stream_id=0, bn=None, bn_eps=1e-5, head=None, group=0, onehot=None,
-             bn_part=None, bn_rpg=0, tile=None, chain=False):
+             bn_part=None, bn_rpg=0, tile=None, chain=False, splitk=None):
         """C = epi(alpha op(A) op(B) + beta C + bias [+ onehot]).  head = (coef [M], v [N], A_out [M, N]):
         with the LeakyReLU+dropout epilogue also A_out = coef v^T * mask-slopes (D's head seed).
         onehot = (W_c [N, C], col [M], opt [M], cond_offset[, transposed]): A holds only the dense input
@@ -287,7 +287,7 @@ class HipOps:
         kc = 64 if self.f32 else 128
         tile_p, sk = _plan(M, N, K, kc, self._plan_clients())
         tile = self.tile_override or tile or tile_p
-        sk = _effective_splits(K, self.split_override or sk, kc)
+        sk = _effective_splits(K, splitk or self.split_override or sk, kc)
         if c.dtype == torch.bfloat16:
             sk = 1          # a bf16 output is written by the GEMM's own epilogue
         ws = cnt = None
@@ -302,6 +302,19 @@ class HipOps:
                     *(onehot[:4] if onehot else (None, None, None, None)),
                     bool(onehot is not None and len(onehot) > 4 and onehot[4]), bn_part, int(bn_rpg), cnt,
                     bool(chain))
+
+    def gemm_plan(self, M: int, N: int, K: int) -> Tuple[int, int]:
+        """(output tile, split-K factor) gemm() picks for an M x N x K product on this backend."""
+        kc = 64 if self.f32 else 128
+        tile, sk = _plan(M, N, K, kc, self._plan_clients())
+        return self.tile_override or tile, _effective_splits(K, self.split_override or sk, kc)
+
+    def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
+        """The next gemm() stages relu(BatchNorm(a)) for the given column ranges of its A operand (see
+        csrc/kernels/launch.h GemmArgs::bnl and EngineConfig.bn_fold)."""
+        self.L.gemm_bnl_next(list(part), list(mean), list(invstd), list(gamma), list(beta), list(rm), list(rv),
+                             list(nhat), [int(k) for k in k0], [int(t) for t in ptm], int(rpg), float(momentum),
+                             float(eps), out)
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):
@@ -385,9 +398,10 @@ class HipOps:
         self.L.activate(logits, out, st, w, k, ci, el, float(tau), self.seed, self.ctr, int(stream_id) * 16, sr, so,
                         cols, ss)
 
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None):
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None, tile=None,
+                        splitk=None):
         """logits = x W^T + b; out = activate(logits) (optionally + the fused slerp)."""
-        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot)
+        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot, tile=tile, splitk=splitk)
         self.activate(logits, out, spans, tau, stream_id, slerp=slerp)
 
     def act_bwd_ce(self, dact, act, logits, spans, cond_spans, col, opt, dlogits, loss_out, tau=0.2):

@@ -36,6 +36,7 @@ class Comm:
         self.rank = rank
         self.world_size = world_size
         self.client_ranks = list(client_ranks)
+        # "auto" / "auto_all": agreed over the control plane at init (_vote_data_backend)
         self.data_backend = data_backend
         self.device = device or torch.device("cpu")
         self.timeout = datetime.timedelta(seconds=timeout_s)
@@ -51,6 +52,8 @@ class Comm:
         self.dist_active = (world_size > 1 or force_dist) and init
         if self.dist_active:
             self._init(ip, port)
+        elif self.data_backend in ("auto", "auto_all"):
+            self.data_backend = "nccl" if self.device.type == "cuda" else "gloo"
 
     def _init(self, ip: str, port: int):
         os.environ.setdefault("MASTER_ADDR", ip)
@@ -60,6 +63,8 @@ class Comm:
                                     world_size=self.world_size, timeout=self.timeout)
         self.initialized = True
         self.ctrl = dist.group.WORLD
+        if self.data_backend in ("auto", "auto_all"):
+            self.data_backend = self._vote_data_backend(self.data_backend == "auto_all")
         if self.data_backend == "nccl":
             # every rank must call new_group, members or not
             self.data = dist.new_group(ranks=self.client_ranks, backend="nccl", timeout=self.timeout)
@@ -74,6 +79,27 @@ class Comm:
             # gloo data plane: reduce over every rank; a dedicated federator contributes zeros
             self.data = self.ctrl
 
+    def _vote_data_backend(self, all_ranks: bool) -> str:
+        """Collective (control plane): every rank reaches the SAME data-plane choice.  RCCL when each rank
+        that joins it (the client ranks; every rank for ``all_ranks``, the MD-GAN point-to-point group) has
+        a GPU of its own -- no two such ranks on one (host, device) -- and gloo on every rank otherwise.
+        Deciding from each rank's local device count alone let ranks disagree (a CPU-only dedicated
+        federator picking gloo while a GPU client created an RCCL group: init hung until the timeout)."""
+        import socket
+        me = (self.rank in self.client_ranks or all_ranks, self.device.type, socket.gethostname(),
+              self.device.index if self.device.type == "cuda" else -1)
+        views = [None] * self.world_size
+        dist.all_gather_object(views, me, group=self.ctrl)
+        return self.pick_data_backend(views)
+
+    @staticmethod
+    def pick_data_backend(views) -> str:
+        """views: one (joins the data plane, device type, host, device index) per rank."""
+        members = [v for v in views if v[0]]
+        ok = bool(members) and all(v[1] == "cuda" for v in members) and \
+            len({(v[2], v[3]) for v in members}) == len(members)
+        return "nccl" if ok else "gloo"
+
     @classmethod
     def from_env(cls, data_backend: str = "auto", device: torch.device | None = None,
                  force_dist: bool = False) -> "Comm":
@@ -81,7 +107,7 @@ class Comm:
         rank = int(os.environ.get("RANK", "0"))
         ip = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("MASTER_PORT", "29500"))
-        if data_backend == "auto":
+        if data_backend == "auto" and not (ws > 1 or force_dist):
             data_backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
         return cls(rank, ws, list(range(ws)), data_backend, ip, port, device=device, force_dist=force_dist)
 
@@ -212,50 +238,67 @@ class Comm:
             flat.copy_(host)
         return flat
 
-    def share_with_federator(self, flat: torch.Tensor, federator: int = 0) -> torch.Tensor:
+    def share_with_federator(self, flat: torch.Tensor, federator: int = 0, extra: Optional[torch.Tensor] = None):
         """After an RCCL reduce among the clients, hand the aggregate to a dataless federator rank
         (the reference's server holds the averaged model to sample from, `Server/dtds/distributed.py:
         809-820`).  The first client copies it to pinned host memory on a side stream and a helper thread
         sends it over the pair group once the copy lands, so the clients go on with the next round at
         once (only the copy, ~0.2 ms for 8.5 MB, is ordered before the next round's kernels); the
-        federator receives it and copies it to its device."""
+        federator receives it and copies it to its device.  ``extra`` (a small device tensor every client
+        holds, e.g. the client-averaged losses) rides along in the same message and lands in the
+        federator's ``extra``.  Returns True where the hand-off happened (both ends)."""
         if not self.dist_active or self.data_backend != "nccl" or federator in self.client_ranks:
-            return flat
+            return False
         src = self.client_ranks[0]
         pg = self.share_pg.get(federator)
+        parts = [flat] + ([extra] if extra is not None else [])
         if self.rank == src:
-            self._share_send(flat, federator, pg)
+            self._share_send(parts, federator, pg)
         elif self.rank == federator:
-            host = self._share_buffer(flat)[0]
+            host = self._share_buffer(parts)[0]
             dist.recv(host, src=src, group=pg)
-            flat.copy_(host, non_blocking=flat.is_cuda)
+            off = 0
+            for t in parts:
+                n = t.numel()
+                t.view(-1).copy_(host[off:off + n], non_blocking=t.is_cuda)
+                off += n
             if flat.is_cuda:            # the pinned buffer is received into again next round
                 torch.cuda.current_stream(flat.device).synchronize()
-        return flat
+        else:
+            return False
+        return True
 
-    def _share_buffer(self, flat: torch.Tensor):
-        if self._share is None or self._share[0].shape != flat.shape:
-            pin = flat.is_cuda
-            host = torch.empty(flat.shape, dtype=flat.dtype, pin_memory=pin)
-            stream = torch.cuda.Stream(flat.device) if flat.is_cuda else None
+    def _share_buffer(self, parts):
+        n = sum(t.numel() for t in parts)
+        if self._share is None or self._share[0].numel() != n:
+            cuda = parts[0].is_cuda
+            host = torch.empty(n, dtype=parts[0].dtype, pin_memory=cuda)
+            stream = torch.cuda.Stream(parts[0].device) if cuda else None
             from concurrent.futures import ThreadPoolExecutor
             self._share = [host, stream, ThreadPoolExecutor(1), None]
         return self._share
 
-    def _share_send(self, flat: torch.Tensor, dst: int, pg) -> None:
-        host, stream, pool, pending = self._share_buffer(flat)
+    def _share_send(self, parts, dst: int, pg) -> None:
+        host, stream, pool, pending = self._share_buffer(parts)
         if pending is not None:
             pending.result()            # the previous round's send has left the buffer
+        flat = parts[0]
         if flat.is_cuda:
             cur = torch.cuda.current_stream(flat.device)
             stream.wait_stream(cur)
             with torch.cuda.stream(stream):
-                host.copy_(flat, non_blocking=True)
+                off = 0
+                for t in parts:
+                    host[off:off + t.numel()].copy_(t.view(-1), non_blocking=True)
+                    off += t.numel()
                 ev = torch.cuda.Event()
                 ev.record(stream)
             cur.wait_stream(stream)     # the next round's updates of flat wait for the copy, not for the send
         else:
-            host.copy_(flat)
+            off = 0
+            for t in parts:
+                host[off:off + t.numel()].copy_(t.view(-1))
+                off += t.numel()
             ev = None
 
         def send():
@@ -263,6 +306,14 @@ class Comm:
                 ev.synchronize()
             dist.send(host, dst=dst, group=pg)
         self._share[3] = pool.submit(send)
+
+    def client_mean(self, t: torch.Tensor) -> torch.Tensor:
+        """t <- mean of t over the client ranks, in place, on the RCCL data plane (device-side: no host
+        wait).  Only meaningful where ``data_backend == "nccl"`` and this rank is a client."""
+        if self.dist_active and self.data_backend == "nccl" and self.is_client:
+            t.div_(self.n_clients)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.data)
+        return t
 
     def share_wait(self) -> None:
         """Block until this rank's last hand-off to the federator has been sent."""

@@ -457,3 +457,62 @@ def test_chain_tail_coalesced_matches_row_per_lane():
     (d0, f0), (d1, f1) = res
     assert torch.allclose(d0, d1, atol=1e-5, rtol=1e-4), float((d0 - d1).abs().max())
     assert (f0 - f1).abs().max().item() <= 2 * 2e-4 + 1e-6
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_bn_fold_matches_bn_launches(precision):
+    """EngineConfig.bn_fold: the generator's BatchNorm folded into its GEMMs (partials from the producing GEMM,
+    relu(BN(a)) staged by the consumers, materialised by the output GEMM) gives the forward of the GEMM +
+    bn_relu_train launches -- activations, nhat, batch and running statistics, logits -- up to the statistics'
+    summation order (and bf16 rounding of the staged operands), and trains the same."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    engs = []
+    for fold in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, bn_fold=fold), DEV,
+                          backend="hip", seed=21)
+        eng.set_training_data(X)
+        engs.append(eng)
+    a, b = engs
+    b.flat.copy_(a.flat)
+    assert not a._fold_on() and b._fold_on()
+    for e in engs:
+        e._prepare_paired()
+    torch.cuda.synchronize()
+    tol = 2e-5 if precision == "fp32" else 2e-2
+    c0 = a.c_cols[0]
+    for i in range(len(a.gdims)):
+        assert _rel(b.bn_mean2[i], a.bn_mean2[i]) < 1e-5, i
+        assert _rel(b.bn_invstd2[i], a.bn_invstd2[i]) < 1e-4, i
+        assert _rel(b.p[f"G.{i}.rm"], a.p[f"G.{i}.rm"]) < 1e-5 and _rel(b.p[f"G.{i}.rv"], a.p[f"G.{i}.rv"]) < 1e-4
+        assert _rel(b.nhat2[i], a.nhat2[i]) < tol, (i, _rel(b.nhat2[i], a.nhat2[i]))
+    assert _rel(b.H2[:, :c0], a.H2[:, :c0]) < tol, _rel(b.H2[:, :c0], a.H2[:, :c0])
+    assert torch.equal(b.H2[:, c0:], a.H2[:, c0:])          # the condition block, written by the sampler
+    assert _rel(b.logits2, a.logits2) < (1e-4 if precision == "fp32" else 5e-2)
+    # whole steps: the same training up to rounding
+    for e in engs:
+        e.train_steps(3, use_graph=False)
+    torch.cuda.synchronize()
+    assert _rel(b.flat, a.flat) < 1e-3, _rel(b.flat, a.flat)
+    b.train_steps(8)            # graph capture of the folded step
+    ld, lg = b.losses()
+    assert np.isfinite(ld) and np.isfinite(lg)
+
+
+def test_bn_fold_config_is_checked():
+    """gemm_bnl_next refuses ranges the kernel cannot stage, and a pending configuration is consumed (or
+    dropped by reset_held) -- never applied to a later, unrelated GEMM."""
+    from fed_tgan_amd.ops import native
+    L = native.require()
+    f = lambda *s: torch.zeros(*s, device=DEV)  # noqa: E731
+    w = 64
+    args = lambda width, k0: ([None], [f(2, width)], [f(2, width)], [f(width)], [f(width)], [f(width)], [f(width)],  # noqa: E731
+                              [None], [k0], [32], 100, 0.1, 1e-5, None)
+    with pytest.raises(RuntimeError):
+        L.gemm_bnl_next(*args(258, 0))        # wider than 256
+    with pytest.raises(RuntimeError):
+        L.gemm_bnl_next(*args(w, 2))          # k0 not a multiple of 4
+    L.gemm_bnl_next(*args(w, 0))
+    assert L.reset_held() == 1 and L.reset_held() == 0
