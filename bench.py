@@ -200,7 +200,10 @@ def run_rank(args) -> None:
     for kv in args.fed:
         k, v = kv.split("=", 1)
         cur = getattr(cfg, k)
-        setattr(cfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+        if isinstance(cur, bool) or (cur is None and v.lower() in ("0", "1", "true", "false", "yes", "no")):
+            setattr(cfg, k, v.lower() in ("1", "true", "yes"))
+        else:
+            setattr(cfg, k, v if cur is None else type(cur)(v))
     if args.tuning:
         from fed_tgan_amd.ops import native
         for kv in args.tuning:

@@ -45,7 +45,7 @@ from ..data.constants import CATEGORICAL
 from ..data.decode import csv_layout, decode_frame
 from ..data.schema import DatasetSpec
 from ..data.synthetic import generate, shard
-from ..data.table import TablePreprocessor, dump_meta_json
+from ..data.table import TablePreprocessor, dump_meta_json, read_csv_table
 from ..data.vocab import CategoryVocab
 from ..features.gmm import VGMBank, fit_vgm, sample_pool
 from ..features.transformer import VGMTransformer
@@ -74,6 +74,7 @@ class FedConfig:
     backend: str = "auto"                   # engine ops: auto | hip | torch
     write_csv: bool = True
     csv_writer: str = "auto"                # auto | native | pandas
+    table_reader: str = "auto"              # client CSVs: auto | pandas | arrow (data/table.py read_csv_table)
     async_csv: bool = True                  # write each epoch CSV in the background (overlaps next round)
     # formatter threads of a CSV write (0: min(cores, 16)).  Measured: 4 background threads fall
     # behind a 21 ms round (the last flush then waits for a backlog): 20.9 -> 23.4 ms/epoch
@@ -115,6 +116,10 @@ class FedConfig:
     # the generation graph, the pinned D2H copy and the CSV hand-off while the 80-step epoch still runs
     # stretches the epoch's kernels by ~2 ms (profiles/bench_train_sync_r3.txt)
     train_sync: bool = True
+    # wait on the host for the round's device work (aggregation, generation) before returning: the round time
+    # then is device time; without it the next round's launches queue behind the generation and the host
+    # returns at once (the epoch CSV's own hand-off waits for the table copy either way)
+    round_sync: bool = True
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -229,7 +234,7 @@ class FedRuntime:
         if cfg.datapath:
             path = cfg.datapath.format(client=idx, rank=self.rank)
             if os.path.exists(path):
-                return pd.read_csv(path)
+                return read_csv_table(path, cfg.table_reader)
             print(f"[data] rank {self.rank}: {path} not found; using the synthetic {cfg.spec.name}-schema "
                   f"generator ({cfg.synthetic_rows} rows, shard mode {cfg.shard_mode})", flush=True)
         if cfg.shard_mode == "independent":
@@ -765,7 +770,7 @@ class FedRuntime:
         if dump:
             with self.timer.phase("sample_dump", self.device):
                 self.sample_round(epoch, aggregated)
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and self.cfg.round_sync:
             stream_sync(self.device)
         dt = time.time() - t0
         if self.metrics is not None:

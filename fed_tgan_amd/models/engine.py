@@ -436,7 +436,7 @@ class CTGANEngine:
         # sampler writes z there and the condition block into H in one launch); the output GEMM materialises
         # relu(BN(a)) and z into H for the backward
         c0 = self.c_cols[0]
-        self._fold_static = (self.ops.name == "hip" and self.use_onehot and bool(cfg.bn_fold) and
+        self._fold_static = (getattr(self.ops, "bn_fold_capable", False) and self.use_onehot and bool(self.cfg.bn_fold) and
                              1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
                              all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
         if self._fold_static:

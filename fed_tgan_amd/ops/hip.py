@@ -24,6 +24,9 @@ EPI_NONE, EPI_LRELU_DROPOUT, EPI_MASK, EPI_RELU, EPI_BN_EVAL_RELU = 0, 1, 2, 3, 
 
 
 LONG_K_64 = True    # _plan's long-K rule with 64x64 tiles when workgroups are plentiful (A/B knob)
+# 128x128 tiles covering less than two waves of the 256 CUs give way to 64x64 tiles when those still number
+# >= 1024 (the wide table's G-out forward: 440 128-tiles, 1.7 waves, with a short K of 640) (A/B knob)
+WAVE_FILL_64 = False
 
 
 def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
@@ -51,6 +54,8 @@ def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
     t32 = -(-M // 32) * -(-N // 32) * c
     bursts = -(-K // kc)
     if t128 >= 256 and K >= 128 and M >= 128:    # (a 128-row tile over < 128 rows idles its MFMA rows)
+        if WAVE_FILL_64 and c == 1 and t128 < 512 and t64 >= 1024:
+            return 64, 1
         return 128, 1
     if t64 >= 256:
         return 64, 1
@@ -97,6 +102,7 @@ def _effective_splits(K: int, sk: int, kc: int) -> int:
 
 class HipOps:
     name = "hip"
+    bn_fold_capable = True       # EngineConfig.bn_fold (gemm_bnl_next + BN partials)
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
     gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
 

@@ -26,16 +26,96 @@ EPI_RELU = 3
 class TorchOps:
     adam_counts_steps = True     # eager Adam bumps its step counter (the HIP sampler does it there)
     name = "torch"
+    # EngineConfig.bn_fold on this backend (the GEMM-folded BatchNorm stated in torch: the oracle of the HIP
+    # path's partials / BN-on-load / materialisation; off by default -- the eager path runs BN as its own op)
+    bn_fold_capable = False
+
+    def __init__(self):
+        self._bnl = None
 
     # ------------------------------------------------------------------ GEMM
+    def gemm_plan(self, M: int, N: int, K: int):
+        return 32, 1
+
+    def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
+        """The next gemm() multiplies relu(BatchNorm(a)) for these column ranges of its A (see HipOps)."""
+        if self._bnl is not None:
+            raise RuntimeError("gemm_bnl_next: a configuration is already pending")
+        self._bnl = (list(zip(part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm)), int(rpg), float(momentum),
+                     float(eps), out)
+
+    @staticmethod
+    def _bn_partials(v: torch.Tensor, part: torch.Tensor, rpg: int, tile: int):
+        """Per row tile and batch: (count, mean, M2) of every column -- the GEMM epilogue's partials."""
+        M, N = v.shape
+        pv = part.view(-1, 2, 3, N)
+        for t in range(-(-M // tile)):
+            for b in range(2):
+                lo, hi = max(t * tile, rpg if b else 0), min((t + 1) * tile, M if b else rpg)
+                if hi <= lo:
+                    pv[t, b].zero_()
+                    continue
+                x = v[lo:hi]
+                mu = x.mean(0)
+                pv[t, b, 0] = float(hi - lo)
+                pv[t, b, 1] = mu
+                pv[t, b, 2] = ((x - mu) ** 2).sum(0)
+
+    def _bn_on_load(self, A: torch.Tensor) -> torch.Tensor:
+        ranges, rpg, mom, eps, out = self._bnl
+        self._bnl = None
+        M = A.shape[0]
+        ng = 2 if M > rpg else 1
+        A = A.clone()
+        for part, mean, istd, gm, bt, rm, rv, nh, k0, ptm in ranges:
+            w = gm.numel()
+            x = A[:, k0:k0 + w]
+            if part is not None:        # merge the producer's tiles (Chan), publish, advance the running stats
+                pv = part.view(-1, 2, 3, w)
+                for b in range(ng):
+                    n = torch.zeros(w, dtype=A.dtype, device=A.device)
+                    mu = torch.zeros_like(n)
+                    m2 = torch.zeros_like(n)
+                    t0, t1 = (rpg // ptm, (M - 1) // ptm) if b else (0, (min(rpg, M) - 1) // ptm)
+                    for t in range(t0, t1 + 1):
+                        nb, mb, m2b = pv[t, b, 0], pv[t, b, 1], pv[t, b, 2]
+                        nt = n + nb
+                        d = mb - mu
+                        f = torch.where(nt > 0, nb / nt.clamp_min(1), torch.zeros_like(nt))
+                        mu = mu + d * f
+                        m2 = m2 + m2b + d * d * torch.where(nt > 0, n * nb / nt.clamp_min(1), torch.zeros_like(nt))
+                        n = nt
+                    var = torch.where(n > 0, m2 / n.clamp_min(1), torch.zeros_like(n))
+                    mean.view(-1, w)[b].copy_(mu)
+                    istd.view(-1, w)[b].copy_(torch.rsqrt(var + eps))
+                    unb = rpg / max(rpg - 1, 1)
+                    with torch.no_grad():
+                        rm.mul_(1 - mom).add_(mom * mu)
+                        rv.mul_(1 - mom).add_(mom * var * unb)
+            rows_b = (torch.arange(M, device=A.device) >= rpg).long()
+            mu_r = mean.view(-1, w)[rows_b]
+            is_r = istd.view(-1, w)[rows_b]
+            nhat_v = (x - mu_r) * is_r
+            y = torch.relu(nhat_v * gm + bt)
+            A[:, k0:k0 + w] = y
+            if out is not None:
+                nh.copy_(nhat_v)
+        if out is not None:
+            out[:, :A.shape[1]].copy_(A)
+        return A
+
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
-             slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0, onehot=None):
+             slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0, onehot=None, bn_part=None, bn_rpg=0, tile=None,
+             splitk=None, **_):
         """c = epi(alpha * op(a) @ op(b) + beta * c + bias [+ onehot]).
 
         onehot = (W_c [N, C], col [M], opt [M], cond_offset): a holds only the dense input columns and
-        the one-hot conditional block adds W_c[:, cond_offset[col[m]] + opt[m]] to row m."""
+        the one-hot conditional block adds W_c[:, cond_offset[col[m]] + opt[m]] to row m.
+        bn_part (with bn_rpg, tile): also the per-tile BatchNorm partials of the stored output."""
         A = a.t() if ta else a
         B = b.t() if tb else b
+        if self._bnl is not None:
+            A = self._bn_on_load(A)
         acc = torch.matmul(A, B)
         if alpha != 1.0:
             acc = acc * alpha
@@ -63,6 +143,8 @@ class TorchOps:
         elif epi == EPI_RELU:
             acc = torch.relu(acc)
         c.copy_(acc)
+        if bn_part is not None:
+            self._bn_partials(acc, bn_part, int(bn_rpg), int(tile or 32))
 
     # ------------------------------------------------------------------ samplers
     def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,
@@ -184,8 +266,8 @@ class TorchOps:
             dbias.copy_(da.sum(0))
 
     # ------------------------------------------------------------------ activations
-    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None):
-        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot)
+    def linear_activate(self, x, W, b, logits, out, spans, tau=0.2, stream_id=0, slerp=None, onehot=None, **kw):
+        self.gemm(x, W, logits, tb=True, bias=b, onehot=onehot, **kw)
         self.activate(logits, out, spans, tau, stream_id=stream_id)
         if slerp is not None:
             real, fake_full, interp, sid = slerp

@@ -224,7 +224,8 @@ class Comm:
             return flat
         if self.data_backend == "nccl":
             if self.is_client:
-                flat.mul_(weight)
+                if weight != 1.0:
+                    flat.mul_(weight)
                 dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.data)
             return flat
         # gloo: reduce on host memory

@@ -26,8 +26,10 @@ def _engine_cfg(ecfg, overrides):
     for kv in overrides:
         k, v = kv.split("=", 1)
         cur = getattr(ecfg, k)
-        setattr(ecfg, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else
-                v if cur is None else type(cur)(v))
+        if isinstance(cur, bool) or (cur is None and v.lower() in ("0", "1", "true", "false", "yes", "no")):
+            setattr(ecfg, k, v.lower() in ("1", "true", "yes"))
+        else:
+            setattr(ecfg, k, v if cur is None else type(cur)(v))
     return ecfg
 
 
@@ -55,8 +57,15 @@ def main():
                     help="FedConfig override for A/B runs, e.g. --fed label_encoders_early=0")
     ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE",
                     help="native set_tuning knob for A/B runs, e.g. --tuning gemm_pairs=0")
+    ap.add_argument("--plan", action="append", default=[], metavar="KEY=VALUE",
+                    help="GEMM planner knob of fed_tgan_amd.ops.hip (module constant), e.g. --plan WAVE_FILL_64=1")
     args = ap.parse_args()
-    if args.tuning:
+    if args.plan:
+        from fed_tgan_amd.ops import hip as hip_ops
+        for kv in args.plan:
+            key, val = kv.split("=", 1)
+            getattr(hip_ops, key)
+            setattr(hip_ops, key, bool(int(val)) if isinstance(getattr(hip_ops, key), bool) else int(val))
         from fed_tgan_amd.ops import native
         for kv in args.tuning:
             key, val = kv.split("=", 1)
@@ -116,6 +125,8 @@ def main():
         summ["engine_overrides"] = args.engine
     if args.tuning:
         summ["tuning"] = args.tuning
+    if args.plan:
+        summ["plan"] = args.plan
     if args.fed:
         summ["fed_overrides"] = args.fed
     print(json.dumps(summ), flush=True)
