@@ -440,11 +440,12 @@ class CTGANEngine:
                              1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
                              all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
         if self._fold_static:
-            hw4 = _ceil4(self.Hw)
-            big = _padded_rows(2 * B, hw4 + c0, dev)
-            self.H2 = big[:, :self.Hw]
-            self.Hp2 = big[:, hw4:hw4 + c0]
-            self._hp_off = hw4           # z's column in the big rows: hw4 + off[0]
+            # rows [Hp | H]: the sampler gets both as one row ([z in Hp] ... [c block in H], the c block last, as
+            # its width is read off the row's end)
+            big = _padded_rows(2 * B, c0 + self.Hw, dev)
+            self.Hp2 = big[:, :c0]
+            self.H2 = big[:, c0:c0 + self.Hw]
+            self._Hbig = big
             self._bn_part = [z(-(-2 * B // 32) * 6 * g) for g in self.gdims]   # 32-row tiles at most
         else:
             self.H2 = _padded_rows(2 * B, self.Hw, dev)
@@ -766,11 +767,11 @@ class CTGANEngine:
         updated D batch first, then G batch.  Halves the generator-side launches of a step and
         doubles their workgroups (M = 1000 fills the chip better than M = 500)."""
         o, B = self.ops, self.B
-        h, zc = self.H2, self.z_cols
-        if self._fold_on():     # z goes to the pre-BN rows Hp (same row stride: one sampler launch)
-            h = self.H2.as_strided((2 * B, self._hp_off + self.c_cols[0]), self.H2.stride(), self.H2.storage_offset())
-            zc = (self._hp_off + self.z_cols[0], self._hp_off + self.z_cols[1])
-        o.sample_train(self.tables, h, zc, self.c_cols, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
+        h, cc = self.H2, self.c_cols
+        if self._fold_on():     # z goes to the pre-BN rows Hp, the condition block to H: one sampler launch
+            c0 = self.c_cols[0]
+            h, cc = self._Hbig, (c0 + self.c_cols[0], c0 + self.c_cols[1])
+        o.sample_train(self.tables, h, self.z_cols, cc, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
                        self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
                        zero_metrics=True, stream_id=1)
         self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
