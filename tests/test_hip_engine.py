@@ -206,7 +206,8 @@ def test_large_batches_train(batch):
     eng._prepare_paired()
     torch.cuda.synchronize()
     B, g0 = eng.B, eng.gdims[0]
-    a = eng.abuf2[0]
+    # the layer's pre-BN output: the GEMM's scratch, or (EngineConfig.bn_fold) the pre-BN rows beside H
+    a = eng.Hp2[:, eng.off[1]:eng.off[0]] if eng._fold_on() else eng.abuf2[0]
     out = eng.H2[:, eng.off[1]:eng.off[0]]
     for h in (slice(0, B), slice(B, 2 * B)):
         ref = torch.relu(F.batch_norm(a[h], None, None, eng.p["G.0.gamma"], eng.p["G.0.beta"], True, 0.1, 1e-5))

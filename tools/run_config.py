@@ -111,6 +111,7 @@ def main():
         fake = pd.read_csv(os.path.join(res, f"{spec.name}_synthesis_epoch_{ep}.csv"))
         jsd, wd = stat_sim(real, fake, spec.categorical_list)
         rec = {"spec": spec.name, "clients": k, "shard": args.shard, "precision": args.precision, "epoch": ep,
+               "backend": rt.engine.ops.name, "seed": args.seed,
                "sec": round(rt.round_times[ep], 4), "avg_jsd": round(jsd, 5), "avg_wd": round(wd, 5)}
         lines.append(rec)
         print(json.dumps(rec), flush=True)
