@@ -437,6 +437,7 @@ class CTGANEngine:
         # relu(BN(a)) and z into H for the backward
         c0 = self.c_cols[0]
         self._fold_static = (getattr(self.ops, "bn_fold_capable", False) and self.use_onehot and bool(self.cfg.bn_fold) and
+                             not self.cfg.bn_colown and
                              1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
                              all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
         if self._fold_static:
