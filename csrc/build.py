@@ -98,9 +98,13 @@ def main():
         list(ex.map(lambda j: run(j[2]), todo))
     objs = [o for _, o, _ in jobs]
     if args.force or todo or newer(objs, out):
-        run([hipcc(), "-shared", "-o", out] + objs + [f"--offload-arch={ARCH}", "-L" + tlib, "-lc10", "-lc10_hip",
+        # linked beside the library and renamed over it: a reader (an import, a gpurun snapshot) never sees a
+        # half-written file
+        tmp = out + ".tmp"
+        run([hipcc(), "-shared", "-o", tmp] + objs + [f"--offload-arch={ARCH}", "-L" + tlib, "-lc10", "-lc10_hip",
                                                        "-ltorch", "-ltorch_cpu", "-l:libamdhip64.so", "-pthread",
                                                        "-Wl,-rpath," + tlib])
+        os.replace(tmp, out)
     print(f"built {out} ({len(todo)} objects recompiled)")
 
 

@@ -550,10 +550,20 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
           if (!fin && (b < blo || b > bhi)) continue;
           const int t0 = b ? rpg / L.ptm : 0, t1 = b ? (M - 1) / L.ptm : (min(rpg, M) - 1) / L.ptm;
           float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll 8
-          for (int t = t0; t <= t1; ++t) {
-            const float* p = L.part + ((size_t)(t * 2 + b) * 3) * L.width + c;
-            bnl_merge(n, mean, m2, p[0], p[L.width], p[2 * (size_t)L.width]);
+          // 16 tiles' triples are requested together (clamped, always-valid addresses; tiles past t1 count 0),
+          // then merged: one memory round trip per 16 tiles, not one per tile behind the dependent merge chain
+          for (int tb = t0; tb <= t1; tb += 16) {
+            float pc[16], pm[16], pq[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const float* p = L.part + ((size_t)(min(tb + u, t1) * 2 + b) * 3) * L.width + c;
+              pc[u] = p[0];
+              pm[u] = p[L.width];
+              pq[u] = p[2 * (size_t)L.width];
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+              if (tb + u <= t1) bnl_merge(n, mean, m2, pc[u], pm[u], pq[u]);
           }
           mu[b] = mean;
           var[b] = n > 0.f ? m2 / n : 0.f;

@@ -226,6 +226,7 @@ class FedRuntime:
         self.dump_csv = None
         self._round_start: Dict[int, float] = {}    # epoch -> wall time its round began
         self._csv_done: Dict[int, float] = {}       # epoch -> wall time its CSV was on disk
+        self._csv_times: Dict[int, tuple] = {}      # epoch -> (copy wait, format + write) seconds, writer side
 
     # ================================================================= data
     def _local_frame(self) -> pd.DataFrame:
@@ -406,8 +407,12 @@ class FedRuntime:
         self.engine.prepare_graphs(train, gen)
         if self.is_fed and cfg.write_csv and cfg.async_csv:
             self._copy_stream = torch.cuda.Stream(self.device)
+            # the table of round r is held by the writer while round r + 1 copies its own: two (three if the
+            # writer lags) pinned buffers are live at once.  A second first-time pinned allocation in round 1
+            # (hipHostMalloc of the 40k-row table, ~80 ms) was the "round-1 stall" of round 4
             n_cols = len(self.global_meta["columns"])
-            torch.empty((self.n_sample, n_cols), dtype=torch.float64, pin_memory=True)   # back to the cache
+            bufs = [torch.empty((self.n_sample, n_cols), dtype=torch.float64, pin_memory=True) for _ in range(3)]
+            del bufs                                # back to torch's caching host allocator
             from ..utils.csvio import AsyncTableWriter
             if self._writer is None:
                 self._writer = AsyncTableWriter()
@@ -706,8 +711,14 @@ class FedRuntime:
             self._writer.flush()
 
     def _write_epoch_csv(self, values, epoch: int):
+        t0 = time.perf_counter()
+        if isinstance(values, PendingHost):
+            values = values.get()
+        t1 = time.perf_counter()
         path = self._write_epoch_csv_body(values, epoch)
         self._csv_done[epoch] = time.time()
+        # writer-side seconds of this table: waiting for its device-to-host copy, formatting + writing
+        self._csv_times[epoch] = (t1 - t0, time.perf_counter() - t1)
         return path
 
     def _write_epoch_csv_body(self, values, epoch: int):
@@ -756,6 +767,7 @@ class FedRuntime:
         self._host_train = {"h_wait": (hw - h0) if hw else 0.0, "h_issue": (hi - hw) if hi else 0.0,
                             "h_total": time.perf_counter() - h0}
         self._epoch_done = epoch + 1
+        h1 = time.perf_counter()
         with self.timer.phase("aggregate", self.device):
             # -E_interval (accepted but unused by the reference, `Server/dtds/distributed.py:904`):
             # local epochs between aggregations (1 = aggregate every round, the reference behaviour)
@@ -767,12 +779,16 @@ class FedRuntime:
             dump = epoch in self.cfg.csv_epochs or epoch + 1 == self.cfg.epochs
         else:
             dump = (epoch + 1) % every == 0 or epoch + 1 == self.cfg.epochs
+        h2 = time.perf_counter()
         if dump:
             with self.timer.phase("sample_dump", self.device):
                 self.sample_round(epoch, aggregated)
+        h3 = time.perf_counter()
         if self.device.type == "cuda" and self.cfg.round_sync:
             stream_sync(self.device)
         dt = time.time() - t0
+        # host seconds of the round's phases after the train phase: aggregation, sampling + CSV hand-off, final wait
+        self._host_train.update({"h_agg": h2 - h1, "h_sample": h3 - h2, "h_end": time.perf_counter() - h3})
         if self.metrics is not None:
             # process CPU seconds of the round (all threads) and the cgroup's CFS throttling during it
             self._host_train["cpu_s"] = time.process_time() - cpu0
@@ -840,8 +856,10 @@ class FedRuntime:
                 ld, lg = self.round_losses()
                 _log(cfg, self.rank, f"EPOCH {ep}: loss_d:{ld:>6.2f}   loss_g:{lg:>6.2f}   round time: {dt:.3f} sec")
                 if self.metrics is not None:
+                    csv_t = self._csv_times.get(ep - 1)      # the previous table, written during this round
                     self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,
-                                        **self.timer.last(), **getattr(self, "_host_train", {})})
+                                        **self.timer.last(), **getattr(self, "_host_train", {}),
+                                        **({"csv_wait_prev": csv_t[0], "csv_write_prev": csv_t[1]} if csv_t else {})})
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
                 self.flush_writes()      # the checkpoint's per-round stamps include every CSV so far
                 self.save_checkpoint(ep + 1)

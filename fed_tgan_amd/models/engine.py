@@ -607,7 +607,7 @@ class CTGANEngine:
         cond: the rows' (col, opt) int32 condition indices -- the conditional block of H is then
         applied as a one-hot gather instead of a dense K range (``EngineConfig.onehot``)."""
         o = self.ops
-        if training and paired and self._fold_on():
+        if training and paired and cond is not None and self._fold_on():
             self._g_forward_fold(logits, act_out, stream_id, slerp, cond)
             return
         for i, g in enumerate(self.gdims):
