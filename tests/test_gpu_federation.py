@@ -267,3 +267,25 @@ def test_dedicated_federator_rccl_among_clients(tmp_path):
     assert res["data_backend"] == ["nccl", "nccl"] and res["data_world_size"][1] == 1
     assert res["flat_equal"] and res["epochs"] == 2
     _check_outputs(tmp_path, 2, 3000)
+
+
+def test_gpu_round_zero_costs_a_steady_round(tmp_path):
+    """Nothing first-time happens inside the rounds (FedRuntime._prepare_round_zero: the step and generation
+    graphs, the table writer and the pinned table buffers are made at init): every round of a 4-round run --
+    round 0 and round 1 included, which used to pay 40-80 ms of captures and a second pinned allocation --
+    costs within 1.5x of the steady round (`Server/dtds/distributed.py:790-829` times every round alike)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    import json
+    m = tmp_path / "m.jsonl"
+    cfg = FedConfig(spec=intrusion_spec(), epochs=4, synthetic_rows=40000, out_dir=str(tmp_path), backend="hip",
+                    gmm_backend="torch", verbose=False, metrics_log=str(m))
+    rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=DEV), DEV)
+    rt.initialize()
+    rt.fit()
+    r = rt.round_times
+    steady = sorted(r[1:])[1]
+    recs = [json.loads(line) for line in open(m)]
+    assert max(r) <= 1.5 * steady, (r, recs)
+    stamps = pd.read_csv(tmp_path / "timestamp_experiment.csv", header=None)[0].tolist()
+    assert len(stamps) == 4 and all(s > 0 for s in stamps)
