@@ -178,25 +178,24 @@ struct BnlCtx {
 // 4 consecutive k of row m (k % 4 == 0; a range never splits a float4: k0 and width are multiples of 4).
 // ok[e]: element in range (others stay 0 and are not materialised).
 __device__ __forceinline__ void bnl_apply4(const BnlCtx& c, int m, int k, float (&x)[4], const bool (&ok)[4]) {
-  int j = -1, kk = 0;
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj)
-    if (jj < c.nr && k >= c.k0[jj] && k < c.k0[jj] + c.w[jj]) {
-      j = jj;
-      kk = k - c.k0[jj];
-    }
+  // range selection by selects, not by indexing the context's arrays with a run-time index (that put the
+  // context in scratch: 80 B per lane, every staged float4 paying scratch loads)
+  const bool in0 = k >= c.k0[0] && k < c.k0[0] + c.w[0];
+  const bool in1 = !in0 && c.nr > 1 && k >= c.k0[1] && k < c.k0[1] + c.w[1];
+  const int kk = k - (in0 ? c.k0[0] : c.k0[1]);
   const int b = m >= c.rpg ? 1 : 0;
-  if (j >= 0) {
+  if (in0 || in1) {
+    const f32x4* t4 = c.tab + ((in0 ? 0 : 2) + b) * BNL_W + kk;
     float n[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const f32x4 t = c.tab[(j * 2 + b) * BNL_W + kk + e];
+      const f32x4 t = t4[e];
       n[e] = (x[e] - t[0]) * t[1];            // the bn_relu_train expressions
       const float y = n[e] * t[2] + t[3];
       x[e] = ok[e] ? (y > 0.f ? y : 0.f) : 0.f;
     }
     if (c.out && ok[0]) {
-      float* dst = c.nhat[j] + (size_t)m * c.ldn[j] + kk;
+      float* dst = (in0 ? c.nhat[0] : c.nhat[1]) + (size_t)m * (in0 ? c.ldn[0] : c.ldn[1]) + kk;
       if (ok[3]) *reinterpret_cast<f32x4*>(dst) = f32x4{n[0], n[1], n[2], n[3]};
       else
 #pragma unroll
@@ -555,7 +554,9 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
   bool need[2] = {false, false};
   if (jp >= 0 && jp < 99) {
     const int ptm = g.bnl[jp].ptm;
-    for (int b = 0; b < ng; ++b) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (b >= ng) continue;
       need[b] = fin || (b >= blo && b <= bhi);
       tlo[b] = b ? rpg / ptm : 0;
       thi[b] = b ? (M - 1) / ptm : (min(rpg, M) - 1) / ptm;
@@ -624,7 +625,9 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
       if (fin) {
         const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnl_mom;
         float rm = L.rm[c], rv = L.rv[c];
-        for (int b = 0; b < ng; ++b) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (b >= ng) continue;
           rm = (1.f - mom) * rm + mom * mu[b];
           rv = (1.f - mom) * rv + mom * var[b] * unb;
         }
@@ -641,8 +644,9 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
       const float gm = L.gamma[c], bt = L.beta[c];
       if (L.part) {
         float mu[2] = {0.f, 0.f}, var[2] = {0.f, 0.f};
-        for (int b = 0; b < ng; ++b) {
-          if (!fin && (b < blo || b > bhi)) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (b >= ng || (!fin && (b < blo || b > bhi))) continue;
           const int t0 = b ? rpg / L.ptm : 0, t1 = b ? (M - 1) / L.ptm : (min(rpg, M) - 1) / L.ptm;
           float n = 0.f, mean = 0.f, m2 = 0.f;
           // 16 tiles' triples requested together (clamped, always-valid addresses), then merged
@@ -671,7 +675,9 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
         if (fin) {
           const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnl_mom;
           float rm = L.rm[c], rv = L.rv[c];
-          for (int b = 0; b < ng; ++b) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b >= ng) continue;
             rm = (1.f - mom) * rm + mom * mu[b];
             rv = (1.f - mom) * rv + mom * var[b] * unb;
           }
@@ -679,8 +685,10 @@ __device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin
           L.rv[c] = rv;
         }
       } else {
-        for (int b = blo; b <= bhi; ++b)
-          tab[(j * 2 + b) * BNL_W + c] = f32x4{L.mean[(size_t)b * L.width + c], L.invstd[(size_t)b * L.width + c], gm, bt};
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          if (b >= blo && b <= bhi)
+            tab[(j * 2 + b) * BNL_W + c] = f32x4{L.mean[(size_t)b * L.width + c], L.invstd[(size_t)b * L.width + c], gm, bt};
       }
     }
   }
