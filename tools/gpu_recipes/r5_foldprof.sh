@@ -11,4 +11,5 @@ for f in 1 0; do
   python3 $R/tools/step_breakdown.py $OUT/step_$f/run_results.db > $OUT/step_breakdown_fold$f.txt 2>&1 || exit 1
   rm -rf $OUT/step_$f
 done
+(cd $R && timeout -k 10 200 python tools/microbench.py --cfg-ab bn_fold > $OUT/step_ab.txt 2>&1) || exit 1
 echo done

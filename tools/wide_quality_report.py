@@ -15,8 +15,8 @@ import numpy as np
 def _load(paths):
     runs = []
     for p in paths:
-        with open(p) as f:
-            runs += [json.loads(line) for line in f if line.strip()]
+        with open(p) as f:                               # .log files: the JSON lines among other output
+            runs += [json.loads(line) for line in f if line.lstrip().startswith("{")]
     return runs
 
 
@@ -56,18 +56,25 @@ def reduced_table(runs):
 
 def full_table(runs):
     by = collections.defaultdict(lambda: collections.defaultdict(list))
+    seen = set()
     for r in runs:
-        if "epoch" not in r:
+        if "epoch" not in r or "precision" not in r:     # metrics-log lines and summaries carry no per-epoch score
             continue
+        key = (r.get("backend", "hip"), r["precision"], r.get("seed"), r["epoch"])
+        if key in seen:                                  # the same record in a log and in the JSONL
+            continue
+        seen.add(key)
         tag = f"{r.get('backend', 'hip')}-{r['precision']}"
         by[tag][r["epoch"]].append(r)
-    lines = ["## 100k x 512, 1 client, 5 epochs (tools/run_config.py): Avg_JSD / Avg_WD, mean over seeds (n)"]
+    lines = ["## 100k x 512, 1 client, 5 epochs (tools/run_config.py): Avg_JSD / Avg_WD, mean +- SE over seeds (n)"]
     for tag, eps in sorted(by.items()):
         cells = []
         for e in sorted(eps):
-            j = np.mean([r["avg_jsd"] for r in eps[e]])
-            w = np.mean([r["avg_wd"] for r in eps[e]])
-            cells.append(f"{e}: {j:.4f} / {w:.4f} (n={len(eps[e])})")
+            j = np.asarray([r["avg_jsd"] for r in eps[e]])
+            w = np.asarray([r["avg_wd"] for r in eps[e]])
+            n = len(j)
+            se = (lambda a: a.std(ddof=1) / np.sqrt(n)) if n > 1 else (lambda a: float("nan"))
+            cells.append(f"{e}: {j.mean():.4f}+-{se(j):.4f} / {w.mean():.4f}+-{se(w):.4f} (n={n})")
         lines.append(f"{tag:12s} " + "  ".join(cells))
     return lines + [""]
 
