@@ -416,8 +416,20 @@ class FedRuntime:
             from ..utils.csvio import AsyncTableWriter
             if self._writer is None:
                 self._writer = AsyncTableWriter()
-            self._writer.submit(lambda: None)       # the writer thread starts now
+            self._writer.submit(self._warm_csv, n_cols)     # the writer thread (and the formatter's) start now
             self._writer.flush()
+
+    def _warm_csv(self, n_cols: int):
+        """One small table through the native formatter to the null device, on the writer thread: its first
+        call's one-time costs (formatter threads' malloc arenas, the column descriptors' first build) are
+        paid at initialisation instead of in round 1."""
+        from ..utils import csvio
+        if self.csv_cols is None or self.cfg.csv_writer not in ("auto", "native") or not csvio.available():
+            return
+        try:
+            csvio.write_layout(os.devnull, np.zeros((4096, n_cols)), self.csv_cols, threads=self.cfg.csv_threads)
+        except (RuntimeError, ValueError) as e:     # a warm-up only: the real tables report their own errors
+            _log(self.cfg, self.rank, f"csv warm-up skipped: {e}")
 
     def _batch_group(self, lay):
         """The batched multi-client engine's arena when this process' clients run as one (threads of an

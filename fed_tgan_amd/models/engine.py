@@ -144,7 +144,10 @@ class EngineConfig:
     # GEMM stores its pre-BN output plus per-tile partial statistics; the next layer's GEMM and the output GEMM
     # merge those statistics in their prologue and stage relu(BN(a)) from the pre-BN values as they load them;
     # the output GEMM also writes relu(BN(a)) and nhat back for the backward.  Removes both bn_relu_train launches.
-    bn_fold: bool = True
+    # Off by default: measured slower (Intrusion step +11.5 us, profiles/bn_fold_r5.txt): every consumer
+    # workgroup re-merges all producer tiles' partials (+6-13 us per consumer GEMM) against 2 x 7.7 us of BN
+    # launches removed.
+    bn_fold: bool = False
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):

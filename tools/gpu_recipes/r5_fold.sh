@@ -10,12 +10,10 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 timeout -k 10 700 python -u -m pytest -q --timeout 200 --timeout-method thread tests -m gpu > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $OUT/pytest_gpu.log
 if [ $rc -ge 124 ]; then exit 1; fi      # a hang / abort / fault: nothing more on the GPU (assertion failures go on)
+timeout -k 10 200 python tools/microbench.py --cfg-ab bn_fold >> $OUT/step_ab.txt 2>&1 || exit 1
 for i in 1 2; do
-  timeout -k 10 200 python tools/microbench.py --cfg-ab bn_fold >> $OUT/step_ab.txt 2>&1 || exit 1
-done
-for i in 1 2; do
-  timeout -k 10 150 python bench.py --steps 20 --warmup 5 --engine bn_fold=0 2>/dev/null | tail -1 >> $OUT/bench_nofold.jsonl || exit 1
-  timeout -k 10 150 python bench.py --steps 20 --warmup 5 2>/dev/null | tail -1 >> $OUT/bench_fold.jsonl || exit 1
+  timeout -k 10 150 python bench.py --steps 20 --warmup 5 2>/dev/null | tail -1 >> $OUT/bench_nofold.jsonl || exit 1
+  timeout -k 10 150 python bench.py --steps 20 --warmup 5 --engine bn_fold=1 2>/dev/null | tail -1 >> $OUT/bench_fold.jsonl || exit 1
 done
 timeout -k 10 150 python tools/run_config.py --spec intrusion --clients 1 --epochs 6 --fed metrics_log=$OUT/m_int.jsonl > $OUT/int.log 2>&1 || exit 1
 mkdir -p $OUT/cli && (cd $OUT/cli && PYTHONPATH=$R timeout -k 10 150 python -m dtds.distributed -world_size 1 -colocated -epochs 2 > cli2.log 2>&1 && cp timestamp_experiment.csv ts2.csv) || exit 1
