@@ -420,16 +420,33 @@ class FedRuntime:
             self._writer.flush()
 
     def _warm_csv(self, n_cols: int):
-        """One small table through the native formatter to the null device, on the writer thread: its first
-        call's one-time costs (formatter threads' malloc arenas, the column descriptors' first build) are
-        paid at initialisation instead of in round 1."""
+        """One table of the real size and shape through the native formatter to the null device, on the writer
+        thread.  The first table a process formats costs ~18x a steady one (83 vs 4.6 ms on the box: the
+        formatter threads' fresh malloc arenas fault in every page of the formatted text), and while it ran the
+        main thread stalled as long (round 1: 78 ms waiting to enter the train phase, profiles/stall_r5.txt).
+        Formatting plausible values (long float reprs, every vocabulary index) pays that at initialisation."""
+        from ..data.decode import KIND_FLOAT, KIND_NONNEG, KIND_VOCAB
         from ..utils import csvio
-        if self.csv_cols is None or self.cfg.csv_writer not in ("auto", "native") or not csvio.available():
+        lay = self.csv_cols
+        if lay is None or self.cfg.csv_writer not in ("auto", "native") or not csvio.available():
             return
+        t0 = time.perf_counter()
+        rows = max(int(self.n_sample), 1)
+        vals = np.zeros((rows, n_cols))
+        rng = np.random.default_rng(0)
+        for j, k in enumerate(lay.kinds):
+            s = lay.src[j]
+            if k == KIND_VOCAB:
+                vals[:, s] = np.arange(rows) % max(len(lay.vocabs[j]), 1)
+            elif k == KIND_FLOAT:
+                vals[:, s] = rng.standard_normal(rows) * 1e3
+            elif k == KIND_NONNEG:
+                vals[:, s] = rng.standard_normal(rows)
         try:
-            csvio.write_layout(os.devnull, np.zeros((4096, n_cols)), self.csv_cols, threads=self.cfg.csv_threads)
+            csvio.write_layout(os.devnull, vals, lay, threads=self.cfg.csv_threads)
         except (RuntimeError, ValueError) as e:     # a warm-up only: the real tables report their own errors
             _log(self.cfg, self.rank, f"csv warm-up skipped: {e}")
+        self.csv_warm_s = time.perf_counter() - t0
 
     def _batch_group(self, lay):
         """The batched multi-client engine's arena when this process' clients run as one (threads of an
@@ -871,7 +888,9 @@ class FedRuntime:
                     csv_t = self._csv_times.get(ep - 1)      # the previous table, written during this round
                     self.metrics.write({"epoch": ep, "round_s": dt, "loss_d": ld, "loss_g": lg,
                                         **self.timer.last(), **getattr(self, "_host_train", {}),
-                                        **({"csv_wait_prev": csv_t[0], "csv_write_prev": csv_t[1]} if csv_t else {})})
+                                        **({"csv_wait_prev": csv_t[0], "csv_write_prev": csv_t[1]} if csv_t else {}),
+                                        **({"csv_warm_s": self.csv_warm_s}
+                                           if ep == self.start_epoch and hasattr(self, "csv_warm_s") else {})})
             if cfg.ckpt_every and (ep + 1) % cfg.ckpt_every == 0:
                 self.flush_writes()      # the checkpoint's per-round stamps include every CSV so far
                 self.save_checkpoint(ep + 1)

@@ -16,6 +16,9 @@ for i in 1 2; do
   timeout -k 10 150 python bench.py --steps 20 --warmup 5 --engine bn_fold=1 2>/dev/null | tail -1 >> $OUT/bench_fold.jsonl || exit 1
 done
 timeout -k 10 150 python tools/run_config.py --spec intrusion --clients 1 --epochs 6 --fed metrics_log=$OUT/m_int.jsonl > $OUT/int.log 2>&1 || exit 1
-mkdir -p $OUT/cli && (cd $OUT/cli && PYTHONPATH=$R timeout -k 10 150 python -m dtds.distributed -world_size 1 -colocated -epochs 2 > cli2.log 2>&1 && cp timestamp_experiment.csv ts2.csv) || exit 1
-(cd $OUT/cli && PYTHONPATH=$R timeout -k 10 150 python -m dtds.distributed -world_size 1 -colocated -epochs 4 > cli4.log 2>&1 && cp timestamp_experiment.csv ts4.csv) || exit 1
+# (the CLI runs in a scratch directory: its epoch tables would overflow gpurun_out; logs + timestamps copied back)
+C=/tmp/r5cli; rm -rf $C; mkdir -p $C $OUT/cli
+(cd $C && PYTHONPATH=$R timeout -k 10 150 python -m dtds.distributed -world_size 1 -colocated -epochs 2 > $OUT/cli/cli2.log 2>&1 && cp timestamp_experiment.csv $OUT/cli/ts2.csv) || exit 1
+(cd $C && PYTHONPATH=$R timeout -k 10 150 python -m dtds.distributed -world_size 1 -colocated -epochs 4 > $OUT/cli/cli4.log 2>&1 && cp timestamp_experiment.csv $OUT/cli/ts4.csv) || exit 1
+rm -rf $C
 echo done

@@ -55,6 +55,12 @@ def main(argv):
     lines = [f"{'disp':>5}  {'MFMA busy':>9} {'wait':>6} {'issue':>6} {'LDS cf':>6} {'fetch KB':>9} {'write KB':>9}  kernel"]
     for n, k, a, b, c, d, e, f in rows[:top]:
         lines.append(f"{n:5d}  {a:>9} {b:>6} {c:>6} {d:>6} {e} {f}  {k}")
+    # then every counter's mean per dispatch, kernel by kernel
+    lines.append("")
+    for k in sorted(per, key=lambda k: -len(disp[k]))[:top]:
+        lines.append(k)
+        for c, v in sorted(per[k].items()):
+            lines.append(f"   {c:28s} {sum(v) / len(v):16.1f}  (n={len(v)})")
     text = "\n".join(lines)
     print(text)
     if out:
