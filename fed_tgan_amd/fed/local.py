@@ -386,15 +386,24 @@ def run_local_emulation(cfg, k: int, backend: str = "auto", device: Optional[tor
     runtimes: List[Optional[FedRuntime]] = [None] * k
     errors: List[BaseException] = []
 
+    # one HIP stream per emulated client: the clients' small step kernels (a few dozen workgroups each) run
+    # concurrently on the 256 CUs instead of queueing on one stream.  HIP maps streams onto its few hardware queues
+    # (GPU_MAX_HW_QUEUES, 4) round-robin in creation order, and a hardware queue runs its streams' kernels in
+    # order: the K client streams are created here, back to back, so they spread evenly (8 clients: 2 per queue).
+    # Created inside the threads they interleaved with each engine's capture / lane streams -- measured, 3 clients
+    # on one queue and 1 on another, 72 ms rounds for 8 clients (profiles/multiclient_r5.txt).
+    client_streams = None
+    if device.type == "cuda" and getattr(cfg, "client_streams", True):
+        torch.cuda.set_device(device)
+        client_streams = [torch.cuda.Stream(device) for _ in range(k)]
+
     def worker(rank: int):
         try:
             stream_ctx = contextlib.nullcontext()
             if device.type == "cuda":
                 torch.cuda.set_device(device)
-                # one HIP stream per emulated client: the clients' small step kernels (a few dozen
-                # workgroups each) run concurrently on the 256 CUs instead of queueing on one stream
-                if getattr(cfg, "client_streams", True):
-                    stream_ctx = torch.cuda.stream(torch.cuda.Stream(device))
+                if client_streams is not None:
+                    stream_ctx = torch.cuda.stream(client_streams[rank])
             with stream_ctx:
                 comm = ThreadComm(group, rank, device) if outer is None else HierComm(group, rank, device, outer)
                 rt = FedRuntime(cfg, comm, device, federator=0)
