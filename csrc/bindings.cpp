@@ -1157,6 +1157,18 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_decode_rows = (int)value;
     return prev;
   }
+  if (key == "chain_pre") {   // chained tail weights prefetched: 0 never, 1 grids of <= 512 workgroups, 2 always
+    TORCH_CHECK(value >= 0 && value <= 2, "chain_pre: 0, 1 or 2");
+    const int prev = fedtgan::g_chain_pre;
+    fedtgan::g_chain_pre = (int)value;
+    return prev;
+  }
+  if (key == "chain_rows") {  // head rows per chain workgroup when the one-row grid is too large to prefetch
+    TORCH_CHECK(value == 1 || value == 2, "chain_rows: 1 or 2");
+    const int prev = fedtgan::g_chain_rows;
+    fedtgan::g_chain_rows = (int)value;
+    return prev;
+  }
   if (key == "chain_coalesced") {   // chained tail GEMM: lane-contiguous weight rows + wave sums (1)
     const int prev = fedtgan::g_chain_coalesced;
     fedtgan::g_chain_coalesced = value ? 1 : 0;

@@ -1363,44 +1363,71 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue(GemmArgs g) {
 // were launches of their own after D0's / R0's reduction.
 constexpr int CH_MAXK = 1024, CH_COLS = 64;
 int g_chain_coalesced = 0;   // chain tail: per-column weight rows read lane-contiguous + wave sums (1) or one row per lane (0)
+int g_chain_pre = 1;         // chain tail weights prefetched: 0 never, 1 grids of <= 512 workgroups, 2 always
+int g_chain_rows = 2;        // 2: a grid too large for the prefetch runs two head rows per workgroup (with it)
 // MASK: head and tail both EPI_MASK (the R chain) -- the launch carries no Philox / BN epilogue code
-template <int SMAX, bool MASK = false, bool BT_ = false>
+// PRE: the tail's weights are prefetched (K = 256; host: grids that stay resident at the larger register count).
+// ROWS (PRE only): head rows per workgroup -- 2 halves the workgroups and the tail-weight traffic of a grid that
+// would not stay resident with one row each (the 150-row D phase).
+template <int SMAX, bool MASK = false, bool BT_ = false, bool PRE = false, int ROWS = 1>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
+  static_assert(ROWS == 1 || PRE, "two rows per workgroup only with the prefetched tail");
   const BIdx bi_ = batch_bidx<BT_>(g.xcd_cl);
-  __shared__ __attribute__((aligned(16))) float row[CH_MAXK];
-  __shared__ float part[4][CH_COLS];
+  __shared__ __attribute__((aligned(16))) float row[ROWS][CH_MAXK];
+  __shared__ float part[ROWS][4][CH_COLS];
   if (bi_.z) {
     client_view(g, bi_.z);
     client_view(t, bi_.z);
   }
-  const int m = bi_.x, s = bi_.y;
+  const int m0 = bi_.x * ROWS, s = bi_.y;
   const uint64_t step = (g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
+  // K = 256 (the discriminator's second layer): this thread's 16 float4 of its tail weight row do not depend on
+  // the head's row, so all 16 are requested before the slabs are reduced -- one round trip, overlapping the
+  // slabs' -- instead of four dependent batches of 4 after the barrier.  (Compile-time trip count: a runtime
+  // bound on the register array would put it in scratch.)  The 64 extra VGPRs (130 -> 194) leave room for two
+  // workgroups per CU instead of three, so one-row workgroups take it only in grids of <= 512 (host): measured,
+  // the 50-row chains 9.9 -> 9.1 and 7.9 -> 6.9 us, the 600-workgroup D-phase chain 11.9 -> 13.1 us.
+  constexpr int PQ = 16;
+  const bool pre = PRE && !t.chain_co && g.N == 16 * PQ;
+  float4 wp[PRE ? PQ : 1];
+  if (pre) {
+    const int jp = min(s * CH_COLS + (int)(threadIdx.x & (CH_COLS - 1)), t.N - 1);
+    const float4* w4 = reinterpret_cast<const float4*>(t.b + (size_t)jp * t.ldb) + (threadIdx.x >> 6) * PQ;
+#pragma unroll
+    for (int k = 0; k < (PRE ? PQ : 1); ++k) wp[k] = w4[k];
+  }
   for (int n = threadIdx.x; n < g.N; n += blockDim.x) {
-    float v;
-    if constexpr (SMAX > 0) {
-      v = splitk_value<SMAX, MASK>(g, (size_t)m * g.N + n, m, n, step);
-      if (s == 0) st_out(g.c, (size_t)m * g.ldc + n, v, g.wt);
-    } else {
-      v = g.c[(size_t)m * g.ldc + n];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      const int m = m0 + r;
+      float v = 0.f;
+      if (ROWS == 1 || m < g.M) {
+        if constexpr (SMAX > 0) {
+          v = splitk_value<SMAX, MASK>(g, (size_t)m * g.N + n, m, n, step);
+          if (s == 0) st_out(g.c, (size_t)m * g.ldc + n, v, g.wt);
+        } else {
+          v = g.c[(size_t)m * g.ldc + n];
+        }
+      }
+      row[r][n] = v;
     }
-    row[n] = v;
   }
   __syncthreads();
   const int jl = threadIdx.x & (CH_COLS - 1), kq = threadIdx.x >> 6;
   const int j = s * CH_COLS + jl;
-  if (t.chain_co) {
+  if (!PRE && t.chain_co) {
     // wave kq owns 16 of the block's 64 output columns; for each, the 64 lanes read the column's weight row as
     // consecutive float4 (one coalesced 1 KB request per 256 K values, instead of 64 rows 1 KB apart per
     // request) and a wave sum finishes the dot product
     constexpr int JW = CH_COLS / 4;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, m = m0;
     float p[JW];
 #pragma unroll
     for (int jj = 0; jj < JW; ++jj) p[jj] = 0.f;
     for (int k0 = 0; k0 < g.N; k0 += 256) {
       const int k = k0 + 4 * lane;
       const bool kin = k < g.N;
-      const float4 x = kin ? *reinterpret_cast<const float4*>(row + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = kin ? *reinterpret_cast<const float4*>(row[0] + k) : make_float4(0.f, 0.f, 0.f, 0.f);
       float4 w[JW];
 #pragma unroll
       for (int jj = 0; jj < JW; ++jj) {
@@ -1414,11 +1441,11 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
 #pragma unroll
     for (int jj = 0; jj < JW; ++jj) {
       const float tsum = wave_sum(p[jj]);
-      if (lane == 0) part[0][kq * JW + jj] = tsum;
+      if (lane == 0) part[0][0][kq * JW + jj] = tsum;
     }
     __syncthreads();
     if (kq == 0 && j < t.N) {
-      float v = t.alpha * part[0][jl];
+      float v = t.alpha * part[0][0][jl];
       if (t.bias) v += t.bias[j];
       const uint64_t st = (t.epi == EPI_LRELU_DROPOUT && t.rng_ctr) ? *t.rng_ctr : 0ull;
       if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
@@ -1427,27 +1454,49 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
     return;
   }
   const int q4 = g.N / 16;                       // float4 per K-quarter (host: N % 16 == 0)
-  float a0 = 0.f, a1 = 0.f;
-  if (j < t.N) {
-    const float4* w4 = reinterpret_cast<const float4*>(t.b + (size_t)j * t.ldb) + kq * q4;
-    const float4* r4 = reinterpret_cast<const float4*>(row) + kq * q4;
-#pragma unroll 4
-    for (int k = 0; k < q4; ++k) {
-      const float4 w = w4[k], x = r4[k];
-      a0 = fmaf(w.x, x.x, a0);
-      a1 = fmaf(w.y, x.y, a1);
-      a0 = fmaf(w.z, x.z, a0);
-      a1 = fmaf(w.w, x.w, a1);
+  if (pre) {
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      const float4* r4 = reinterpret_cast<const float4*>(row[r]) + kq * PQ;
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < (PRE ? PQ : 1); ++k) {
+        const float4 w = wp[k], x = r4[k];
+        a0 = fmaf(w.x, x.x, a0);
+        a1 = fmaf(w.y, x.y, a1);
+        a0 = fmaf(w.z, x.z, a0);
+        a1 = fmaf(w.w, x.w, a1);
+      }
+      part[r][kq][jl] = a0 + a1;
     }
+  } else {
+    float a0 = 0.f, a1 = 0.f;
+    if (j < t.N) {
+      const float4* w4 = reinterpret_cast<const float4*>(t.b + (size_t)j * t.ldb) + kq * q4;
+      const float4* r4 = reinterpret_cast<const float4*>(row[0]) + kq * q4;
+#pragma unroll 4
+      for (int k = 0; k < q4; ++k) {
+        const float4 w = w4[k], x = r4[k];
+        a0 = fmaf(w.x, x.x, a0);
+        a1 = fmaf(w.y, x.y, a1);
+        a0 = fmaf(w.z, x.z, a0);
+        a1 = fmaf(w.w, x.w, a1);
+      }
+    }
+    part[0][kq][jl] = a0 + a1;
   }
-  part[kq][jl] = a0 + a1;
   __syncthreads();
   if (kq == 0 && j < t.N) {
-    float v = t.alpha * ((part[0][jl] + part[1][jl]) + (part[2][jl] + part[3][jl]));
-    if (t.bias) v += t.bias[j];
     const uint64_t st = (t.epi == EPI_LRELU_DROPOUT && t.rng_ctr) ? *t.rng_ctr : 0ull;
-    if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
-    else t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      const int m = m0 + r;
+      if (ROWS > 1 && m >= g.M) break;
+      float v = t.alpha * ((part[r][0][jl] + part[r][1][jl]) + (part[r][2][jl] + part[r][3][jl]));
+      if (t.bias) v += t.bias[j];
+      if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
+      else t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+    }
   }
 }
 
@@ -1629,12 +1678,26 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     // float4 loads from t.b + jc * t.ldb + k: the row stride and the base must keep them 16-B aligned
     t.chain_co = g_chain_coalesced && (g.N % 4 == 0) && (t.ldb % 4 == 0) &&
                  ((reinterpret_cast<uintptr_t>(t.b) & 15) == 0);
-    const dim3 grid(g.M, (t.N + CH_COLS - 1) / CH_COLS, g.nclient), block(256);
+    const int nb = (t.N + CH_COLS - 1) / CH_COLS;
     const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
-#define FEDTGAN_CHAIN(S)                                                                                 \
-  do {                                                                                                   \
-    if (mk) hipLaunchKernelGGL((g.xcd_cl ? chain_epilogue_kernel<S, true, true> : chain_epilogue_kernel<S, true, false>), grid, block, 0, stream, h, t);          \
-    else hipLaunchKernelGGL((g.xcd_cl ? chain_epilogue_kernel<S, false, true> : chain_epilogue_kernel<S, false, false>), grid, block, 0, stream, h, t);            \
+    // prefetched tail weights (K = 256) where the grid stays resident at 194 VGPRs (<= 512 workgroups): one row
+    // per workgroup, or two when one row each would overflow (g_chain_rows)
+    const bool can_pre = g.nclient <= 1 && g.N == 256 && !t.chain_co && g_chain_pre > 0;
+    const bool big = (int64_t)g.M * nb > 512;
+    const int rows = (can_pre && big && g_chain_rows == 2 && (int64_t)((g.M + 1) / 2) * nb <= 512) ? 2 : 1;
+    const bool pre = can_pre && (rows == 2 || !big || g_chain_pre == 2);
+    const dim3 grid((g.M + rows - 1) / rows, nb, g.nclient), block(256);
+#define FEDTGAN_CHAIN_K(S, MK)                                                                                       \
+  do {                                                                                                               \
+    if (g.xcd_cl) hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, true>), grid, block, 0, stream, h, t);            \
+    else if (rows == 2) hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, false, true, 2>), grid, block, 0, stream, h, t); \
+    else if (pre) hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, false, true>), grid, block, 0, stream, h, t);     \
+    else hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, false>), grid, block, 0, stream, h, t);                    \
+  } while (0)
+#define FEDTGAN_CHAIN(S)              \
+  do {                                \
+    if (mk) FEDTGAN_CHAIN_K(S, true);  \
+    else FEDTGAN_CHAIN_K(S, false);    \
   } while (0)
     if (g.splitk <= 1 || g.red_inl) FEDTGAN_CHAIN(0);
     else if (g.splitk <= 8) FEDTGAN_CHAIN(8);
@@ -1642,6 +1705,7 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     else if (g.splitk <= 32) FEDTGAN_CHAIN(32);
     else FEDTGAN_CHAIN(64);
 #undef FEDTGAN_CHAIN
+#undef FEDTGAN_CHAIN_K
     return;
   }
   if (g.splitk <= 1 || g.red_inl) return;

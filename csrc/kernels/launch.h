@@ -229,6 +229,8 @@ void launch_gp_scale(const float* g, int ldg, float* out, int ldo, int rows, int
                      int loss_per_row, float* ws, int64_t ws_n, hipStream_t stream);
 extern int g_gp_split;
 extern int g_chain_coalesced;   // set_tuning("chain_coalesced")
+extern int g_chain_pre;         // set_tuning("chain_pre")
+extern int g_chain_rows;        // set_tuning("chain_rows")
 extern int g_gp_threads;   // register-resident gp_scale workgroup size (set_tuning("gp_threads"))
 extern int g_bn_threads;   // BN workgroup size (set_tuning("bn_threads"))
 extern int g_act_rowreg_narrow;   // narrow rows on the register-resident row kernels (set_tuning("act_rowreg_narrow"))

@@ -460,6 +460,38 @@ def test_chain_tail_coalesced_matches_row_per_lane():
     assert (f0 - f1).abs().max().item() <= 2 * 2e-4 + 1e-6
 
 
+@pytest.mark.parametrize("batch", [500, 510])
+def test_chain_tail_prefetch_matches_plain(batch):
+    """set_tuning("chain_pre" / "chain_rows"): the chained tail with its weights prefetched before the slab
+    reduction, one head row per workgroup (the 50-row G-phase / R chains) or two (the 150-row D phase; batch 510:
+    153 rows, an odd last pair), gives the outputs of the plain tail (same products, same order: bitwise) and a
+    step with it trains the same parameters."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    res = []
+    for pre, rows in ((0, 1), (1, 1), (1, 2), (2, 1)):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=batch, precision="fp32"), DEV, backend="hip", seed=14)
+        eng.set_training_data(X)
+        p0 = torch.ops.fedtgan.set_tuning("chain_pre", pre)
+        r0 = torch.ops.fedtgan.set_tuning("chain_rows", rows)
+        try:
+            eng.train_steps(1, use_graph=False)
+            torch.cuda.synchronize()
+            res.append((eng.dl[1].clone(), eng.flat.clone()))
+            eng.train_steps(8, use_graph=True)
+            torch.cuda.synchronize()
+            assert bool(torch.isfinite(eng.flat).all())
+        finally:
+            torch.ops.fedtgan.set_tuning("chain_pre", p0)
+            torch.ops.fedtgan.set_tuning("chain_rows", r0)
+    d0, f0 = res[0]
+    for d, f in res[1:]:
+        assert torch.equal(d, d0), float((d - d0).abs().max())
+        assert torch.equal(f, f0), float((f - f0).abs().max())
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_bn_fold_matches_bn_launches(precision):
     """EngineConfig.bn_fold: the generator's BatchNorm folded into its GEMMs (partials from the producing GEMM,
