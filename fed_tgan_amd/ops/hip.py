@@ -27,6 +27,11 @@ LONG_K_64 = True    # _plan's long-K rule with 64x64 tiles when workgroups are p
 # 128x128 tiles covering less than two waves of the 256 CUs give way to 64x64 tiles when those still number
 # >= 1024 (the wide table's G-out forward: 440 128-tiles, 1.7 waves, with a short K of 640) (A/B knob)
 WAVE_FILL_64 = False
+# long-K GEMMs over 128..255 rows (the wide table's D0 forward: 150 x 256 x 137,800) with 128x128 tiles and deep
+# split-K: the 150 rows are 2 row tiles instead of 3, so W0 (141 MB) streams twice instead of three times, and X
+# (83 MB) twice instead of four times (A/B knob).  Measured slower, off: wide 0.2489 / 0.2504 -> 0.2541 / 0.2552
+# s/epoch (profiles/wide_r5.md)
+LONG_K_128 = False
 
 
 def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
@@ -64,6 +69,9 @@ def _plan(M: int, N: int, K: int, kc: int = 128, clients: int = 1) -> tuple:
     cap_ws = max(1, (6 << 20) // max(1, M * N * 4))
     want = max(-(-512 // t32), -(-bursts // 8))
     sk32 = int(max(1, min(want, -(-bursts // 2), cap_ws)))
+    if LONG_K_128 and c == 1 and 128 <= M < 256 and N >= 128 and bursts >= 256:
+        want = max(-(-256 // t128), -(-bursts // 16))
+        return 128, int(max(1, min(want, GEMM_MAX_SPLITS, -(-bursts // 2))))
     if LONG_K_64 and c == 1 and t32 * min(sk32, 64) >= 768:
         # plenty of workgroups either way (the wide table's K = 137k): 64x64 tiles re-read the long operands half as
         # often (the 150-row D0 input by 4 instead of 8 column tiles, W0 by 3 instead of 5 row tiles).  Measured
