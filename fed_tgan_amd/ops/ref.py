@@ -29,6 +29,7 @@ class TorchOps:
     # EngineConfig.bn_fold on this backend (the GEMM-folded BatchNorm stated in torch: the oracle of the HIP
     # path's partials / BN-on-load / materialisation; off by default -- the eager path runs BN as its own op)
     bn_fold_capable = False
+    _bnl = None                  # pending gemm_bnl_next configuration (class default: subclasses need no __init__)
 
     def __init__(self):
         self._bnl = None

@@ -46,6 +46,9 @@ class Comm:
         self.share_pg = {}          # dedicated federator rank -> gloo pair group {first client, federator}
         self._share = None          # first client: (pinned buffer, side stream, executor, pending send)
         self.initialized = False
+        # RCCL data plane: fold the client weight into the all-reduce (pre-multiplied sum) instead of scaling the
+        # buffer first (tools/premul_probe.py checks it against x * w on the box)
+        self.premul_sum = True
         # ``force_dist``: build real process groups even for one rank, so the collective branches
         # (RCCL all-reduce / gather / send-recv) execute on a single-GPU box instead of the
         # world-size-1 short-circuits
@@ -224,6 +227,11 @@ class Comm:
             return flat
         if self.data_backend == "nccl":
             if self.is_client:
+                if weight != 1.0 and self.premul_sum and hasattr(dist, "_make_nccl_premul_sum"):
+                    # the client weight rides in the collective (RCCL's pre-multiplied sum: each rank's input is
+                    # scaled as it is loaded), so no separate scaling launch precedes the all-reduce
+                    dist.all_reduce(flat, op=dist._make_nccl_premul_sum(float(weight)), group=self.data)
+                    return flat
                 if weight != 1.0:
                     flat.mul_(weight)
                 dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.data)
