@@ -1,4 +1,5 @@
-"""Training quality on a reduced WIDE table: the reference's own code vs this framework, same data.
+"""Training quality on a reduced WIDE table (or a built-in spec, --spec adult / covertype, optionally with
+Dirichlet non-IID shards): the reference's own code vs this framework, same data.
 
 BASELINE config 5 (100k rows x 512 columns) has no published reference number, and the reference's
 CPU code cannot train it in reasonable time.  This tool builds a reduced wide table the reference CAN
@@ -39,21 +40,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-from fed_tgan_amd.data.schema import wide_spec  # noqa: E402
-from fed_tgan_amd.data.synthetic import generate  # noqa: E402
+from fed_tgan_amd.data.schema import get_spec, wide_spec  # noqa: E402
+from fed_tgan_amd.data.synthetic import generate, shard  # noqa: E402
 
 
-def make_wide_split(out: str, n_cols: int, rows: int, clients: int, seed: int = 2025):
-    """``rows`` per client of the ``wide:<n_cols>`` table; train.csv = the union of the shards."""
-    spec = wide_spec(n_cols)
+def make_wide_split(out: str, n_cols: int, rows: int, clients: int, seed: int = 2025, spec_name: str | None = None,
+                    shard_mode: str = "contiguous", alpha: float = 0.3):
+    """``rows`` per client of the ``wide:<n_cols>`` table (or of a built-in spec: ``spec_name`` = adult /
+    covertype / intrusion); train.csv = the union of the shards.  shard_mode "dirichlet": label-skewed
+    Dirichlet(alpha) shards of the spec's target column (``data.synthetic.shard``), the non-IID config-4 split."""
+    spec = get_spec(spec_name) if spec_name else wide_spec(n_cols)
     df = generate(spec, rows * clients, seed=seed)
     d = os.path.join(out, "data")
     os.makedirs(d, exist_ok=True)
     train = os.path.join(d, "train.csv")
     if not os.path.exists(train):
         df.to_csv(train, index=False)
-        for i, part in enumerate(np.array_split(np.arange(len(df)), clients)):
-            df.iloc[part].to_csv(os.path.join(d, f"client{i}.csv"), index=False)
+        if shard_mode == "dirichlet":
+            parts = shard(df, clients, "dirichlet", seed=seed, target=spec.target_column, alpha=alpha)
+        else:
+            parts = [df.iloc[p] for p in np.array_split(np.arange(len(df)), clients)]
+        for i, part in enumerate(parts):
+            part.to_csv(os.path.join(d, f"client{i}.csv"), index=False)
     return spec, train, os.path.join(d, "client{client}.csv")
 
 
@@ -74,7 +82,8 @@ def run_reference(ref_dir: str, work: str, spec, train_path: str, datapath: str,
     import similarity_analysis as rsim      # (reference)
     t0 = time.time()
     cs = [rdist.MDGANClient(datapath.format(client=i), list(spec.selected_variables), list(spec.categorical_list),
-                            [], {}, spec.target_column, spec.problem_type, epochs) for i in range(clients)]
+                            list(spec.nonnegative_list), dict(spec.date_dic), spec.target_column, spec.problem_type,
+                            epochs) for i in range(clients)]
     server = rdist.MDGANServer([FakeRRefAsync(c) for c in cs], epochs)
     server.uniform_meta_category()
     server.uniform_continuous_gmm()
@@ -138,6 +147,9 @@ def main():
     ap.add_argument("--impl", choices=["reference", "ours"], required=True)
     ap.add_argument("--reference", default="/root/reference/Server")
     ap.add_argument("--cols", type=int, default=128)
+    ap.add_argument("--spec", default=None, help="a built-in spec (adult, covertype, intrusion) instead of wide:<cols>")
+    ap.add_argument("--shard", default="contiguous", choices=["contiguous", "dirichlet"])
+    ap.add_argument("--alpha", type=float, default=0.3, help="Dirichlet concentration of --shard dirichlet")
     ap.add_argument("--rows", type=int, default=10000, help="rows per client")
     ap.add_argument("--clients", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=8)
@@ -150,7 +162,8 @@ def main():
     ap.add_argument("--out", default=None, help="append one JSON line per seed to this file")
     ap.add_argument("--threads", type=int, default=0)
     args = ap.parse_args()
-    spec, train_path, datapath = make_wide_split(args.work, args.cols, args.rows, args.clients)
+    spec, train_path, datapath = make_wide_split(args.work, args.cols, args.rows, args.clients, spec_name=args.spec,
+                                                 shard_mode=args.shard, alpha=args.alpha)
     if args.impl == "reference":
         import reference_quality  # noqa: F401  (it puts this repo first on sys.path: import it before the reference)
         shim = os.path.join(args.work, "shim")
@@ -175,7 +188,8 @@ def main():
         else:
             r = run_ours(work, spec, train_path, datapath, args.clients, seed, args.epochs, args.backend,
                          args.precision, args.force_wide)
-        r.update({"cols": args.cols, "rows_per_client": args.rows, "clients": args.clients, "tuning": args.tuning})
+        r.update({"spec": spec.name, "shard": args.shard, "cols": args.cols, "rows_per_client": args.rows,
+                  "clients": args.clients, "tuning": args.tuning})
         runs.append(r)
         print(json.dumps(r), flush=True)
         if args.out:
