@@ -152,3 +152,29 @@ def test_meta_json_dump(tmp_path):
     dump_meta_json(meta, str(p))
     again = json.loads(p.read_text())
     assert again["columns"][0]["column_name"] == "duration"
+
+
+@pytest.mark.parametrize("name", ["intrusion", "adult"])
+def test_arrow_reader_matches_pandas(tmp_path, name):
+    """read_csv_table(reader="arrow") (pyarrow's parser, dictionary-encoded strings) gives the preprocessor the same
+    metadata, vocabulary and encoded matrix as pd.read_csv -- including pandas' missing-value spellings in a
+    categorical column."""
+    pytest.importorskip("pyarrow")
+    from fed_tgan_amd.data.table import read_csv_table
+    spec = get_spec(name)
+    df = generate(spec, 3000, seed=5)
+    cat = spec.categorical_list[0]
+    df = df.astype({cat: object})
+    df.loc[df.index[5::89], cat] = np.nan               # gaps in a categorical column
+    path = tmp_path / "client.csv"
+    df.to_csv(path, index=False)
+    text = path.read_text().replace(",,", ",NA,", 3)    # pandas' "NA" spelling too
+    path.write_text(text)
+    tps = [_tp(read_csv_table(str(path), r)[spec.selected_variables], spec) for r in ("pandas", "arrow")]
+    m0, m1 = (dict(tp.local_meta()) for tp in tps)
+    m0.pop("name"), m1.pop("name")                     # (the reference's per-instance name suffix)
+    assert json.dumps(m0, sort_keys=True, default=str) == json.dumps(m1, sort_keys=True, default=str)
+    metas = [tps[0].local_meta()]
+    _, vocabs, _ = merge_categorical_metas(metas)
+    a, b = (tp.encode(vocabs) for tp in tps)
+    np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
