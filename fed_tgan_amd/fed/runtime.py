@@ -120,6 +120,10 @@ class FedConfig:
     # then is device time; without it the next round's launches queue behind the generation and the host
     # returns at once (the epoch CSV's own hand-off waits for the table copy either way)
     round_sync: bool = True
+    # generate round r's epoch table while round r + 1 trains (CTGANEngine.generate_decoded_split: a ~10 us prep
+    # on the training stream snapshots what generation reads, the sampler / generator / decode run on a side
+    # stream).  None = on where it applies (one process per GPU, HIP bf16 generation with graphs, FedAvg)
+    pipeline_sample: Optional[bool] = None
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -376,6 +380,11 @@ class FedRuntime:
             # threads): a failure falls back to per-thread engines instead of aborting round 0
             self._prepare_batched()
         self.csv_cols = csv_layout(merged, self.vocabs)     # None: a date format only the pandas path handles
+        if getattr(self, "thread_local_capture", False):
+            # client threads of one process: none captures its graphs while another still uploads its tables (a
+            # pageable host-to-device copy fails while any stream of the process captures -- with independent
+            # initial weights nothing else orders the threads here)
+            self.comm.barrier()
         self._prepare_round_zero()
         self.init_times["engine"] = time.time() - t0
         # RCCL's lazy communicator / P2P setup happens here, not in round 0
@@ -404,7 +413,10 @@ class FedRuntime:
         # (a batched engine's step graphs were captured by _prepare_batched)
         train = 0 if getattr(self, "batched", False) or not self.is_client or not self.engine.tables \
             else self.engine.steps_per_epoch
-        self.engine.prepare_graphs(train, gen)
+        self._pipe = self._pipeline_sample()
+        if self._pipe:
+            self._gen_stream = torch.cuda.Stream(self.device)
+        self.engine.prepare_graphs(train, gen, gen_split=self._pipe)
         if self.is_fed and cfg.write_csv and cfg.async_csv:
             self._copy_stream = torch.cuda.Stream(self.device)
             # the table of round r is held by the writer while round r + 1 copies its own: two (three if the
@@ -418,6 +430,17 @@ class FedRuntime:
                 self._writer = AsyncTableWriter()
             self._writer.submit(self._warm_csv, n_cols)     # the writer thread (and the formatter's) start now
             self._writer.flush()
+
+    def _pipeline_sample(self) -> bool:
+        """FedConfig.pipeline_sample resolved: the table of round r is generated on a side stream while round
+        r + 1 trains.  Off in the in-process client emulations (their threads order the gather with events of
+        their own streams) and for a batched engine."""
+        cfg = self.cfg
+        if cfg.pipeline_sample is False or self.device.type != "cuda" or cfg.mode != "fedavg":
+            return False
+        if getattr(self, "batched", False) or type(self.comm).__name__ != "Comm":
+            return False
+        return bool(self.engine.can_split_generation())
 
     def _warm_csv(self, n_cols: int):
         """One table of the real size and shape through the native formatter to the null device, on the writer
@@ -692,20 +715,26 @@ class FedRuntime:
         # stream and the writer waits for it: round r's copy + CSV overlap round r + 1's training
         # (bench.py's timed region still ends with every table on disk)
         async_copy = self.cfg.async_csv and self.device.type == "cuda"
+        # (pipelined: the rows come from the generation side stream, and the gather / copy are ordered on it, so
+        # the round ends without waiting for them -- the next round's training overlaps them)
+        pipe = bool(getattr(self, "_pipe", False)) and self.rank in samplers
+        gen = (lambda k: self.engine.generate_decoded_split(k, self._gen_stream)) if pipe \
+            else self.engine.generate_decoded
+        on_gen = (lambda: torch.cuda.stream(self._gen_stream)) if pipe else contextlib.nullcontext
         if len(samplers) == 1:
             if self.rank in samplers:
                 with self._sub("generate"):
-                    vals = self.engine.generate_decoded(per[0])
-                with self._sub("d2h"):
+                    vals = gen(per[0])
+                with self._sub("d2h"), on_gen():
                     share = self._host(vals) if async_copy else vals.cpu().numpy()
         else:
             # every client decodes its share on its GPU; one gather to the federator (RCCL over
             # xGMI when the data plane is RCCL), one device-to-host copy there
             with self._sub("generate"):
-                vals = self.engine.generate_decoded(per[samplers.index(self.rank)])
-            with self._sub("gather"):
+                vals = gen(per[samplers.index(self.rank)])
+            with self._sub("gather"), on_gen():
                 rows = c.gather_rows(vals, per, samplers, dst=self.federator, to_host=not async_copy)
-            with self._sub("d2h"):
+            with self._sub("d2h"), on_gen():
                 if self.is_fed:
                     if rows.device.type == "cuda":
                         share = self._host(rows)

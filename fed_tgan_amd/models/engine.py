@@ -213,6 +213,8 @@ class CTGANEngine:
         self.gen_tables = None
         self._gen_bufs = None
         self._gen_graphs: Dict[int, tuple] = {}   # n -> (hipGraph, H, logits, out) of generate_decoded
+        self._gen_split: Dict[int, tuple] = {}    # n -> (prep graph, body graph, H, logits, out, col, opt)
+        self._gen_done = None                     # event: the last pipelined generation body has finished
         self.graphs: Dict[int, object] = {}    # steps per graph -> captured hipGraph
         self.capture_mode = "global"   # "thread_local" when several engines capture from threads
         self.bn_batches = 0       # num_batches_tracked of every BN layer
@@ -571,6 +573,7 @@ class CTGANEngine:
                            "sd": torch.as_tensor(sd, dtype=torch.float64, device=dev)}
         self._gen_bufs = None
         self._gen_graphs = {}
+        self._gen_split = {}
 
     # ================================================================= forward pieces
     def _kpad(self, H, a: int, W: torch.Tensor):
@@ -1063,7 +1066,7 @@ class CTGANEngine:
         instantiation (segfault in capture_end, 100k x 512 table, round 5)."""
         return self.device.type == "cuda" and self.ops.name == "hip"
 
-    def prepare_graphs(self, steps: int | None = None, gen_rows: Sequence[int] = ()) -> None:
+    def prepare_graphs(self, steps: int | None = None, gen_rows: Sequence[int] = (), gen_split: bool = False) -> None:
         """Capture, ahead of the first round, every hipGraph that ``train_steps(steps)`` and
         ``generate_decoded(n)`` for ``n`` in ``gen_rows`` will replay: the capture (one eager warm-up step
         or pass plus the capture itself, ~40 ms for the Intrusion step graph) then happens at
@@ -1080,7 +1083,10 @@ class CTGANEngine:
                 self._capture(1)
         if self.gen_tables is not None and self.cfg.gen_graph and self.ops.name == "hip":
             for n in gen_rows:
-                if n > 0 and n not in self._gen_graphs:
+                if n > 0 and gen_split and self.can_split_generation():
+                    if n not in self._gen_split:
+                        self._capture_gen_split(int(n))
+                elif n > 0 and n not in self._gen_graphs:
                     self._capture_gen(int(n))
 
     def _graph_key(self, steps: int):
@@ -1157,6 +1163,8 @@ class CTGANEngine:
             raise RuntimeError("set_generation_tables() first")
         if use_graph is None:
             use_graph = self.device.type == "cuda" and self.cfg.gen_graph and self.ops.name == "hip"
+        if self._gen_done is not None:    # a pipelined body may still read the shared weight copies
+            torch.cuda.current_stream(self.device).wait_event(self._gen_done)
         if use_graph:
             ent = self._gen_graphs.get(n) or self._capture_gen(n)
             ent[0].replay()
@@ -1167,6 +1175,95 @@ class CTGANEngine:
         if hasattr(self.ops, "check"):
             self.ops.check()
         return out
+
+    # ------------------------------------------------------------------ pipelined generation
+    def can_split_generation(self) -> bool:
+        """generate_decoded_split applies: HIP bf16 generation with graphs."""
+        return (self.device.type == "cuda" and self.gen16 and self.cfg.gen_graph and self.ops.name == "hip" and
+                self.gen_tables is not None and getattr(self.ops, "batch_k", 1) == 1)
+
+    def generate_decoded_split(self, n: int, gen_stream: "torch.cuda.Stream") -> torch.Tensor:
+        """generate_decoded(n) in two parts, so the table of round r is generated while round r + 1 trains.
+
+        The prep graph (on the current stream, ~10 us) copies everything the generation reads from the live model
+        -- the bf16 / transposed weight copies of gen_weight_prep, each layer's bias, BatchNorm affine and running
+        statistics, the output bias -- and snapshots the RNG step counter, advancing the live one by the body's
+        bumps; the body graph (sampler, eval generator, decode) then runs on ``gen_stream`` reading only those
+        copies.  The table is bit-identical to generate_decoded(n), and training's random numbers are unchanged
+        (the live counter moves exactly as the unsplit pass would move it).  Returns a fresh tensor whose
+        producer is ``gen_stream``."""
+        ent = self._gen_split.get(n) or self._capture_gen_split(n)
+        cur = torch.cuda.current_stream(self.device)
+        if self._gen_done is not None:          # the previous body still reads the snapshot
+            cur.wait_event(self._gen_done)
+        ent[0].replay()
+        gen_stream.wait_stream(cur)
+        with torch.cuda.stream(gen_stream):
+            ent[1].replay()
+            out = ent[4].clone()
+            done = torch.cuda.Event()
+            done.record(gen_stream)
+        self._gen_done = done
+        if hasattr(self.ops, "check"):
+            self.ops.check()
+        return out
+
+    def _gen_snapshot(self):
+        if getattr(self, "_gsnap", None) is None:
+            names = [f"G.{i}.{k}" for i in range(len(self.gdims)) for k in ("b", "gamma", "beta", "rm", "rv")]
+            names.append("G.out.b")
+            self._gsnap = {nm: torch.empty_like(self.p[nm]) for nm in names}
+            self._gsnap_pairs = ([self._gsnap[nm] for nm in names], [self.p[nm] for nm in names])
+            self._gsnap_ctr = torch.zeros_like(self.ops.ctr)
+        return self._gsnap
+
+    def _gen_prep(self, n: int):
+        self._gen_weights16()
+        self._gen_snapshot()
+        torch._foreach_copy_(*self._gsnap_pairs)
+        self._gsnap_ctr.copy_(self.ops.ctr)
+        for _ in range(-(-n // self.cfg.gen_chunk)):     # the body's decode bumps, once per chunk
+            self.ops.L.rng_bump(self.ops.ctr)
+
+    def _gen_body(self, n: int, out: torch.Tensor, bufs):
+        w16 = (self._gw16, self._gwt)
+        for a in range(0, n, self.cfg.gen_chunk):
+            b = min(n, a + self.cfg.gen_chunk)
+            H, logits, col, opt = bufs(b - a)
+            self.ops.sample_gen(self.gen_cond, H, self.c_cols, self.z_cols, col_out=col, opt_out=opt, stream_id=21,
+                                ctr=self._gsnap_ctr)
+            self._g_forward16(H, logits, w16, (col, opt), params=self._gsnap)
+            self.ops.sample_decode(logits, out[a:b], self.gen_tables, stream_id=23, ctr=self._gsnap_ctr)
+
+    def _capture_gen_split(self, n: int):
+        from ..utils.devsync import CAPTURE_LOCK
+        m = min(n, self.cfg.gen_chunk)
+        H = self._gen_h16(m)
+        lg = _padded_rows(m, self.Dd, self.device)
+        col, opt = (torch.zeros(m, dtype=torch.int32, device=self.device) for _ in range(2))
+        out = torch.empty(n, len(self.gen_tables["cols"]), dtype=torch.float64, device=self.device)
+        bufs = lambda k: (H[:k], lg[:k], col[:k], opt[:k])  # noqa: E731
+        lane = self.ops.lane
+        with CAPTURE_LOCK:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            # the body runs beside training: its own split-K / scratch slots (ops lane 7), never the step's
+            self.ops.lane = 7
+            try:
+                with torch.cuda.stream(s):      # warm-up (decode tables, lazy init); advances the RNG once
+                    self._gen_prep(n)
+                    self._gen_body(n, out, bufs)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                torch.cuda.synchronize(self.device)
+                gp, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gp, capture_error_mode=self.capture_mode):
+                    self._gen_prep(n)
+                with torch.cuda.graph(gb, capture_error_mode=self.capture_mode):
+                    self._gen_body(n, out, bufs)
+            finally:
+                self.ops.lane = lane
+        self._gen_split[n] = (gp, gb, H, lg, out, col, opt)
+        return self._gen_split[n]
 
     def _gen_pass(self, n: int, out: torch.Tensor, bufs):
         w16 = self._gen_weights16() if self.gen16 else None
@@ -1207,11 +1304,12 @@ class CTGANEngine:
         self.ops.L.gen_weight_prep([self.p[nm] for nm in names], [c0 - a for a in starts], self._gw16, self._gwt)
         return self._gw16, self._gwt
 
-    def _g_forward16(self, H16, logits, w16, cond):
+    def _g_forward16(self, H16, logits, w16, cond, params=None):
         """Eval-mode generator on the bf16 buffer: each layer's GEMM reads bf16 rows and weights,
         gathers the one-hot block from col / opt, and writes bf16 (BN-eval + ReLU epilogue); the output
-        layer writes fp32 logits.  w16 = _gen_weights16()."""
-        o, p = self.ops, self.p
+        layer writes fp32 logits.  w16 = _gen_weights16(); params: biases / BN tensors by name (default the
+        live ones; the pipelined generation passes its snapshot)."""
+        o, p = self.ops, (self.p if params is None else params)
         c0 = self.c_cols[0]
         col, opt = cond
         wd, wt = w16

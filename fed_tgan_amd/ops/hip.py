@@ -392,11 +392,13 @@ class HipOps:
                           t["cond_width"], None, None, None, None, col_out, opt_out, sc[0], sc[1], metrics,
                           bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
 
-    def sample_gen(self, t, h, c_cols, z_cols, col_out=None, opt_out=None, stream_id=0):
+    def sample_gen(self, t, h, c_cols, z_cols, col_out=None, opt_out=None, stream_id=0, ctr=None):
+        """ctr: the step counter to key the draws on (default the engine's; the pipelined generation passes its
+        snapshot)."""
         E = z_cols[1] - z_cols[0]
         self.L.sample(h, z_cols[0], c_cols[0], E, None, None, 0, t["cdf_emp"], t["cond_offset"], t["cond_width"],
-                      None, None, None, None, col_out, opt_out, None, None, None, False, self.seed, self.ctr,
-                      int(stream_id) * 16)
+                      None, None, None, None, col_out, opt_out, None, None, None, False, self.seed,
+                      self.ctr if ctr is None else ctr, int(stream_id) * 16)
 
     # ------------------------------------------------------------------ activations
     def activate(self, logits, out, spans, tau=0.2, stream_id=0, slerp=None):
@@ -547,10 +549,11 @@ class HipOps:
             self._dec[key] = q
         return q
 
-    def sample_decode(self, logits, out, tabs, stream_id=0):
+    def sample_decode(self, logits, out, tabs, stream_id=0, ctr=None):
+        ctr = self.ctr if ctr is None else ctr
         kind, start, width, cont, code_off, codes, mu, sd = self._decode_tables(tabs)
-        self.L.sample_decode(logits, out, kind, start, width, cont, code_off, codes, mu, sd, self.seed, self.ctr,
+        self.L.sample_decode(logits, out, kind, start, width, cont, code_off, codes, mu, sd, self.seed, ctr,
                              int(stream_id) * 16, self._decode_ecol(tabs, logits.shape[1]),
                              self._decode_quads(tabs, logits.shape[1]))
-        self.L.rng_bump(self.ctr)
+        self.L.rng_bump(ctr)
         return out
