@@ -62,6 +62,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="native set_tuning knob for A/B measurements, e.g. --tuning gemm_xcd_remap=0")
     ap.add_argument("--phase-timer", default="events", choices=["events", "sync"],
                     help="phase timers: HIP events (no host sync) or stream-synchronised wall time")
+    ap.add_argument("--native-rccl", action="store_true",
+                    help="the weight all-reduce through the native RCCL plane (csrc/comm) instead of torch.distributed")
     ap.add_argument("--force-dist", action="store_true",
                     help="build real process groups even for one rank (1 GPU: the aggregation runs as an "
                          "RCCL all-reduce on a one-rank communicator)")
@@ -179,6 +181,8 @@ def run_rank(args) -> None:
     if args.force_dist and world == 1:
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
     rccl_dir = _rccl_log_setup() if (device.type == "cuda" and (world > 1 or args.force_dist)) else None
+    if args.native_rccl:
+        os.environ["FEDTGAN_NATIVE_RCCL"] = "1"
     comm = Comm.from_env("auto", device, force_dist=args.force_dist)
     n_data = comm.data_world_size()
     if n_data != world:
@@ -279,6 +283,7 @@ def run_rank(args) -> None:
                 except Exception:   # pragma: no cover - build without RCCL
                     ver = None
             rec["comm"] = {"data_world_size": dist.get_world_size(comm.data), "data_backend": comm.data_backend,
+                           "all_reduce_plane": "native" if getattr(comm, "_native", None) is not None else "torch",
                            "rccl_version": ver, "transport": _rccl_transport(rccl_dir)}
         if args.engine:
             rec["engine_overrides"] = args.engine

@@ -5,9 +5,11 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cstring>
 #include <string>
 #include <vector>
 
+#include "comm/rccl_comm.h"
 #include "host/csv_writer.h"
 #include "kernels/launch.h"
 
@@ -954,6 +956,31 @@ void rng_bump(const Tensor& ctr) {
   fedtgan::launch_rng_bump(reinterpret_cast<uint64_t*>(ctr.data_ptr<int64_t>()), cur_stream());
 }
 
+// ----------------------------------------------------------------------------- native RCCL plane (csrc/comm)
+void rccl_load_op(const std::string& path) { fedtgan::comm::rccl_load(path); }
+
+Tensor rccl_unique_id_op() {
+  const std::vector<uint8_t> v = fedtgan::comm::rccl_unique_id();
+  Tensor t = at::empty({(int64_t)v.size()}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(t.data_ptr(), v.data(), v.size());
+  return t;
+}
+
+int64_t rccl_init_op(const Tensor& id, int64_t rank, int64_t nranks) {
+  TORCH_CHECK(id.device().is_cpu() && id.scalar_type() == at::kByte && id.numel() == 128 && id.is_contiguous(),
+              "rccl_init: id must be the 128-byte CPU uint8 tensor of rccl_unique_id()");
+  return fedtgan::comm::rccl_init(id.data_ptr<uint8_t>(), (int)rank, (int)nranks);
+}
+
+// in place on the current HIP stream (capturable); premul: this rank's weight, folded into the collective
+void rccl_all_reduce_op(int64_t comm, const Tensor& x, double premul) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(),
+              "rccl_all_reduce: x must be a contiguous fp32 device tensor");
+  fedtgan::comm::rccl_all_reduce_f32(comm, x.data_ptr<float>(), (size_t)x.numel(), (float)premul, cur_stream());
+}
+
+void rccl_destroy_op(int64_t comm) { fedtgan::comm::rccl_destroy(comm); }
+
 void write_csv(const std::string& path, const Tensor& values, std::vector<std::string> names, std::vector<int64_t> kinds,
                std::vector<std::string> vocab_flat, std::vector<int64_t> vocab_offsets, int64_t threads,
                std::vector<int64_t> src, std::vector<int64_t> date_desc, std::vector<int64_t> date_lut,
@@ -1325,6 +1352,11 @@ TORCH_LIBRARY(fedtgan, m) {
       "write_csv(str path, Tensor values, str[] names, int[] kinds, str[] vocab_flat, int[] vocab_offsets, "
       "int threads, int[] src=[], int[] date_desc=[], int[] date_lut=[], Tensor? aux=None) -> ()");
   m.def("py_float(float x) -> str", &py_float);
+  m.def("rccl_load(str path) -> ()", &rccl_load_op);
+  m.def("rccl_unique_id() -> Tensor", &rccl_unique_id_op);
+  m.def("rccl_init(Tensor id, int rank, int nranks) -> int", &rccl_init_op);
+  m.def("rccl_all_reduce(int comm, Tensor(a!) x, float premul) -> ()", &rccl_all_reduce_op);
+  m.def("rccl_destroy(int comm) -> ()", &rccl_destroy_op);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
   m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "

@@ -89,6 +89,10 @@ def main():
     for src in sorted(glob.glob(os.path.join(HERE, "host", "*.cpp"))):
         obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         jobs.append((src, obj, ["g++", "-c", src, "-o", obj, "-pthread"] + common))
+    for src in sorted(glob.glob(os.path.join(HERE, "comm", "*.cpp"))):   # native RCCL plane (host code, HIP headers)
+        obj = os.path.join(build_dir, "comm_" + os.path.basename(src) + ".o")
+        jobs.append((src, obj, [hipcc(), "-c", src, "-o", obj, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1",
+                                "-I" + os.path.join(rocm(), "include")] + common))
     bsrc = os.path.join(HERE, "bindings.cpp")
     bobj = os.path.join(build_dir, "bindings.cpp.o")
     jobs.append((bsrc, bobj, [hipcc(), "-c", bsrc, "-o", bobj, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
@@ -102,7 +106,7 @@ def main():
         # half-written file
         tmp = out + ".tmp"
         run([hipcc(), "-shared", "-o", tmp] + objs + [f"--offload-arch={ARCH}", "-L" + tlib, "-lc10", "-lc10_hip",
-                                                       "-ltorch", "-ltorch_cpu", "-l:libamdhip64.so", "-pthread",
+                                                       "-ltorch", "-ltorch_cpu", "-l:libamdhip64.so", "-ldl", "-pthread",
                                                        "-Wl,-rpath," + tlib])
         os.replace(tmp, out)
     print(f"built {out} ({len(todo)} objects recompiled)")

@@ -32,7 +32,8 @@ import torch.distributed as dist
 class Comm:
     def __init__(self, rank: int = 0, world_size: int = 1, client_ranks: Sequence[int] = (0,),
                  data_backend: str = "gloo", ip: str = "127.0.0.1", port: int = 7788, timeout_s: float = 600.0,
-                 device: torch.device | None = None, init: bool = True, force_dist: bool = False):
+                 device: torch.device | None = None, init: bool = True, force_dist: bool = False,
+                 native_rccl: bool | None = None):
         self.rank = rank
         self.world_size = world_size
         self.client_ranks = list(client_ranks)
@@ -49,6 +50,10 @@ class Comm:
         # RCCL data plane: fold the client weight into the all-reduce (pre-multiplied sum) instead of scaling the
         # buffer first (tools/premul_probe.py checks it against x * w on the box)
         self.premul_sum = True
+        # the weight all-reduce through the native RCCL plane (parallel/rccl.py, csrc/comm) instead of
+        # torch.distributed's ProcessGroup (None: FEDTGAN_NATIVE_RCCL=1 in the environment)
+        self.native_rccl = (os.environ.get("FEDTGAN_NATIVE_RCCL", "0") == "1") if native_rccl is None else native_rccl
+        self._native = None
         # ``force_dist``: build real process groups even for one rank, so the collective branches
         # (RCCL all-reduce / gather / send-recv) execute on a single-GPU box instead of the
         # world-size-1 short-circuits
@@ -78,9 +83,30 @@ class Comm:
                 if f not in self.client_ranks:
                     pg = dist.new_group(ranks=sorted({self.client_ranks[0], f}), backend="gloo", timeout=self.timeout)
                     self.share_pg[f] = pg
+            if self.native_rccl:
+                self._init_native()
         else:
             # gloo data plane: reduce over every rank; a dedicated federator contributes zeros
             self.data = self.ctrl
+
+    def _init_native(self):
+        """The client ranks' native RCCL communicator: the first client's unique id travels over the control
+        plane (every rank takes part in that collective; only client ranks join the communicator)."""
+        from .rccl import NativeRccl
+        first = self.client_ranks[0]
+        ids = [None] * self.world_size
+        uid = None
+        if self.rank == first:
+            from ..ops import native
+            from .rccl import rccl_library_path
+            L = native.require()
+            L.rccl_load(rccl_library_path())
+            uid = L.rccl_unique_id().tolist()
+        dist.all_gather_object(ids, uid, group=self.ctrl)
+        if self.rank in self.client_ranks:
+            shared = torch.tensor(ids[first], dtype=torch.uint8)
+            self._native = NativeRccl(self.client_ranks.index(self.rank), len(self.client_ranks), self.device,
+                                      share_id=lambda _uid: shared)
 
     def _vote_data_backend(self, all_ranks: bool) -> str:
         """Collective (control plane): every rank reaches the SAME data-plane choice.  RCCL when each rank
@@ -226,6 +252,9 @@ class Comm:
                 flat.mul_(weight)
             return flat
         if self.data_backend == "nccl":
+            if self._native is not None:        # client ranks: the native plane, on the current stream
+                self._native.all_reduce(flat, weight)
+                return flat
             if self.is_client:
                 if weight != 1.0 and self.premul_sum and hasattr(dist, "_make_nccl_premul_sum"):
                     # the client weight rides in the collective (RCCL's pre-multiplied sum: each rank's input is
@@ -379,6 +408,11 @@ class Comm:
 
     def destroy(self):
         self.share_wait()
+        if self._native is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)      # (no collective of this communicator in flight)
+            self._native.destroy()
+            self._native = None
         if self.initialized and dist.is_initialized():
             dist.destroy_process_group()
             self.initialized = False
