@@ -1242,6 +1242,12 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_adam_store = (int)value;
     return prev;
   }
+  if (key == "adam_u_min") {   // float4 count (x clients) from which the Adam loop loads ADAM_U float4 per thread
+    TORCH_CHECK(value >= 0, "adam_u_min: >= 0");
+    const int64_t prev = fedtgan::g_adam_u_min;
+    fedtgan::g_adam_u_min = value;
+    return prev;
+  }
   if (key == "adam_max_blocks") {
     TORCH_CHECK(value >= 1 && value <= 65535, "adam_max_blocks: 1..65535");
     const int64_t prev = fedtgan::g_adam_max_blocks;

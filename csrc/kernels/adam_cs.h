@@ -56,7 +56,7 @@ __device__ __forceinline__ void adam_store4(float4* base, __amdgpu_buffer_rsrc_t
 // U: float4 per thread and operand per pass of the Adam loop (1, or ADAM_U for large optimizers: adam_unroll)
 constexpr int ADAM_U = 4;
 // the launchers' choice of U: the unrolled loop for optimizers of >= 4 M elements over the launch's clients
-inline int adam_unroll(int64_t n4, int clients) { return n4 * (clients > 1 ? clients : 1) >= (int64_t)(1 << 20) ? ADAM_U : 1; }
+inline int adam_unroll(int64_t n4, int clients) { return n4 * (clients > 1 ? clients : 1) >= g_adam_u_min ? ADAM_U : 1; }
 
 template <int AUX, int U = 1>
 __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restrict__ p, const float* __restrict__ g,

@@ -300,6 +300,7 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
+extern int64_t g_adam_u_min;   // Adam launches over >= this many float4 (x clients) load ADAM_U float4 per thread
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
 extern int g_gemm_splitk_inlaunch;   // split-K reduced inside the GEMM launch where a tile counter is given (1)
 extern int g_act_row_mode;   // activation kernels on rows wider than 512: one workgroup per row (1) or per 1-4 rows
