@@ -55,7 +55,7 @@ __device__ __forceinline__ void adam_store4(float4* base, __amdgpu_buffer_rsrc_t
 // float4 is shared.  bid / nblk: this workgroup's index and the count among the launch's Adam ones.
 // U: float4 per thread and operand per pass of the Adam loop (1, or ADAM_U for large optimizers: adam_unroll)
 constexpr int ADAM_U = 4;
-// the launchers' choice of U: the unrolled loop for optimizers of >= 4 M elements over the launch's clients
+// the launchers' choice of U: the unrolled loop from g_adam_u_min float4 over the launch's clients (default: always)
 inline int adam_unroll(int64_t n4, int clients) { return n4 * (clients > 1 ? clients : 1) >= g_adam_u_min ? ADAM_U : 1; }
 
 template <int AUX, int U = 1>

@@ -2454,7 +2454,10 @@ void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, cons
 // with these cache bits (2 = nt, 16 = sc1 write-through) so the write-back overlaps the kernel.
 int g_adam_store = 16;
 int g_adam_max_blocks = 65535;
-int64_t g_adam_u_min = (int64_t)1 << 20;   // set_tuning("adam_u_min")
+// set_tuning("adam_u_min").  0: every Adam launch loads ADAM_U float4 per thread.  Measured on the one-client
+// Intrusion step (D 1.67 M, G ~0.5 M parameters; tools/gpu_recipes/r5_adamu.sh, 12 samples each): 196.5 ->
+// 194.8 us with the unrolled loop also below the old 4 M-element threshold
+int64_t g_adam_u_min = 0;
 
 template <int AUX, bool BT_ = false>
 __global__ __launch_bounds__(256) void adam_kernel(float4* __restrict__ p, const float4* __restrict__ g,
