@@ -124,6 +124,9 @@ class FedConfig:
     # on the training stream snapshots what generation reads, the sampler / generator / decode run on a side
     # stream).  None = on where it applies (one process per GPU, HIP bf16 generation with graphs, FedAvg)
     pipeline_sample: Optional[bool] = None
+    # pipelined sampling: issue the table's body / gather / copy / writer hand-off after the next round's training
+    # is queued (their host time then overlaps it).  None = on
+    defer_handoff: Optional[bool] = None
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -718,6 +721,15 @@ class FedRuntime:
         # (pipelined: the rows come from the generation side stream, and the gather / copy are ordered on it, so
         # the round ends without waiting for them -- the next round's training overlaps them)
         pipe = bool(getattr(self, "_pipe", False)) and self.rank in samplers
+        if pipe and async_copy and self.cfg.defer_handoff is not False:
+            # only the prep (snapshot of the model) is issued now; the body, the gather, the copy and the writer
+            # hand-off are issued by _complete_handoff once the next round's training is queued, so their host
+            # time overlaps that training instead of the GPU idling behind it
+            k = per[samplers.index(self.rank)]
+            with self._sub("generate"):
+                self.engine.generation_prep(k)
+            self._handoff = (k, per, samplers, epoch)
+            return None
         gen = (lambda k: self.engine.generate_decoded_split(k, self._gen_stream)) if pipe \
             else self.engine.generate_decoded
         on_gen = (lambda: torch.cuda.stream(self._gen_stream)) if pipe else contextlib.nullcontext
@@ -744,6 +756,26 @@ class FedRuntime:
             self.write_epoch_csv(share, epoch)
         return share if self.is_fed else None
 
+    def _complete_handoff(self):
+        """Issue the deferred part of the last pipelined sample_round: the generation body on the side stream,
+        the gather to the federator, the pinned copy and the CSV writer hand-off."""
+        h = getattr(self, "_handoff", None)
+        if h is None:
+            return
+        self._handoff = None
+        k, per, samplers, epoch = h
+        share = None
+        with torch.cuda.stream(self._gen_stream):
+            vals = self.engine.generation_body(k, self._gen_stream)
+            if len(samplers) == 1:
+                share = self._host(vals)
+            else:
+                rows = self.comm.gather_rows(vals, per, samplers, dst=self.federator, to_host=False)
+                if self.is_fed:
+                    share = self._host(rows) if rows.device.type == "cuda" else rows.numpy()
+        if self.is_fed and self.cfg.write_csv:
+            self.write_epoch_csv(share, epoch)
+
     def _host(self, t: torch.Tensor) -> PendingHost:
         if getattr(self, "_copy_stream", None) is None:
             self._copy_stream = torch.cuda.Stream(t.device)
@@ -764,7 +796,8 @@ class FedRuntime:
         return self._write_epoch_csv(values, epoch)
 
     def flush_writes(self):
-        """Block until every submitted epoch CSV is on disk."""
+        """Block until every submitted epoch CSV is on disk (a deferred pipelined hand-off is issued first)."""
+        self._complete_handoff()
         if self._writer is not None:
             self._writer.flush()
 
@@ -819,6 +852,8 @@ class FedRuntime:
                 hi = time.perf_counter()
                 if self.gradflow is not None:
                     self.gradflow.update(self.engine)
+            # the previous round's deferred table work, now that this round's training is queued
+            self._complete_handoff()
             if self.cfg.train_sync and self.device.type == "cuda":
                 stream_sync(self.device)
         # host-side seconds of the train phase: waiting at the entry barrier, issuing the epoch, until its end

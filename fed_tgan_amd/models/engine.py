@@ -1192,12 +1192,24 @@ class CTGANEngine:
         copies.  The table is bit-identical to generate_decoded(n), and training's random numbers are unchanged
         (the live counter moves exactly as the unsplit pass would move it).  Returns a fresh tensor whose
         producer is ``gen_stream``."""
+        self.generation_prep(n)
+        return self.generation_body(n, gen_stream)
+
+    def generation_prep(self, n: int) -> None:
+        """The prep half of generate_decoded_split(n), on the current stream (see there)."""
         ent = self._gen_split.get(n) or self._capture_gen_split(n)
         cur = torch.cuda.current_stream(self.device)
         if self._gen_done is not None:          # the previous body still reads the snapshot
             cur.wait_event(self._gen_done)
         ent[0].replay()
-        gen_stream.wait_stream(cur)
+        self._gen_prepped = torch.cuda.Event()
+        self._gen_prepped.record(cur)
+
+    def generation_body(self, n: int, gen_stream: "torch.cuda.Stream") -> torch.Tensor:
+        """The body half, on ``gen_stream``: it waits for the prep (an event), not for whatever the current stream
+        queued since -- the body of round r may be issued after round r + 1's training."""
+        ent = self._gen_split[n]
+        gen_stream.wait_event(self._gen_prepped)
         with torch.cuda.stream(gen_stream):
             ent[1].replay()
             out = ent[4].clone()
