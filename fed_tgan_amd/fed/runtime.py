@@ -125,8 +125,10 @@ class FedConfig:
     # stream).  None = on where it applies (one process per GPU, HIP bf16 generation with graphs, FedAvg)
     pipeline_sample: Optional[bool] = None
     # pipelined sampling: issue the table's body / gather / copy / writer hand-off after the next round's training
-    # is queued (their host time then overlaps it).  None = on
-    defer_handoff: Optional[bool] = None
+    # is queued (their host time then overlaps it).  Off: measured no gain on one GPU (16.12-16.22 vs 16.11-16.25 ms)
+    # and +2 ms over an RCCL communicator, where that work queued beside the epoch stretches its kernels as
+    # train_sync=0 does (profiles/sync_r5.txt)
+    defer_handoff: bool = False
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -721,7 +723,7 @@ class FedRuntime:
         # (pipelined: the rows come from the generation side stream, and the gather / copy are ordered on it, so
         # the round ends without waiting for them -- the next round's training overlaps them)
         pipe = bool(getattr(self, "_pipe", False)) and self.rank in samplers
-        if pipe and async_copy and self.cfg.defer_handoff is not False:
+        if pipe and async_copy and self.cfg.defer_handoff:
             # only the prep (snapshot of the model) is issued now; the body, the gather, the copy and the writer
             # hand-off are issued by _complete_handoff once the next round's training is queued, so their host
             # time overlaps that training instead of the GPU idling behind it
