@@ -315,14 +315,15 @@ def test_gpu_round_zero_costs_a_steady_round(tmp_path):
 def test_gpu_pipelined_sampling_matches_unpipelined(tmp_path):
     """FedConfig.pipeline_sample: round r's table generated on a side stream while round r + 1 trains
     (CTGANEngine.generate_decoded_split) writes the same epoch CSVs byte for byte, leaves the same trained model and
-    the same RNG counter as the unsplit generation after the round's training."""
+    the same RNG counter as the unsplit generation after the round's training -- also with the body / copy /
+    writer hand-off deferred past the next round's training issue (FedConfig.defer_handoff)."""
     from fed_tgan_amd.ops import native
     native.require()
     res = []
-    for pipe in (False, True):
-        out = tmp_path / f"p{int(pipe)}"
+    for pipe, defer in ((False, False), (True, False), (True, True)):
+        out = tmp_path / f"p{int(pipe)}{int(defer)}"
         cfg = FedConfig(spec=intrusion_spec(), epochs=3, synthetic_rows=8000, out_dir=str(out), backend="hip",
-                        gmm_backend="torch", verbose=False, pipeline_sample=pipe)
+                        gmm_backend="torch", verbose=False, pipeline_sample=pipe, defer_handoff=defer)
         rt = FedRuntime(cfg, Comm(0, 1, [0], "gloo", device=DEV), DEV)
         rt.initialize()
         assert rt._pipe == pipe
@@ -330,10 +331,11 @@ def test_gpu_pipelined_sampling_matches_unpipelined(tmp_path):
         torch.cuda.synchronize()
         csvs = [(out / f"{rt.name}_result" / f"{rt.name}_synthesis_epoch_{e}.csv").read_bytes() for e in range(3)]
         res.append((csvs, rt.engine.flat.clone(), rt.engine.ops.ctr.clone()))
-    (c0, f0, k0), (c1, f1, k1) = res
-    assert all(a == b for a, b in zip(c0, c1))
-    assert torch.equal(f0, f1)
-    assert torch.equal(k0, k1)
+    c0, f0, k0 = res[0]
+    for c1, f1, k1 in res[1:]:            # pipelined, and pipelined with the hand-off deferred past the next issue
+        assert all(a == b for a, b in zip(c0, c1))
+        assert torch.equal(f0, f1)
+        assert torch.equal(k0, k1)
 
 
 _TWO_RANK_SCRIPT = r"""
