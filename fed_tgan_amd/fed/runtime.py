@@ -129,6 +129,10 @@ class FedConfig:
     # and +2 ms over an RCCL communicator, where that work queued beside the epoch stretches its kernels as
     # train_sync=0 does (profiles/sync_r5.txt)
     defer_handoff: bool = False
+    # HIP stream priority of the pipelined generation stream (torch convention: lower = higher priority; 0 normal).
+    # HIP maps streams onto hardware queues round-robin in creation order, so a normal-priority side stream can
+    # share the training stream's in-order queue (seen in a kernel trace: both on queue 1)
+    gen_stream_priority: int = 0
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -420,7 +424,7 @@ class FedRuntime:
             else self.engine.steps_per_epoch
         self._pipe = self._pipeline_sample()
         if self._pipe:
-            self._gen_stream = torch.cuda.Stream(self.device)
+            self._gen_stream = torch.cuda.Stream(self.device, priority=int(self.cfg.gen_stream_priority))
         self.engine.prepare_graphs(train, gen, gen_split=self._pipe)
         if self.is_fed and cfg.write_csv and cfg.async_csv:
             self._copy_stream = torch.cuda.Stream(self.device)
