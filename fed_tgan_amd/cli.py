@@ -96,6 +96,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("-batched_clients", default="auto", choices=["auto", "on", "off"],
                    help="-local_clients K: the K clients as one batched launch sequence (on) or one engine and HIP "
                         "stream per client thread (off; what auto picks, see FedConfig.batched_clients)")
+    p.add_argument("-native_rccl", action="store_true",
+                   help="the weight all-reduce through the native RCCL plane (csrc/comm) instead of torch.distributed")
+    p.add_argument("-pipeline_sample", default="auto", choices=["auto", "on", "off"],
+                   help="generate round r's table on a side stream after a model snapshot (FedConfig.pipeline_sample)")
+    p.add_argument("-table_reader", default="auto", choices=["auto", "pandas", "arrow"],
+                   help="client CSV reader (pyarrow from 32 MiB up with auto)")
     p.add_argument("-quiet", action="store_true")
     return p
 
@@ -128,7 +134,8 @@ def fed_config_from_args(args):
                      e_interval=args.E_interval, grad_flow=args.grad_flow, profile_dir=args.profile_dir,
                      heartbeat_s=args.heartbeat,
                      dump_real=args.dump_real, async_csv=not args.sync_csv, init=args.init,
-                     batched_clients=args.batched_clients)
+                     batched_clients=args.batched_clients, table_reader=args.table_reader,
+                     pipeline_sample={"auto": None, "on": True, "off": False}[args.pipeline_sample])
 
 
 def pick_device(rank: int, colocated: bool, backend: str, mode: str = "fedavg") -> torch.device:
@@ -207,7 +214,8 @@ def run_rank(rank: int, args, on_done=None) -> None:
         # dedicated federator stays outside the RCCL group and receives the aggregate from the first client
         # (Comm.share_with_federator)
         data_backend = "auto_all" if args.mode == "mdgan" else "auto"
-    comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device)
+    comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device,
+                native_rccl=bool(args.native_rccl))
     if not args.quiet:
         print(f"[rank {rank}] data plane {comm.data_backend} over client ranks {client_ranks}", flush=True)
     try:

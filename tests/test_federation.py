@@ -301,3 +301,13 @@ def test_saved_generator_samples_standalone(tmp_path):
     vocab = {v.column_name: set(v.tolist()) for v in rt.vocabs}
     for c in intrusion_spec().categorical_list:          # decoded categories come from the same vocab
         assert set(df[c].astype(str)) <= vocab[c] | {" "}, c
+
+
+def test_cli_round5_flags_reach_the_config():
+    """-pipeline_sample / -table_reader land in FedConfig; -native_rccl is accepted (it only changes the RCCL plane)."""
+    from fed_tgan_amd.cli import build_parser, fed_config_from_args
+    a = build_parser().parse_args(["-pipeline_sample", "off", "-table_reader", "arrow", "-native_rccl"])
+    cfg = fed_config_from_args(a)
+    assert cfg.pipeline_sample is False and cfg.table_reader == "arrow" and a.native_rccl
+    cfg = fed_config_from_args(build_parser().parse_args([]))
+    assert cfg.pipeline_sample is None and cfg.table_reader == "auto"
