@@ -1147,6 +1147,16 @@ void vgm_fit(const Tensor& x, const Tensor& n_rows, const c10::optional<Tensor>&
   a.out = out.data_ptr<double>();
   a.info = info.data_ptr<int>();
   a.lower_bound = lower_bound.data_ptr<double>();
+  // split fit: a cluster of workgroups per column (the record buffer and the zeroed arrival counters live
+  // until the launch has run: stream-ordered caching-allocator blocks)
+  a.split = fedtgan::vgm_fit_split((int)nc, (int)x.size(1));
+  Tensor xpart, sync;
+  if (a.split > 1) {
+    xpart = at::empty({nc * 2 * a.split * 32}, x.options());
+    sync = at::zeros({nc * 32}, x.options().dtype(at::kInt));
+    a.xpart = xpart.data_ptr<double>();
+    a.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
+  }
   fedtgan::launch_vgm_fit(a, cur_stream());
 }
 
@@ -1247,6 +1257,15 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     const int64_t prev = fedtgan::g_adam_u_min;
     fedtgan::g_adam_u_min = value;
     return prev;
+  }
+  if (key == "vgm_split") {   // workgroups per column of the whole-fit VGM kernel: 0 auto, 1 one, n n
+    TORCH_CHECK(value >= 0 && value <= 64, "vgm_split: 0..64");
+    const int64_t prev = fedtgan::g_vgm_split;
+    fedtgan::g_vgm_split = (int)value;
+    return prev;
+  }
+  if (key == "vgm_split_of") {   // read-only probe: the split a fit of `value` columns x 40000 rows would use
+    return fedtgan::vgm_fit_split((int)value, 40000);
   }
   if (key == "adam_max_blocks") {
     TORCH_CHECK(value >= 1 && value <= 65535, "adam_max_blocks: 1..65535");

@@ -447,9 +447,20 @@ struct VgmFitAllArgs {
   double wprior, tol, reg_covar;
   int max_iter, km_iter;
   double* out;                // [n_cols, 6, 10]: stick a, stick b, beta, means, dof, covariances
-  int* info;                  // [n_cols, 2]: EM iterations, converged
+  int* info;                  // [n_cols, 2]: EM iterations, converged (-1: a cluster barrier timed out)
   double* lower_bound;        // [n_cols]
+  // Split fit (split = G > 1 workgroups per column): every workgroup of a column seeds, runs Lloyd and the
+  // M-steps on the whole column as before, but each E-step pass covers 1/G of the rows and the G partial records
+  // meet through xpart [n_cols, 2, G, 32] (double-buffered by iteration) behind an arrival counter per column
+  // (sync [n_cols * 32], zeroed by the caller).  split <= 1: one workgroup per column.
+  int split;
+  double* xpart;
+  unsigned* sync;
 };
+// workgroups per column for a fit of n_cols columns of <= max_rows rows (set_tuning("vgm_split"): 0 = auto,
+// 1 = one workgroup per column, n = n, capped by what the device holds at once)
+int vgm_fit_split(int n_cols, int max_rows);
+extern int g_vgm_split;
 void launch_vgm_fit(const VgmFitAllArgs& a, hipStream_t stream);
 
 }  // namespace fedtgan

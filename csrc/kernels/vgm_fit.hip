@@ -22,6 +22,8 @@
 //   vgm_fit_kernel      the WHOLE fit of a column in one workgroup (seeding, Lloyd, EM loop with
 //                       device-side M-step / lower bound / convergence): one launch per fit
 #include <algorithm>
+#include <stdexcept>
+#include <string>
 
 #include "common.h"
 #include "launch.h"
@@ -209,6 +211,42 @@ __device__ __forceinline__ void wf_mstep(const double* st, WfState& s, double wp
   __syncthreads();
 }
 
+// Split fit: the E-step statistics of the G workgroups of column j.  Wave 0 publishes this workgroup's record
+// with agent-scope stores, thread 0 arrives on the column's counter (agent release) and spins on relaxed loads
+// until all G records of this pass are in (one acquire after), then wave 0 sums the G records in workgroup
+// order -- the same bits in every workgroup of the column, so all of them take the same M-step and stop at the
+// same iteration.  Records are double-buffered by pass: a workgroup can only overwrite a slot after every
+// workgroup of its column arrived at the next pass, i.e. finished reading this one.  The spin is bounded; a
+// timeout marks the column (info[2j+1] = -1) and stops waiting, so the grid always drains.
+constexpr int VGM_XP = 32;                    // doubles per record (3K + 1 used)
+constexpr unsigned VGM_SPIN_LIMIT = 1u << 22;
+
+template <int NV>
+__device__ __forceinline__ void cluster_sum(const VgmFitAllArgs& a, int j, int g, int G, int pass, double* tot,
+                                            int* dead) {
+  double* rec = a.xpart + ((size_t)(j * 2 + (pass & 1)) * G) * VGM_XP;
+  const int t = threadIdx.x;
+  if (t < NV) __hip_atomic_store(&rec[g * VGM_XP + t], tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    unsigned* cnt = a.sync + (size_t)j * 32;
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (unsigned)(pass + 1) * (unsigned)G;
+    unsigned spins = 0;
+    while (!*dead && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > VGM_SPIN_LIMIT) *dead = 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (t < NV) {
+    double s = 0.0;
+    for (int q = 0; q < G; ++q) s += __hip_atomic_load(&rec[q * VGM_XP + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tot[t] = s;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
   __shared__ double red[WF_WAVES * (3 * FIT_K + 1)];
   __shared__ double tot[3 * FIT_K + 1];
@@ -216,8 +254,14 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
   __shared__ double scan[WF_THREADS];
   __shared__ WfState s;
   __shared__ int flag;
-  const int j = blockIdx.x, t = threadIdx.x;
+  __shared__ int dead;
+  const int G = a.split > 1 ? a.split : 1;
+  const int j = blockIdx.x / G, g = blockIdx.x % G, t = threadIdx.x;
   const int n = a.n_rows[j];
+  // this workgroup's rows of the E-step passes
+  const int e_chunk = (n + G - 1) / G;
+  const int e_lo = min(n, g * e_chunk), e_hi = min(n, e_lo + e_chunk);
+  if (t == 0) dead = 0;
   const double* x = a.x + (size_t)j * a.ldx;
   // ---- prior covariance: var(x, ddof=1) of the centred column
   {
@@ -367,7 +411,7 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
     double v[3 * FIT_K + 1];
 #pragma unroll
     for (int k = 0; k < 3 * FIT_K + 1; ++k) v[k] = 0.0;
-    for (int r = t; r < n; r += WF_THREADS) {
+    for (int r = e_lo + t; r < e_hi; r += WF_THREADS) {
       const double xv = x[r];
       double lp[FIT_K], mx = -INFINITY;
 #pragma unroll
@@ -391,6 +435,7 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
       }
     }
     wf_reduce<3 * FIT_K + 1>(v, red, tot);
+    if (G > 1) cluster_sum<3 * FIT_K + 1>(a, j, g, G, it, tot, &dead);
     const double rlr = tot[3 * FIT_K];
     wf_mstep(tot, s, a.wprior, cov0, a.reg_covar);
     double new_lb = -rlr;
@@ -404,6 +449,7 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
       break;
     }
   }
+  if (g != 0) return;
   if (t < FIT_K) {
     double* o = a.out + (size_t)j * 6 * FIT_K;
     o[t] = s.a[t];
@@ -415,13 +461,38 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
   }
   if (t == 0) {
     a.info[2 * j] = iters;
-    a.info[2 * j + 1] = converged;
+    a.info[2 * j + 1] = dead ? -1 : converged;
     a.lower_bound[j] = lb;
   }
 }
 
+int g_vgm_split = 0;
+
+int vgm_fit_split(int n_cols, int max_rows) {
+  if (n_cols <= 0 || g_vgm_split == 1) return 1;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, vgm_fit_kernel, WF_THREADS, 0) != hipSuccess)
+    return 1;
+  const int cap = cus * std::max(per_cu, 1) / n_cols;     // workgroups per column the device holds at once
+  // auto: fill the CUs one workgroup each, >= 4 rows per thread, <= 16 per column
+  int G = g_vgm_split > 1 ? g_vgm_split : std::min(std::min(16, cus / n_cols), max_rows / (4 * WF_THREADS));
+  return std::max(1, std::min(G, cap));
+}
+
 void launch_vgm_fit(const VgmFitAllArgs& a, hipStream_t stream) {
   if (a.n_cols == 0) return;
+  if (a.split > 1) {
+    // the workgroups of a column wait for each other: a cooperative launch guarantees they are co-resident
+    // (or fails instead of deadlocking)
+    if (!a.xpart || !a.sync) throw std::runtime_error("vgm_fit: split fit without its record / counter buffers");
+    VgmFitAllArgs arg = a;
+    void* args[] = {&arg};
+    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(vgm_fit_kernel),
+                                                    dim3(a.n_cols * a.split), dim3(WF_THREADS), args, 0, stream);
+    if (e != hipSuccess) throw std::runtime_error(std::string("vgm_fit: cooperative launch: ") + hipGetErrorString(e));
+    return;
+  }
   hipLaunchKernelGGL(vgm_fit_kernel, dim3(a.n_cols), dim3(WF_THREADS), 0, stream, a);
 }
 

@@ -121,3 +121,26 @@ def test_own_init_statistically_equivalent_fused_kernel(columns):
     _own_init_checks(fit_vgm_torch(columns, seed=3, device="cuda:0"), columns)
     info = fit_vgm_torch.last_info
     assert (info[:, 0] >= 1).all() and (info[:, 0] <= 100).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [4, 11])
+def test_split_fit_matches_sklearn_and_is_deterministic(columns, sk, split):
+    """set_tuning("vgm_split"): a cluster of workgroups per column (E-step rows split, the partial records summed in
+    workgroup order behind a per-column arrival counter) still reproduces sklearn from the same initialisation,
+    every barrier completes, and two fits give the same bits."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    prev = torch.ops.fedtgan.set_tuning("vgm_split", split)
+    try:
+        assert torch.ops.fedtgan.set_tuning("vgm_split_of", len(columns)) == split
+        ic = np.stack([c for _, c in sk])
+        a = fit_vgm_torch(columns, seed=0, device="cuda:0", init_centers=ic)
+        info = fit_vgm_torch.last_info.copy()
+        b = fit_vgm_torch(columns, seed=0, device="cuda:0", init_centers=ic)
+    finally:
+        torch.ops.fedtgan.set_tuning("vgm_split", prev)
+    assert (info[:, 1] >= 0).all(), info          # -1: a cluster barrier timed out
+    for f in ("means", "covariances", "weights"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
+    _check_same_init(a, sk, f"hip split {split}")
