@@ -107,14 +107,26 @@ struct BnlPending {
 };
 thread_local BnlPending g_bnl{};
 
+// Published BatchNorm statistics for the NEXT gemm() with bn_part of this thread (gemm_bnpub_next, launch.h
+// GemmArgs::bnf_*): the producing GEMM's last workgroup per column tile writes mean / invstd and the running stats
+struct BnPubPending {
+  float *mean, *invstd, *rm, *rv;
+  unsigned* cnt;
+  int64_t width, cnt_numel;
+  float mom, eps;
+  bool active;
+};
+thread_local BnPubPending g_bnpub{};
+
 // drop every GEMM held by this thread (pairing, chain tail, Adam fusion) without launching it: called at
 // the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
 // (whose operand pointers may since have been freed) can never be launched or block the next step.
 // Returns the number of holds that were dropped.
 int64_t reset_held() {
   const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0) +
-                    (g_bnl.active ? 1 : 0);
+                    (g_bnl.active ? 1 : 0) + (g_bnpub.active ? 1 : 0);
   g_bnl.active = false;
+  g_bnpub.active = false;
   has_held = false;
   held_stream = nullptr;
   g_adam_held.active = false;
@@ -144,6 +156,21 @@ int64_t set_client_batch(int64_t k, int64_t stride, int64_t seed_step, int64_t b
 // launch.h GemmArgs::bnl): part[j] = the producing GEMM's partials (None: mean / invstd are final), ptm[j] its
 // rows per tile; mean / invstd [2, width] (written by the consumer from partials); out (nullable): materialise
 // relu(BN(a)) (raw outside the ranges) as [M, K] rows, with nhat[j] [M, width_j] alongside.
+// The next gemm() with bn_part publishes its BatchNorm statistics (GemmArgs::bnf_*): mean / invstd [2, N], the
+// running statistics [N] (advanced batch after batch) and cnt (int32, one zeroed counter per column tile).
+void gemm_bnpub_next(const Tensor& cnt, const Tensor& mean, const Tensor& invstd, const Tensor& rm, const Tensor& rv,
+                     double momentum, double eps) {
+  TORCH_CHECK(!g_bnpub.active, "gemm_bnpub_next: already pending");
+  const int64_t w = rm.numel();
+  for (const Tensor* t : {&mean, &invstd, &rm, &rv})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "gemm_bnpub_next: fp32 contiguous");
+  TORCH_CHECK(mean.numel() >= 2 * w && invstd.numel() >= 2 * w && rv.numel() == w, "gemm_bnpub_next: mean / invstd [2, N]");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous(), "gemm_bnpub_next: cnt int32");
+  g_bnpub = BnPubPending{mean.data_ptr<float>(), invstd.data_ptr<float>(), rm.data_ptr<float>(), rv.data_ptr<float>(),
+                         reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), w, cnt.numel(), (float)momentum, (float)eps,
+                         true};
+}
+
 void gemm_bnl_next(const std::vector<optional<Tensor>>& part, const std::vector<Tensor>& mean,
                    const std::vector<Tensor>& invstd, const std::vector<Tensor>& gamma, const std::vector<Tensor>& beta,
                    const std::vector<Tensor>& rm, const std::vector<Tensor>& rv, const std::vector<optional<Tensor>>& nhat,
@@ -333,7 +360,21 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     TORCH_CHECK(bn_rpg >= 1 && bn_rpg <= M, "gemm: bn_rpg");
     g.bn_part = fp(*bn_part);
     g.bn_rpg = (int)bn_rpg;
+    if (g_bnpub.active) {
+      BnPubPending& q = g_bnpub;
+      q.active = false;
+      TORCH_CHECK(q.width == N && q.cnt_numel >= (N + tile - 1) / tile && fedtgan::client_batch().k == 1,
+                  "gemm: published BatchNorm statistics need [2, N] mean / invstd, one counter per column tile, one client");
+      g.bnf_mean = q.mean;
+      g.bnf_invstd = q.invstd;
+      g.bnf_rm = q.rm;
+      g.bnf_rv = q.rv;
+      g.bnf_cnt = q.cnt;
+      g.bnf_mom = q.mom;
+      g.bnf_eps = q.eps;
+    }
   }
+  TORCH_CHECK(!g_bnpub.active, "gemm: gemm_bnpub_next is pending but this GEMM writes no BatchNorm partials");
   if (g_bnl.active) {
     BnlPending& p = g_bnl;
     p.active = false;      // consumed by this call whatever happens below
@@ -1384,6 +1425,8 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy_op);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
+  m.def("gemm_bnpub_next(Tensor cnt, Tensor mean, Tensor invstd, Tensor rm, Tensor rv, float momentum, float eps) -> ()",
+        &gemm_bnpub_next);
   m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "
         "Tensor[] rv, Tensor?[] nhat, int[] k0, int[] ptm, int rpg, float momentum, float eps, Tensor? out) -> ()",
         &gemm_bnl_next);

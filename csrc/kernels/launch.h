@@ -85,6 +85,16 @@ struct GemmArgs {
   // and sum of squared deviations: bn_part[((m_tile * 2 + batch) * 3 + {0,1,2}) * N + n]
   float* bn_part;
   int bn_rpg;
+  // Published statistics (nullable; with bn_part): the last workgroup of each column tile to write its partials
+  // (arrival counter bnf_cnt[column tile], zero between launches, re-zeroed by that workgroup) merges the column
+  // block's partials in tile order, writes mean / invstd [2][N] and advances the running statistics batch after
+  // batch -- the consumers then load final statistics instead of merging every tile's partials.
+  float* bnf_mean;
+  float* bnf_invstd;
+  float* bnf_rm;
+  float* bnf_rv;
+  unsigned* bnf_cnt;
+  float bnf_mom, bnf_eps;
   int oh_c;       // width of the one-hot block (checked build: gather index bound)
   // BatchNorm(train) + ReLU of earlier generator layers applied to op(A) while it is staged (gemm_tile EK 5 / 6;
   // nbnl = 0: none).  op(A) = A row-major, unsplit, C = A op(B) + bias.  Range j covers A's columns

@@ -148,6 +148,12 @@ class EngineConfig:
     # workgroup re-merges all producer tiles' partials (+6-13 us per consumer GEMM) against 2 x 7.7 us of BN
     # launches removed.
     bn_fold: bool = False
+    # With bn_fold: each layer GEMM's last workgroup per column tile merges the partials once and publishes
+    # mean / invstd and the running statistics (GemmArgs::bnf_*), so the consumers' prologues load final
+    # statistics instead of re-merging every producer tile's partials (backends with bn_publish_capable).
+    # Off: the folded step measured 214 us with it against 205 us without (no fold: 194 us) -- the producer's
+    # serialised last-arrival merge costs more than the consumers' merges (profiles/bn_fold_r5.txt).
+    bn_fold_publish: bool = False
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -453,6 +459,8 @@ class CTGANEngine:
             self.H2 = big[:, c0:c0 + self.Hw]
             self._Hbig = big
             self._bn_part = [z(-(-2 * B // 32) * 6 * g) for g in self.gdims]   # 32-row tiles at most
+            # arrival counters of the statistics-publishing GEMMs (one per column tile, re-zeroed by the kernel)
+            self._bn_cnt = torch.zeros(len(self.gdims), 64, dtype=torch.int32, device=self.device)
         else:
             self.H2 = _padded_rows(2 * B, self.Hw, dev)
         self.abuf2 = [z(2 * B, g) for g in self.gdims]
@@ -650,9 +658,11 @@ class CTGANEngine:
         rpg, mom, eps = self.B, self.cfg.bn_momentum, self.cfg.bn_eps
         ptm = []
 
+        pub = bool(self.cfg.bn_fold_publish) and getattr(o, "bn_publish_capable", False)
+
         def bn_args(j, from_part):
-            return (self._bn_part[j] if from_part else None, self.bn_mean2[j], self.bn_invstd2[j], p[f"G.{j}.gamma"],
-                    p[f"G.{j}.beta"], p[f"G.{j}.rm"], p[f"G.{j}.rv"])
+            return (self._bn_part[j] if from_part and not pub else None, self.bn_mean2[j], self.bn_invstd2[j],
+                    p[f"G.{j}.gamma"], p[f"G.{j}.beta"], p[f"G.{j}.rm"], p[f"G.{j}.rv"])
 
         for i in range(L):
             a, b_ = self.off[i], self.off[i + 1]
@@ -662,6 +672,9 @@ class CTGANEngine:
             if i > 0:       # layer i-1's BatchNorm, applied while this GEMM stages its output (its first consumer)
                 part, mean, istd, gm, bt, rm, rv = bn_args(i - 1, True)
                 o.gemm_bnl_next([part], [mean], [istd], [gm], [bt], [rm], [rv], [None], [0], [ptm[i - 1]], rpg, mom, eps)
+            if pub:         # this GEMM's last workgroup per column tile publishes the layer's statistics
+                o.gemm_bnpub_next(self._bn_cnt[i], self.bn_mean2[i], self.bn_invstd2[i], p[f"G.{i}.rm"],
+                                  p[f"G.{i}.rv"], mom, eps)
             o.gemm(x, W, Hp[:, b_:a], tb=True, bias=p[f"G.{i}.b"], onehot=oh, bn_part=self._bn_part[i], bn_rpg=rpg,
                    tile=tile, splitk=1)
             ptm.append(tile)

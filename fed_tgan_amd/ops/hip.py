@@ -111,6 +111,7 @@ def _effective_splits(K: int, sk: int, kc: int) -> int:
 class HipOps:
     name = "hip"
     bn_fold_capable = True       # EngineConfig.bn_fold (gemm_bnl_next + BN partials)
+    bn_publish_capable = True    # EngineConfig.bn_fold_publish (gemm_bnpub_next)
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
     gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
 
@@ -322,6 +323,11 @@ class HipOps:
         kc = 64 if self.f32 else 128
         tile, sk = _plan(M, N, K, kc, self._plan_clients())
         return self.tile_override or tile, _effective_splits(K, self.split_override or sk, kc)
+
+    def gemm_bnpub_next(self, cnt, mean, invstd, rm, rv, momentum, eps):
+        """The next gemm() with bn_part also publishes the final BatchNorm statistics from its last workgroup per
+        column tile (csrc/kernels/launch.h GemmArgs::bnf_*, EngineConfig.bn_fold_publish)."""
+        self.L.gemm_bnpub_next(cnt, mean, invstd, rm, rv, float(momentum), float(eps))
 
     def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
         """The next gemm() stages relu(BatchNorm(a)) for the given column ranges of its A operand (see

@@ -492,19 +492,23 @@ def test_chain_tail_prefetch_matches_plain(batch):
         assert torch.equal(f, f0), float((f - f0).abs().max())
 
 
+@pytest.mark.parametrize("publish", [True, False])
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_bn_fold_matches_bn_launches(precision):
+def test_bn_fold_matches_bn_launches(precision, publish):
     """EngineConfig.bn_fold: the generator's BatchNorm folded into its GEMMs (partials from the producing GEMM,
     relu(BN(a)) staged by the consumers, materialised by the output GEMM) gives the forward of the GEMM +
     bn_relu_train launches -- activations, nhat, batch and running statistics, logits -- up to the statistics'
-    summation order (and bf16 rounding of the staged operands), and trains the same."""
+    summation order (and bf16 rounding of the staged operands), and trains the same.  publish: the producing
+    GEMM's last workgroup per column tile merges the partials and publishes the statistics
+    (EngineConfig.bn_fold_publish); otherwise every consumer workgroup merges them."""
     from fed_tgan_amd.ops import native
     native.require()
     _, _, _, _, _, _, tr, X = small_table()
     engs = []
     for fold in (False, True):
         torch.manual_seed(0)
-        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, bn_fold=fold), DEV,
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, bn_fold=fold,
+                                                  bn_fold_publish=publish), DEV,
                           backend="hip", seed=21)
         eng.set_training_data(X)
         engs.append(eng)

@@ -63,7 +63,7 @@ def onehot_ab(eng, tr, X, dev):
                   f"generate_decoded(40000) {t_gen:8.1f} us", flush=True)
 
 
-def gwt_ab(tr, X, dev, precision, key="g_wt"):
+def gwt_ab(tr, X, dev, precision, key="g_wt", base=None):
     """A/B of a boolean EngineConfig field (default g_wt: generator weights stored [out, in] vs
     input-major); full captured step and generate_decoded(40000), two engines from the same initial
     weights, alternating."""
@@ -71,7 +71,9 @@ def gwt_ab(tr, X, dev, precision, key="g_wt"):
     from fed_tgan_amd.models.samplers import CondTables
     engs = {}
     for g_wt in (False, True):
-        e = CTGANEngine(tr.layout, EngineConfig(precision=precision, **{key: g_wt}), dev, backend="hip", seed=1)
+        import dataclasses
+        cfg = dataclasses.replace(base, **{key: g_wt}) if base is not None else EngineConfig(precision=precision, **{key: g_wt})
+        e = CTGANEngine(tr.layout, cfg, dev, backend="hip", seed=1)
         e.set_training_data(X)
         e.set_generation_tables(CondTables.from_encoded(X, tr.layout), tr)
         engs[g_wt] = e
@@ -311,7 +313,7 @@ def main():
     if args.gwt_ab:
         return gwt_ab(tr, X, dev, args.precision)
     if args.cfg_ab:
-        return gwt_ab(tr, X, dev, args.precision, key=args.cfg_ab)
+        return gwt_ab(tr, X, dev, args.precision, key=args.cfg_ab, base=cfg)
     if args.gen:
         return gen_only(eng, tr, X, dev)
     if args.onehot_ab:
