@@ -217,7 +217,10 @@ __device__ __forceinline__ void wf_mstep(const double* st, WfState& s, double wp
 // order -- the same bits in every workgroup of the column, so all of them take the same M-step and stop at the
 // same iteration.  Records are double-buffered by pass: a workgroup can only overwrite a slot after every
 // workgroup of its column arrived at the next pass, i.e. finished reading this one.  The spin is bounded; a
-// timeout marks the column (info[2j+1] = -1) and stops waiting, so the grid always drains.
+// timeout stops waiting (so the grid always drains) and poisons the whole column: the timed-out workgroup
+// stores the column's dead flag (sync[32j + 1]) BEFORE its next arrival, so every workgroup whose barrier
+// count includes such an arrival sees the flag after its acquire, and workgroup 0 reports the column
+// (info[2j+1] = -1) even when it was another workgroup that timed out.
 constexpr int VGM_XP = 32;                    // doubles per record (3K + 1 used)
 constexpr unsigned VGM_SPIN_LIMIT = 1u << 22;
 
@@ -229,14 +232,20 @@ __device__ __forceinline__ void cluster_sum(const VgmFitAllArgs& a, int j, int g
   if (t < NV) __hip_atomic_store(&rec[g * VGM_XP + t], tot[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (t == 0) {
     unsigned* cnt = a.sync + (size_t)j * 32;
+    unsigned* col_dead = cnt + 1;
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned target = (unsigned)(pass + 1) * (unsigned)G;
     unsigned spins = 0;
     while (!*dead && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > VGM_SPIN_LIMIT) *dead = 1;
+      if (__hip_atomic_load(col_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) *dead = 1;
+      if (++spins > VGM_SPIN_LIMIT) {
+        *dead = 1;
+        __hip_atomic_store(col_dead, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (__hip_atomic_load(col_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) *dead = 1;
   }
   __syncthreads();
   if (t < NV) {
@@ -462,6 +471,7 @@ __global__ __launch_bounds__(WF_THREADS) void vgm_fit_kernel(VgmFitAllArgs a) {
     o[5 * FIT_K + t] = s.cov[t];
   }
   if (t == 0) {
+    if (G > 1 && __hip_atomic_load(a.sync + (size_t)j * 32 + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) dead = 1;
     a.info[2 * j] = iters;
     a.info[2 * j + 1] = dead ? -1 : converged;
     a.lower_bound[j] = lb;

@@ -31,6 +31,7 @@ Data are centred per column first (prior mean 0), and the means shifted back at 
 from __future__ import annotations
 
 import math
+import threading
 
 import numpy as np
 import torch
@@ -40,6 +41,7 @@ from .gmm import VGMBank, WEIGHT_PRIOR
 REG_COVAR = 1e-6
 TOL = 1e-3
 MAX_ITER = 100
+_FIT_LOCK = threading.Lock()
 
 
 def _pad(columns, device, dtype):
@@ -201,10 +203,35 @@ def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: fl
     if init_centers is not None:
         ic = (torch.as_tensor(np.asarray(init_centers, dtype=np.float64), device=dev)
               - shift.unsqueeze(1)).contiguous()
-    L.vgm_fit(X.contiguous(), n, ic, int(seed) & ((1 << 62) - 1), WEIGHT_PRIOR, float(tol), REG_COVAR, int(max_iter),
-              300, out, info, lbs)
+    args = (int(seed) & ((1 << 62) - 1), WEIGHT_PRIOR, float(tol), REG_COVAR, int(max_iter), 300)
+    # the split fit is a cooperative launch sized to about one workgroup per CU: fits of concurrent client
+    # threads (fed/local.py) are serialised process-wide, and each waits for its grid to drain (the info
+    # read) before the next may launch
+    with _FIT_LOCK:
+        L.vgm_fit(X.contiguous(), n, ic, *args, out, info, lbs)
+        info_h = info.cpu().numpy()
+        dead = np.nonzero(info_h[:, 1] == -1)[0]
+        if len(dead):
+            # a cluster barrier timed out (its workgroups were not co-resident): those columns' results are
+            # not trusted -- refit them with one workgroup per column (no inter-workgroup barrier at all)
+            sel = torch.as_tensor(dead, device=dev)
+            prev = L.set_tuning("vgm_split", 1)
+            try:
+                o2 = torch.empty(len(dead), 6, 10, dtype=torch.float64, device=dev)
+                i2 = torch.empty(len(dead), 2, dtype=torch.int32, device=dev)
+                l2 = torch.empty(len(dead), dtype=torch.float64, device=dev)
+                L.vgm_fit(X.index_select(0, sel).contiguous(), n.index_select(0, sel).contiguous(),
+                          None if ic is None else ic.index_select(0, sel).contiguous(), *args, o2, i2, l2)
+            finally:
+                L.set_tuning("vgm_split", prev)
+            out.index_copy_(0, sel, o2)
+            lbs.index_copy_(0, sel, l2)
+            info_h[dead] = i2.cpu().numpy()
+            if (info_h[dead, 1] == -1).any():
+                raise RuntimeError(f"vgm_fit: columns {dead.tolist()} failed even unsplit")
     o = out.cpu().numpy()
-    fit_vgm_torch.last_info = info.cpu().numpy()
+    fit_vgm_torch.last_info = info_h
+    fit_vgm_torch.last_refit_columns = dead
     fit_vgm_torch.last_lower_bound = lbs.cpu().numpy()
     return VGMBank(wc_a=o[:, 0], wc_b=o[:, 1], mean_precision=o[:, 2], means=o[:, 3] + shift.cpu().numpy()[:, None],
                    dof=o[:, 4], covariances=o[:, 5])

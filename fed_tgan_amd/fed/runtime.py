@@ -685,6 +685,11 @@ class FedRuntime:
         c = self.comm
         wts = self.weights if alive is None else effective_weights(self.weights, alive)
         w = float(wts[c.client_index]) if self.is_client else 0.0
+        if getattr(self, "_pipe", False) and getattr(c, "_native", None) is not None:
+            # the previous round's pipelined gather runs on torch's RCCL communicator on the generation stream,
+            # this all-reduce on the native one: two communicators with collectives in flight at once and no
+            # cross-rank order between them can deadlock, so every rank orders the all-reduce after its gather
+            torch.cuda.current_stream(self.device).wait_stream(self._gen_stream)
         with self._sub("allreduce"):
             c.weighted_all_reduce(self.engine.flat, w)
         with self._sub("share"):

@@ -284,7 +284,8 @@ class Comm:
         once (only the copy, ~0.2 ms for 8.5 MB, is ordered before the next round's kernels); the
         federator receives it and copies it to its device.  ``extra`` (a small device tensor every client
         holds, e.g. the client-averaged losses) rides along in the same message and lands in the
-        federator's ``extra``.  Returns True where the hand-off happened (both ends)."""
+        federator's ``extra``.  Returns True on EVERY rank when the hand-off took place this round (the
+        decision depends only on state all ranks share), so callers that branch on it stay collective."""
         if not self.dist_active or self.data_backend != "nccl" or federator in self.client_ranks:
             return False
         src = self.client_ranks[0]
@@ -302,8 +303,8 @@ class Comm:
                 off += n
             if flat.is_cuda:            # the pinned buffer is received into again next round
                 torch.cuda.current_stream(flat.device).synchronize()
-        else:
-            return False
+        # the other clients take no part in the transfer, but the hand-off happened for them too: every
+        # client already holds ``extra`` (client_mean), so nothing else needs a control collective
         return True
 
     def _share_buffer(self, parts):

@@ -31,18 +31,21 @@ def rccl_library_path() -> str:
 class NativeRccl:
     """One RCCL communicator over ``nranks`` ranks of this process group.
 
-    share_id: called on every rank with rank 0's unique id (None elsewhere) and returns rank 0's id -- the
-    control plane's broadcast (the ids must reach every member before any member initialises)."""
+    share_id: called on every rank (with None) and returns rank 0's unique id, which the caller generated and
+    distributed over the control plane (the ids must reach every member before any member initialises)."""
 
     def __init__(self, rank: int, nranks: int, device: torch.device,
                  share_id: Optional[Callable[[Optional[torch.Tensor]], torch.Tensor]] = None):
         L = _lib()
         L.rccl_load(rccl_library_path())
-        uid = L.rccl_unique_id() if rank == 0 else None
+        # (each ncclGetUniqueId starts a bootstrap root -- a listening socket and a thread -- so an id is only
+        # generated here when no caller shares one: a one-rank communicator without a control plane)
         if share_id is not None:
-            uid = share_id(uid)
+            uid = share_id(None)
         elif nranks != 1:
             raise ValueError("NativeRccl over several ranks needs share_id (the control plane's broadcast)")
+        else:
+            uid = L.rccl_unique_id()
         torch.cuda.set_device(device)
         self.rank, self.nranks, self.device = rank, nranks, device
         self.handle = int(L.rccl_init(uid.contiguous(), int(rank), int(nranks)))

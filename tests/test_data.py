@@ -178,3 +178,31 @@ def test_arrow_reader_matches_pandas(tmp_path, name):
     _, vocabs, _ = merge_categorical_metas(metas)
     a, b = (tp.encode(vocabs) for tp in tps)
     np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_auto_reader_is_pandas_bitwise(tmp_path):
+    """reader="auto" must give pd.read_csv's bits whatever the file size: arrow's correctly rounded
+    float parser and pandas' default parser disagree in the last ulp of many random doubles, which would move
+    VGM fits and encodings away from the reference's load path (`Server/dtds/data/load.py:51-70`)."""
+    pytest.importorskip("pyarrow")
+    from fed_tgan_amd.data import table
+    rng = np.random.default_rng(0)
+    n = 20000
+    df = pd.DataFrame({"f": rng.standard_normal(n) * 1e3, "g": np.exp(rng.standard_normal(n) * 5),
+                       "i": rng.integers(0, 1000, n).astype(float), "c": rng.choice(["a", "bb", " d"], n)})
+    df.loc[rng.random(n) < 0.05, "i"] = np.nan
+    path = tmp_path / "t.csv"
+    df.to_csv(path, index=False)
+    ref = pd.read_csv(path)
+    old = table.ARROW_MIN_BYTES
+    table.ARROW_MIN_BYTES = 1            # even a "large" file
+    try:
+        got = table.read_csv_table(str(path), "auto")
+    finally:
+        table.ARROW_MIN_BYTES = old
+    assert list(got.dtypes) == list(ref.dtypes)
+    for c in ("f", "g", "i"):
+        assert np.array_equal(got[c].to_numpy().view(np.int64), ref[c].to_numpy().view(np.int64)), c
+    arrow = table.read_csv_table(str(path), "arrow")
+    # (the opt-in arrow reader really does differ in the last bits: why auto must not pick it)
+    assert not np.array_equal(arrow["g"].to_numpy(dtype=np.float64), ref["g"].to_numpy())
