@@ -467,7 +467,7 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
             const optional<Tensor>& row_cnt, const optional<Tensor>& rows, const optional<Tensor>& data,
             const optional<Tensor>& col, const optional<Tensor>& opt, const optional<Tensor>& step_bump,
             const optional<Tensor>& step_bump2, const optional<Tensor>& metrics, bool zero_metrics, int64_t seed,
-            const Tensor& rng_ctr, int64_t stream) {
+            const Tensor& rng_ctr, int64_t stream, int64_t draws, int64_t draw_h, int64_t draw_x, int64_t draw_col) {
   fedtgan::SampleArgs a{};
   const bool h16 = h.scalar_type() == at::kBFloat16;
   a.B = (int)h.size(0);
@@ -528,6 +528,31 @@ void sample(const Tensor& h, int64_t zc, int64_t cc, int64_t E, const optional<T
   a.seed = (uint64_t)seed;
   a.rng_ctr = ctr_ptr(rng_ctr);
   a.rng_stream = (uint32_t)stream;
+  a.draws = (int)std::max<int64_t>(draws, 1);
+  if (a.draws > 1) {
+    // every draw's buffers must lie inside their tensors' storage: draw k writes at the same views + k x stride
+    TORCH_CHECK(!h16 && draw_h > 0 && draw_col > 0 && (draw_x > 0 || !(xf.has_value() && xf->defined())),
+                "sample: multi-step draws need fp32 h and positive strides");
+    auto fits = [&](const Tensor& t, int64_t stride, const char* what) {
+      const int64_t span = (t.size(0) - 1) * t.stride(0) + (t.dim() > 1 ? t.size(1) : 1);
+      const int64_t last = t.storage_offset() + (a.draws - 1) * stride + span;
+      TORCH_CHECK(last * (int64_t)t.element_size() <= (int64_t)t.storage().nbytes(), "sample: draw ", a.draws - 1,
+                  " of ", what, " runs past its storage");
+    };
+    fits(h, draw_h, "h");
+    if (xf.has_value() && xf->defined()) fits(*xf, draw_x, "xf");
+    if (xr.has_value() && xr->defined()) fits(*xr, draw_x, "xr");
+    for (const auto* t : {&col, &opt})
+      if (t->has_value() && (*t)->defined()) fits(**t, draw_col, "col / opt");
+    for (const auto* t : {&step_bump, &step_bump2})
+      if (t->has_value() && (*t)->defined())
+        TORCH_CHECK((*t)->numel() >= a.draws && (*t)->is_contiguous(), "sample: per-step counters need [draws]");
+    if (metrics.has_value() && metrics->defined())
+      TORCH_CHECK(metrics->numel() >= 4 * a.draws && metrics->is_contiguous(), "sample: metrics need [draws, 4]");
+    a.draw_h = draw_h;
+    a.draw_x = draw_x;
+    a.draw_col = draw_col;
+  }
   fedtgan::launch_sample(a, cur_stream());
 }
 
@@ -1359,7 +1384,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "sample(Tensor(a!) h, int zc, int cc, int E, Tensor(b!)? xf, Tensor(c!)? xr, int Dd, Tensor cdf, Tensor cond_off, "
       "Tensor cond_w, Tensor? row_off, Tensor? row_cnt, Tensor? rows, Tensor? data, Tensor(d!)? col, Tensor(e!)? opt, "
       "Tensor(f!)? step_bump, Tensor(h!)? step_bump2, Tensor(g!)? metrics, bool zero_metrics, int seed, Tensor rng_ctr, "
-      "int stream) -> ()");
+      "int stream, int draws=1, int draw_h=0, int draw_x=0, int draw_col=0) -> ()");
   m.def(
       "activate(Tensor logits, Tensor(a!) out, Tensor start, Tensor width, Tensor kind, Tensor cidx, Tensor elem, "
       "float tau, int seed, Tensor rng_ctr, int stream, Tensor? slerp_real, Tensor(b!)? slerp_out, int slerp_cols, "

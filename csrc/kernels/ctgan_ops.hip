@@ -149,7 +149,7 @@ __device__ __forceinline__ void onehot_row(float* __restrict__ p, int C, int hot
   for (int i = head + 4 * n4 + lane; i < C; i += 64) p[i] = i == hot ? 1.f : 0.f;
 }
 
-template <bool BT_ = false>
+template <bool BT_ = false, bool MULTI = false>
 __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
   const BIdx bi_ = batch_bidx<BT_>(a.cb.xcd);
   if (bi_.z) {   // batched clients: this client's buffers and seed
@@ -173,9 +173,32 @@ __global__ __launch_bounds__(SAMPLE_THREADS) void sample_kernel(SampleArgs a) {
     a.rng_ctr = cptr(a.rng_ctr, o);
     a.seed += (uint64_t)bi_.z * a.cb.seed_step;
   }
-  const uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
+  uint64_t step = a.rng_ctr ? *a.rng_ctr : 0ull;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (bi_.x == 0 && tid == 0) {
+  if constexpr (MULTI) {
+    // draw k of a multi-step launch: step k's RNG key and buffers; ONE thread writes every step's counters
+    // (reading the canonical last entry before overwriting it) and zeroes every step's metrics
+    const int k = (int)blockIdx.y;
+    step += (uint64_t)k;
+    a.h += (size_t)k * a.draw_h;
+    if (a.xf) a.xf += (size_t)k * a.draw_x;
+    if (a.xr) a.xr += (size_t)k * a.draw_x;
+    if (a.col) a.col += (size_t)k * a.draw_col;
+    if (a.opt) a.opt += (size_t)k * a.draw_col;
+    if (bi_.x == 0 && k == 0 && tid == 0) {
+      const int D = a.draws;
+      if (a.step_bump) {
+        const float b = a.step_bump[D - 1];
+        for (int q = 0; q < D; ++q) a.step_bump[q] = b + (float)(q + 1);
+      }
+      if (a.step_bump2) {
+        const float b = a.step_bump2[D - 1];
+        for (int q = 0; q < D; ++q) a.step_bump2[q] = b + (float)(q + 1);
+      }
+      if (a.zero_metrics && a.metrics)
+        for (int q = 0; q < 4 * D; ++q) a.metrics[q] = 0.f;
+    }
+  } else if (bi_.x == 0 && tid == 0) {
     if (a.step_bump) a.step_bump[0] += 1.0f;
     if (a.step_bump2) a.step_bump2[0] += 1.0f;
     if (a.zero_metrics && a.metrics) {
@@ -300,6 +323,11 @@ void launch_sample(const SampleArgs& a0, hipStream_t stream) {
       check_slab(p, "sample operand");
   }
   const int blocks = (a.B + SAMPLE_ROWS - 1) / SAMPLE_ROWS;
+  if (a.draws > 1) {
+    if (a.cb.k > 1 || a.h16) throw std::runtime_error("sample: multi-step draws are for one client's fp32 training batches");
+    hipLaunchKernelGGL((sample_kernel<false, true>), dim3(blocks, a.draws, 1), dim3(SAMPLE_THREADS), 0, stream, a);
+    return;
+  }
   hipLaunchKernelGGL((client_batch().xcd ? sample_kernel<true> : sample_kernel<false>), dim3(blocks, 1, a.cb.k), dim3(SAMPLE_THREADS), 0, stream, a);
 }
 

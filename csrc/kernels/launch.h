@@ -194,6 +194,12 @@ struct SampleArgs {
   uint64_t seed;
   const uint64_t* rng_ctr;
   uint32_t rng_stream;
+  // draws > 1: the batches of `draws` consecutive training steps in ONE launch (blockIdx.y = draw k, keyed on
+  // RNG step *rng_ctr + k, its outputs at the pointers above + k x draw_*).  step_bump / step_bump2 then point at
+  // [draws] per-step counter arrays whose last entry is the canonical counter: entry q becomes last + q + 1 (the
+  // value the q-th per-step launch would have bumped it to), and metrics at [draws, 4] zeroed.
+  int draws;
+  int64_t draw_h, draw_x, draw_col;
   ClientBatch cb;           // set by launch_sample
 };
 

@@ -154,6 +154,10 @@ class EngineConfig:
     # Off: the folded step measured 214 us with it against 205 us without (no fold: 194 us) -- the producer's
     # serialised last-arrival merge costs more than the consumers' merges (profiles/bn_fold_r5.txt).
     bn_fold_publish: bool = False
+    # HIP step graphs (paired step, one client): ONE sampler launch at the head of each graph replay draws the
+    # batches of all graph_unroll steps (step k keyed on RNG step ctr + k, into batch-buffer set k) instead of a
+    # sampler launch heading every step -- bitwise the same draws; the launch is off the per-step serial path
+    multi_draw: bool = True
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -275,8 +279,18 @@ class CTGANEngine:
         self.vG = self.mem.zeros(self.nG)
         self.mD = self.mem.zeros(self.nD)
         self.vD = self.mem.zeros(self.nD)
-        self.stepG = self.mem.zeros(1)
-        self.stepD = self.mem.zeros(1)
+        # multi-step draws (EngineConfig.multi_draw): per-step optimizer counters [D | G] x U; the last entry of each
+        # row is the canonical counter every other path reads and bumps
+        self._U = max(1, int(self.cfg.graph_unroll))
+        self._multi = bool(self.cfg.multi_draw) and self.device.type == "cuda" and getattr(self.ops, "name", "") == "hip" \
+            and bool(self.cfg.paired) and not self.cfg.streams and self._U > 1 and isinstance(self.mem, TorchAlloc)
+        if self._multi:
+            self._step_sets = self.mem.zeros(2, self._U)
+            self.stepD = self._step_sets[0, self._U - 1:]
+            self.stepG = self._step_sets[1, self._U - 1:]
+        else:
+            self.stepG = self.mem.zeros(1)
+            self.stepD = self.mem.zeros(1)
         self.reset_parameters()
 
     def _layout(self, g_wt: bool):
@@ -452,6 +466,7 @@ class CTGANEngine:
                              1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
                              all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
         if self._fold_static:
+            self._multi = False
             # rows [Hp | H]: the sampler gets both as one row ([z in Hp] ... [c block in H], the c block last, as
             # its width is read off the row's end)
             big = _padded_rows(2 * B, c0 + self.Hw, dev)
@@ -461,6 +476,11 @@ class CTGANEngine:
             self._bn_part = [z(-(-2 * B // 32) * 6 * g) for g in self.gdims]   # 32-row tiles at most
             # arrival counters of the statistics-publishing GEMMs (one per column tile, re-zeroed by the kernel)
             self._bn_cnt = torch.zeros(len(self.gdims), 64, dtype=torch.int32, device=self.device)
+        elif self._multi:
+            # one set of the sampler's outputs per step of a graph replay: H2 (z | c behind the activations), the D
+            # input block and the draws' col / opt; set 0 is also what the per-step path uses
+            self._h2_sets = _padded_rows(self._U * 2 * B, self.Hw, dev)
+            self.H2 = self._h2_sets[:2 * B]
         else:
             self.H2 = _padded_rows(2 * B, self.Hw, dev)
         self.abuf2 = [z(2 * B, g) for g in self.gdims]
@@ -481,14 +501,12 @@ class CTGANEngine:
         # D's stacked batch is the first 3B rows; both phases' fake rows are contiguous, so one
         # activation launch writes them; the G phase's rows are separate so its prepare can overlap
         # the D update (lanes)
-        self.Xall = z(4 * B, self.Din)
-        self.X_interp = self.Xall[0:B]
-        self.X_real = self.Xall[B:2 * B]
-        self.X_fake = self.Xall[2 * B:3 * B]
-        self.Xd = self.Xall[0:3 * B]
-        self.X = self.Xd.view(3 * nP, self.K1)
-        self.Xg = self.Xall[3 * B:4 * B]
-        self.XgP = self.Xg.view(nP, self.K1)
+        if self._multi:
+            self._xall_sets = z(self._U * 4 * B, self.Din)
+            self.Xall = self._xall_sets[:4 * B]
+        else:
+            self.Xall = z(4 * B, self.Din)
+        self._x_views()
         self.dact = None
         self.dl = [z(3 * nP, h) for h in self.ddims]
         self.ms = [z(3 * nP, h) for h in self.ddims]
@@ -501,15 +519,57 @@ class CTGANEngine:
         self.coef3 = self.mem.tensor(torch.cat([torch.ones(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).float())
         self.wloss3 = self.mem.tensor(torch.cat([torch.zeros(nP), torch.full((nP,), -inv), torch.full((nP,), inv)]).float())
         self.coefg = self.mem.tensor(torch.full((nP,), -inv, dtype=f32))
-        self.col2 = self.mem.zeros(2 * B, dtype=torch.int32)
-        self.opt2 = self.mem.zeros(2 * B, dtype=torch.int32)
+        if self._multi:
+            self._col_sets = self.mem.zeros(self._U * 2 * B, dtype=torch.int32)
+            self._opt_sets = self.mem.zeros(self._U * 2 * B, dtype=torch.int32)
+            self._metrics_sets = z(self._U, 4)
+            self.col2, self.opt2 = self._col_sets[:2 * B], self._opt_sets[:2 * B]
+            self.metrics = self._metrics_sets[self._U - 1]
+        else:
+            self.col2 = self.mem.zeros(2 * B, dtype=torch.int32)
+            self.opt2 = self.mem.zeros(2 * B, dtype=torch.int32)
+            self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
         self.col = self.col2[B:]
         self.opt = self.opt2[B:]
-        self.metrics = z(4)     # [wgan_d, pen, wgan_g, cond_ce]
         # per-pack penalty / per-row cond-CE terms, summed into metrics by the column-sum launch that
         # follows (no same-address atomics in the producing kernels)
         self.pen_rows = z(nP)
         self.ce_rows = z(B)
+
+    def _x_views(self):
+        """The D input block's views: [interp | real | fake (D phase) | fake (G phase)] rows of self.Xall."""
+        B, nP = self.B, self.nP
+        self.X_interp = self.Xall[0:B]
+        self.X_real = self.Xall[B:2 * B]
+        self.X_fake = self.Xall[2 * B:3 * B]
+        self.Xd = self.Xall[0:3 * B]
+        self.X = self.Xd.view(3 * nP, self.K1)
+        self.Xg = self.Xall[3 * B:4 * B]
+        self.XgP = self.Xg.view(nP, self.K1)
+
+    def _bind_set(self, k: int = 0, step: Optional[int] = None):
+        """Multi-step draws: issue the following launches on batch-buffer set k with step ``step``'s optimizer
+        counters and metrics (None: the canonical ones, the last entries)."""
+        B = self.B
+        self.H2 = self._h2_sets[k * 2 * B:(k + 1) * 2 * B]
+        self.H = self.H2[B:]
+        self.Xall = self._xall_sets[k * 4 * B:(k + 1) * 4 * B]
+        self._x_views()
+        self.col2 = self._col_sets[k * 2 * B:(k + 1) * 2 * B]
+        self.opt2 = self._opt_sets[k * 2 * B:(k + 1) * 2 * B]
+        self.col, self.opt = self.col2[B:], self.opt2[B:]
+        j = self._U - 1 if step is None else int(step)
+        self.stepD = self._step_sets[0, j:j + 1]
+        self.stepG = self._step_sets[1, j:j + 1]
+        self.metrics = self._metrics_sets[j]
+
+    def _draw_all(self):
+        """The batches of the graph's U steps in one sampler launch (bound to set 0 / the counter arrays)."""
+        B, U = self.B, self._U
+        self.ops.sample_train(self.tables, self.H2, self.z_cols, self.c_cols, self.Xall[2 * B:4 * B], self.X_real,
+                              self.Dd, self.col2, self.opt2, step_counter=(self._step_sets[0], self._step_sets[1]),
+                              metrics=self._metrics_sets, zero_metrics=True, stream_id=1, draws=U,
+                              strides=(2 * B * self.H2.stride(0), 4 * B * self.Xall.stride(0), 2 * B))
 
     # ================================================================= data
     def set_training_data(self, encoded, rows: RowIndex | None = None, cond: CondTables | None = None):
@@ -778,7 +838,7 @@ class CTGANEngine:
                         slerp=(self.X_real, self.X_fake, self.X_interp, 3),
                         cond=(self.col, self.opt, self.cfg.onehot_trans))
 
-    def _prepare_paired(self):
+    def _prepare_paired(self, draw: bool = True):
         """Both phases' batches in one pass: one sampler launch draws the D-phase batch (with real
         rows) and the G-phase batch, and the generator runs once on the 2B stacked rows.
 
@@ -791,9 +851,10 @@ class CTGANEngine:
         if self._fold_on():     # z goes to the pre-BN rows Hp, the condition block to H: one sampler launch
             c0 = self.c_cols[0]
             h, cc = self._Hbig, (c0 + self.c_cols[0], c0 + self.c_cols[1])
-        o.sample_train(self.tables, h, self.z_cols, cc, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
-                       self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
-                       zero_metrics=True, stream_id=1)
+        if draw:                # (else drawn ahead by the graph's multi-step sampler launch, _draw_all)
+            o.sample_train(self.tables, h, self.z_cols, cc, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
+                           self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
+                           zero_metrics=True, stream_id=1)
         self._g_forward(self.H2, self.logits2, training=True, act_out=self.Xall[2 * B:4 * B, :self.Dd], stream_id=2,
                         slerp=(self.X_real, self.X_fake, self.X_interp, 3), paired=True,
                         cond=(self.col2, self.opt2, self.cfg.onehot_trans))
@@ -1011,11 +1072,11 @@ class CTGANEngine:
         """The generator input block [z | c] of an H buffer (written by the sampler)."""
         return (self.H if H is None else H)[:, self.off[0]:]
 
-    def _one_step(self):
+    def _one_step(self, draw: bool = True):
         if hasattr(self.ops, "begin_step"):
             self.ops.begin_step(self)
         try:
-            self._issue_step()
+            self._issue_step(draw)
         except BaseException:
             # a raise between a held GEMM (ops.gemm group 1/3/4) and its consumer must not leave the hold
             # behind for the next step on this thread
@@ -1023,10 +1084,10 @@ class CTGANEngine:
                 self.ops.reset_held()
             raise
 
-    def _issue_step(self):
+    def _issue_step(self, draw: bool = True):
         if self.lanes is None and self.cfg.paired:
             # both batches drawn and generated up front (G is unchanged by the D update)
-            self._prepare_paired()
+            self._prepare_paired(draw)
             self._d_update()
             self._g_update()
         elif self.lanes is None:      # the reference order: D step, then G step
@@ -1121,7 +1182,8 @@ class CTGANEngine:
         # (the device Philox counter too: a capture must not shift the clients' random streams, whatever step of
         # an epoch -- or which epoch segment of a batched engine with ragged clients -- it happens at)
         state = self.batch.state_tensors() if self.batch is not None else \
-            [self.flat, self.mG, self.vG, self.mD, self.vD, self.stepG, self.stepD] + \
+            [self.flat, self.mG, self.vG, self.mD, self.vD] + \
+            ([self._step_sets] if self._multi else [self.stepG, self.stepD]) + \
             ([self.ops.ctr] if hasattr(self.ops, "ctr") else [])
         snap = [t.clone() for t in state]
         s = torch.cuda.Stream(self.device)
@@ -1137,9 +1199,23 @@ class CTGANEngine:
             for dst, src in zip(state, snap):
                 dst.copy_(src)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
-            for _ in range(steps):      # every step re-reads the device RNG/step counters
-                self._one_step()
+        multi = self._multi and steps == self._U and self.batch is None
+        try:
+            with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
+                if multi:
+                    # one launch draws every step's batch into its own buffer set; step k then runs on set k with
+                    # its own optimizer counters / metrics (written by that launch)
+                    self._bind_set(0, 0)
+                    self._draw_all()
+                    for k in range(steps):
+                        self._bind_set(k, k)
+                        self._one_step(draw=False)
+                else:
+                    for _ in range(steps):      # every step re-reads the device RNG/step counters
+                        self._one_step()
+        finally:
+            if multi:
+                self._bind_set(0)
         self.graphs[self._graph_key(steps)] = g
         return g
 

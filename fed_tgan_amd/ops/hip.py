@@ -383,16 +383,19 @@ class HipOps:
 
     # ------------------------------------------------------------------ samplers
     def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,
-                     metrics=None, zero_metrics=False, stream_id=0):
+                     metrics=None, zero_metrics=False, stream_id=0, draws=1, strides=(0, 0, 0)):
         """x_real may cover only the leading x_real.shape[0] rows of h / x_fake: those rows are the
         D-phase batch, the rest a G-phase batch drawn by the same launch.  step_counter: a device
-        counter or a pair of them, bumped by the launch."""
+        counter or a pair of them, bumped by the launch.  draws > 1: the batches of that many consecutive
+        steps (strides = element offsets between the draws' h / D-input / col-opt buffers; step_counter and
+        metrics are then per-step arrays, see SampleArgs::draws)."""
         E = z_cols[1] - z_cols[0]
         sc = step_counter if isinstance(step_counter, (tuple, list)) else (step_counter, None)
         if x_real is not None:
             self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, x_real, Dd, t["cdf_log"], t["cond_offset"],
                           t["cond_width"], t["row_offset"], t["row_count"], t["rows"], t["data"], col_out, opt_out,
-                          sc[0], sc[1], metrics, bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16)
+                          sc[0], sc[1], metrics, bool(zero_metrics), self.seed, self.ctr, int(stream_id) * 16,
+                          int(draws), *(int(x) for x in strides))
         else:
             self.L.sample(h, z_cols[0], c_cols[0], E, x_fake, None, Dd, t["cdf_log"], t["cond_offset"],
                           t["cond_width"], None, None, None, None, col_out, opt_out, sc[0], sc[1], metrics,

@@ -553,3 +553,32 @@ def test_bn_fold_config_is_checked():
         L.gemm_bnl_next(*args(w, 2))          # k0 not a multiple of 4
     L.gemm_bnl_next(*args(w, 0))
     assert L.reset_held() == 1 and L.reset_held() == 0
+
+
+@pytest.mark.gpu
+def test_multi_draw_matches_per_step_sampler():
+    """EngineConfig.multi_draw: the step graph's one sampler launch for all graph_unroll steps (buffer set k, RNG
+    step ctr + k, per-step optimizer counters) trains bitwise like a sampler launch per step -- over two graph
+    replays plus a leftover single step, with the canonical counters and last-step losses where the per-step path
+    leaves them."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    out = []
+    for multi in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, multi_draw=multi, graph_unroll=4), DEV,
+                          backend="hip", seed=7)
+        assert eng._multi == multi
+        eng.set_training_data(X)
+        eng.train_steps(9, use_graph=True)      # 2 x 4-step graph + 1 single step
+        eng.train_steps(1, use_graph=False)     # and one eager step on the canonical binding
+        torch.cuda.synchronize()
+        out.append((eng.flat.clone(), eng.mG.clone(), eng.vD.clone(), eng.stepD.clone(), eng.stepG.clone(),
+                    eng.metrics.clone(), eng.ops.ctr.clone()))
+    for name, a, b in zip(("flat", "mG", "vD", "stepD", "stepG", "metrics", "ctr"), *out):
+        if name == "metrics":     # (the WGAN terms are float atomics across workgroups: order-dependent last bits)
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+        else:
+            assert torch.equal(a, b), name
+    assert float(out[1][3]) == 10.0 and float(out[1][4]) == 10.0

@@ -23,6 +23,16 @@ def main(db, out=None):
     lines = [f"critical-path total {tot:.1f} us over {sum(len(v) for v in inc.values())} kernels"]
     for k, v in sorted(inc.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"{100 * sum(v) / tot:5.1f}%  n={len(v):4d}  avg {sum(v) / len(v):6.2f} us  {k}")
+    # one steady-state step in issue order (the last full window of kernels-per-step launches): where the
+    # launches sit relative to each other, with each one's start gap after the previous end and its duration
+    n_samp = sum(len(v) for k, v in inc.items() if k.startswith("sample_kernel") or k.startswith("sample_multi"))
+    per = max(1, round(len(rows) / max(1, n_samp)))
+    if "--order" in sys.argv and len(rows) > 2 * per:
+        lines.append(f"one step in order (~{per} kernels): gap_us dur_us inc_us kernel")
+        seq = rows[len(rows) // 2: len(rows) // 2 + per + 1]
+        for (ps, pe, *_), (s, e, name, gx, gy, gz, wx) in zip(seq, seq[1:]):
+            key = name.split("(")[0].replace("void ", "").replace("fedtgan::", "")[:44] + f" grid=({gx // wx},{gy},{gz})"
+            lines.append(f"  {(s - pe) / 1000.0:6.2f} {(e - s) / 1000.0:6.2f} {(e - max(pe, s)) / 1000.0:6.2f}  {key}")
     text = "\n".join(lines)
     print(text)
     if out:
