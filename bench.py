@@ -290,7 +290,7 @@ def run_rank(args) -> None:
         if args.tuning:
             rec["tuning"] = args.tuning
         print(json.dumps(rec), flush=True)
-    comm.destroy()
+    rt.close()           # writers joined, graphs released, communicators destroyed -- before interpreter exit
 
 
 def main():

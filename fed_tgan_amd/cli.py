@@ -232,6 +232,7 @@ def run_rank(rank: int, args, on_done=None) -> None:
         if on_done is not None:
             on_done(rt, comm)
         comm.barrier()
+        rt.close()          # writers joined, graphs released, communicators destroyed (before interpreter exit)
     finally:
         comm.destroy()
 

@@ -767,6 +767,29 @@ class FedRuntime:
             self.write_epoch_csv(share, epoch)
         return share if self.is_fed else None
 
+    def close(self) -> None:
+        """Orderly teardown (idempotent): every epoch CSV on disk, the writer and label-encoder helper joined,
+        the device drained, the captured graphs and side streams released, then the communicators destroyed --
+        all before interpreter exit, whose destructor order is arbitrary (a run under rocprofv3 segfaulted in
+        exit() after the tool's finalisation, profiles/exit_r6.txt)."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
+        try:
+            self.flush_writes()
+        finally:
+            w, self._writer = getattr(self, "_writer", None), None
+            if w is not None:
+                w.close()
+            if getattr(self, "_le_proc", None) is not None:
+                self.write_label_encoders()
+            eng = getattr(self, "engine", None)
+            if eng is not None:
+                eng.release()
+            self._gen_stream = self._copy_stream = None
+            if getattr(self, "comm", None) is not None:
+                self.comm.destroy()
+
     def _complete_handoff(self):
         """Issue the deferred part of the last pipelined sample_round: the generation body on the side stream,
         the gather to the federator, the pinned copy and the CSV writer hand-off."""

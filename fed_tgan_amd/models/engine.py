@@ -1219,6 +1219,18 @@ class CTGANEngine:
         self.graphs[self._graph_key(steps)] = g
         return g
 
+    def release(self) -> None:
+        """Drop every captured hipGraph (step, generation, split generation) once the device is idle.  Called by
+        FedRuntime.close() before the process exits, so the graphs are destroyed while the HIP runtime (and any
+        tool attached to it, e.g. rocprofv3) is intact rather than by the interpreter's teardown in arbitrary
+        order."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.graphs.clear()
+        self._gen_graphs.clear()
+        self._gen_split.clear()
+        self._gen_done = None
+
     @property
     def graph(self):
         """The one-step graph, if captured (inspection / tests)."""

@@ -112,3 +112,65 @@ def test_aggregation_weight_formula():
     assert aggregation_weights(d_hat, e_hat, rows) == pytest.approx(np.exp(raw) / np.exp(raw).sum())
     assert softmax(np.array([0.0, 0.0])) == pytest.approx([0.5, 0.5])
     assert uniform_weights(4) == pytest.approx([0.25] * 4)
+
+
+def test_unequal_client_aggregate_matches_reference():
+    """The unequal-client FedAvg against the reference's own code.  Fixture
+    tests/golden/unequal_agg.npz (tools/make_unequal_fixture.py): the reference's MDGANClient.train_model(1) on the
+    Adult Dirichlet(0.3) split's two clients (11 and 20 steps per epoch), their state dicts, the federator's
+    distances and weights (`Server/dtds/distributed.py:767-783`) and its aggregate (`average_model`, `:86-106`,
+    loaded into the generator as at `:811`).  This framework's weights (fed/stats.py) and its aggregation
+    (FedRuntime.aggregate: one pre-scaled all-reduce of the flat buffer -- every parameter AND the BatchNorm running
+    statistics -- plus num_batches_tracked = the truncated weighted sum of 2 x steps) must give the same model."""
+    import os
+    import threading
+
+    import torch
+
+    from fed_tgan_amd.features.transformer import SpanLayout
+    from fed_tgan_amd.fed.local import LocalGroup, ThreadComm
+    from fed_tgan_amd.fed.runtime import FedRuntime
+    from fed_tgan_amd.models.engine import CTGANEngine, EngineConfig
+
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "unequal_agg.npz"))
+    w = aggregation_weights(fx["d_hat"], fx["e_hat"], fx["rows"])
+    np.testing.assert_allclose(w, fx["weights"], rtol=1e-12)
+    assert fx["steps"].tolist() == [11, 20]
+    info = [(int(a), "tanh" if k == 0 else "softmax") for a, k in zip(fx["span_width"], fx["span_kind"])]
+    dims = tuple(int(x) for x in fx["dims"])
+    cfg = EngineConfig(gen_dims=dims, dis_dims=dims)
+    k = 2
+    engines = []
+    for i in range(k):
+        e = CTGANEngine(SpanLayout.from_output_info(info), cfg, "cpu", backend="torch", seed=100 + i)
+        e.load_g_state_dict({key: torch.from_numpy(fx[f"G{i}|{key}"]) for key in fx["G_keys"]})
+        e.load_d_state_dict({key: torch.from_numpy(fx[f"D{i}|{key}"]) for key in fx["D_keys"]})
+        assert e.bn_batches == 2 * int(fx["steps"][i])
+        engines.append(e)
+    group = LocalGroup(k)
+
+    class _Cfg:
+        phase_detail = False
+
+    def client(i):
+        rt = FedRuntime.__new__(FedRuntime)
+        rt.cfg, rt.comm, rt.engine = _Cfg(), ThreadComm(group, i, torch.device("cpu")), engines[i]
+        rt.weights, rt.is_client, rt.is_fed, rt.federator = w, True, i == 0, 0
+        rt.steps, rt._epoch_done, rt._pipe = [int(s) for s in fx["steps"]], 1, False
+        rt.aggregate()
+
+    ts = [threading.Thread(target=client, args=(i,)) for i in range(k)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in engines:
+        got_g, got_d = e.g_state_dict(), e.d_state_dict()
+        for key in fx["G_keys"]:
+            want = fx[f"Gagg|{key}"]
+            if key.endswith("num_batches_tracked"):
+                assert int(got_g[key]) == int(want) == 32          # int(0.4307 * 22 + 0.5693 * 40)
+            else:
+                np.testing.assert_allclose(got_g[key].numpy(), want, rtol=2e-6, atol=1e-7, err_msg=key)
+        for key in fx["D_keys"]:
+            np.testing.assert_allclose(got_d[key].numpy(), fx[f"Dagg|{key}"], rtol=2e-6, atol=1e-7, err_msg=key)

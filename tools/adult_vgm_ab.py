@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--work", default="/tmp/fedtgan_adult_vgm")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fed", action="append", default=[], metavar="KEY=VALUE", help="FedConfig override (bool/int)")
+    ap.add_argument("--tag", default="", help="suffix of the recorded variant name")
     args = ap.parse_args()
     import torch
     from fed_tgan_amd.eval.similarity import stat_sim_normalize
@@ -74,12 +76,15 @@ def main():
             shutil.rmtree(work, ignore_errors=True)
             cfg = FedConfig(spec=spec, epochs=args.epochs, datapath=datapath, out_dir=work, n_sample=40000, seed=seed,
                             engine=EngineConfig(precision=args.precision), verbose=False, backend=args.backend)
+            for kv in args.fed:
+                key, val = kv.split("=", 1)
+                setattr(cfg, key, type(getattr(cfg, key))(int(val)) if val.isdigit() else val)
             rt = run_local_emulation(cfg, 2, backend=args.backend, device=dev)
             res_dir = os.path.join(work, f"{spec.name}_result")
             res = [stat_sim_normalize(train_path, os.path.join(res_dir, f"{spec.name}_synthesis_epoch_{ep}.csv"),
                                       list(spec.categorical_list)) for ep in range(args.epochs)]
             tr = rt.transformer
-            r = {"variant": var, "seed": seed, "avg_jsd": [float(x[0]) for x in res],
+            r = {"variant": var + args.tag, "seed": seed, "backend": args.backend, "precision": args.precision, "avg_jsd": [float(x[0]) for x in res],
                  "avg_wd": [float(x[1]) for x in res], "fits_modes": list(fits),
                  "global_modes": [int(c.sum()) for c in tr.components], "n_opt": int(tr.layout.n_opt),
                  "global_weights": np.round(tr.bank.weights, 4).tolist(),

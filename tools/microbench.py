@@ -33,7 +33,20 @@ def per_call(fn, dev, n=50, reps=20):
     return (time.perf_counter() - t) / (reps * n) * 1e6
 
 
-def step_only(eng, dev):
+def step_only(eng, dev, epochs_only=False):
+    # the engine's own epoch path: its graph_unroll-step graphs (multi-step sampler draw, EngineConfig.multi_draw)
+    eng.train_steps(eng.steps_per_epoch)
+    torch.cuda.synchronize(dev)
+    for _ in range(3):
+        t = time.perf_counter()
+        for _ in range(5):
+            eng.train_steps(eng.steps_per_epoch)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t) / (5 * eng.steps_per_epoch) * 1e6
+        print(f"engine epoch graphs (unroll {eng.cfg.graph_unroll}, multi_draw {eng._multi}): {dt:8.2f} us/step",
+              flush=True)
+    if epochs_only:
+        return
     for _ in range(2):
         a = per_call(eng._one_step, dev, n=5, reps=20)
         lanes, eng.lanes = eng.lanes, None
@@ -269,6 +282,7 @@ def main():
                     help="native set_tuning knob for A/B runs, e.g. --tuning bn_cols=16")
     ap.add_argument("--split-sweep", action="store_true", help="time every GEMM shape at each split-K factor")
     ap.add_argument("--step-only", action="store_true", help="time only the full captured step")
+    ap.add_argument("--epochs-only", action="store_true", help="with --step-only: only the engine's own epoch graphs")
     ap.add_argument("--gen", action="store_true", help="time the generation pass (eager / graph, chunk sizes)")
     ap.add_argument("--unroll", action="store_true", help="epoch time vs training steps captured per graph")
     ap.add_argument("--xcd-sweep", action="store_true", help="each step GEMM: dispatch vs XCD-contiguous tile order")
@@ -307,7 +321,7 @@ def main():
     nP, B = eng.nP, eng.B
     res = {}
     if args.step_only:
-        return step_only(eng, dev)
+        return step_only(eng, dev, args.epochs_only)
     if args.fork_probe:
         return fork_probe(eng, dev)
     if args.gwt_ab:
