@@ -291,6 +291,10 @@ def run_rank(args) -> None:
             rec["tuning"] = args.tuning
         print(json.dumps(rec), flush=True)
     rt.close()           # writers joined, graphs released, communicators destroyed -- before interpreter exit
+    maps = os.environ.get("FEDTGAN_DUMP_MAPS")
+    if maps:             # (diagnostics: the loaded libraries' address ranges, to symbolise a crash in exit())
+        with open("/proc/self/maps") as src, open(f"{maps}.{rank}", "w") as dst:
+            dst.write(src.read())
 
 
 def main():

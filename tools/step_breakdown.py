@@ -4,6 +4,8 @@ rocprofv3's kernel start stamps include the wait for the previous kernel of the 
 honest per-kernel cost is the increment it adds to the completion timeline:
 inc_k = end_k - max(end_{k-1}, start_k).  Usage: step_breakdown.py run_results.db [--out=F]"""
 import collections
+
+import numpy as np
 import sqlite3
 import sys
 
@@ -33,6 +35,25 @@ def main(db, out=None):
         for (ps, pe, *_), (s, e, name, gx, gy, gz, wx) in zip(seq, seq[1:]):
             key = name.split("(")[0].replace("void ", "").replace("fedtgan::", "")[:44] + f" grid=({gx // wx},{gy},{gz})"
             lines.append(f"  {(s - pe) / 1000.0:6.2f} {(e - s) / 1000.0:6.2f} {(e - max(pe, s)) / 1000.0:6.2f}  {key}")
+    if "--gaps" in sys.argv:
+        # idle time between consecutive kernels (start_k - end_{k-1} > 0): where the device waits for the host /
+        # the graph's packet submission; the critical-path totals above exclude it
+        gaps = []
+        pe = rows[0][1]
+        for i, (s, e, name, *_rest) in enumerate(rows[1:], 1):
+            if s > pe:
+                gaps.append(((s - pe) / 1000.0, i, rows[i - 1][2].split("(")[0][-40:], name.split("(")[0][-40:]))
+            pe = max(pe, e)
+        big = [g for g in gaps if g[0] > 3.0]
+        span = (rows[-1][1] - rows[0][0]) / 1000.0
+        lines.append(f"gaps: {len(gaps)} idle intervals, {sum(g[0] for g in gaps):.1f} us idle of {span:.1f} us "
+                     f"({len(big)} longer than 3 us, {sum(g[0] for g in big):.1f} us)")
+        for g in big[:12]:
+            lines.append(f"  gap {g[0]:7.2f} us before kernel #{g[1]}: {g[2]} -> {g[3]}")
+        if len(big) > 1:
+            idx = [g[1] for g in big]
+            d = np.diff(idx)
+            lines.append(f"  kernels between long gaps: min {d.min()} median {int(np.median(d))} max {d.max()}")
     text = "\n".join(lines)
     print(text)
     if out:
