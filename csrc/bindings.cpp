@@ -851,13 +851,28 @@ void linear_bn_relu_colown(const Tensor& x, const Tensor& w, const optional<Tens
 }
 
 void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Tensor& gamma, const Tensor& invstd,
-                 const Tensor& da, const Tensor& dgamma, const Tensor& dbeta, const optional<Tensor>& dbias) {
+                 const Tensor& da, const Tensor& dgamma, const Tensor& dbeta, const optional<Tensor>& dbias,
+                 bool paired) {
   check_f32_2d(dr, "dr");
   check_f32_2d(r, "r");
   check_f32_2d(nhat, "nhat");
   check_f32_2d(da, "da");
   TORCH_CHECK(dr.size(0) >= 1, "bn_relu_bwd: empty batch");
   TORCH_CHECK(r.sizes() == dr.sizes() && nhat.sizes() == dr.sizes() && da.sizes() == dr.sizes(), "bn bwd: shapes");
+  TORCH_CHECK(gamma.numel() >= dr.size(1) && invstd.numel() >= dr.size(1) && dgamma.numel() >= dr.size(1) &&
+                  dbeta.numel() >= dr.size(1) && (!(dbias.has_value() && dbias->defined()) || dbias->numel() >= dr.size(1)),
+              "bn bwd: per-column vectors");
+  if (paired) {
+    // the GEMM held with group=1 (an independent weight gradient) runs in the same launch (gemm_bnbwd_kernel)
+    const hipStream_t hs = cur_stream();
+    TORCH_CHECK(has_held && held_stream == hs, "bn_relu_bwd(paired=True) needs a GEMM held with group=1 on this stream");
+    has_held = false;
+    const fedtgan::BnBwdArgs b{cfp(dr), ld_of(dr), cfp(r), ld_of(r), cfp(nhat), ld_of(nhat), cfp(gamma), cfp(invstd),
+                               fp(da), ld_of(da), fp(dgamma), fp(dbeta), optp<float>(dbias), (int)dr.size(0),
+                               (int)dr.size(1)};
+    if (fedtgan::launch_gemm_bnbwd(held, b, hs)) return;
+    fedtgan::launch_gemm(held, hs);     // (a shape the fused launch does not take: two launches)
+  }
   fedtgan::launch_bn_relu_bwd(cfp(dr), ld_of(dr), cfp(r), ld_of(r), cfp(nhat), ld_of(nhat), cfp(gamma), cfp(invstd),
                               fp(da), ld_of(da), fp(dgamma), fp(dbeta), optp<float>(dbias), (int)dr.size(0),
                               (int)dr.size(1), cur_stream());
@@ -1324,6 +1339,17 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_adam_u_min = value;
     return prev;
   }
+  if (key == "bnb_first") {   // gemm_bnbwd_kernel: BN workgroups first (1) or last (0)
+    const int64_t prev = fedtgan::g_bnb_first;
+    fedtgan::g_bnb_first = value ? 1 : 0;
+    return prev;
+  }
+  if (key == "bnb_cols") {    // gemm_bnbwd_kernel: columns per BN workgroup, 4 or 8
+    TORCH_CHECK(value == 4 || value == 8, "bnb_cols: 4 or 8");
+    const int64_t prev = fedtgan::g_bnb_cols;
+    fedtgan::g_bnb_cols = (int)value;
+    return prev;
+  }
   if (key == "vgm_split") {   // workgroups per column of the whole-fit VGM kernel: 0 auto, 1 one, n n
     TORCH_CHECK(value >= 0 && value <= 64, "vgm_split: 0..64");
     const int64_t prev = fedtgan::g_vgm_split;
@@ -1415,7 +1441,7 @@ TORCH_LIBRARY(fedtgan, m) {
       "Tensor(c!) mean, Tensor(d!) invstd, Tensor(e!) rm, Tensor(f!) rv, float momentum, float eps, int groups) -> ()");
   m.def(
       "bn_relu_bwd(Tensor dr, Tensor r, Tensor nhat, Tensor gamma, Tensor invstd, Tensor(a!) da, Tensor(b!) dgamma, "
-      "Tensor(c!) dbeta, Tensor(d!)? dbias) -> ()");
+      "Tensor(c!) dbeta, Tensor(d!)? dbias, bool paired=False) -> ()");
   m.def(
       "adam(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor step, float lr, float b1, float b2, float eps, "
       "float wd, Tensor(d!)? rng_bump) -> ()");

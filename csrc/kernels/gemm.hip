@@ -38,6 +38,7 @@
 #include "common.h"
 #include "launch.h"
 #include "adam_cs.h"
+#include "bn_bwd.h"
 
 namespace fedtgan {
 
@@ -1855,6 +1856,60 @@ void launch_gemm_pair(GemmArgs g1, GemmArgs g2, hipStream_t stream) {
   }
   gemm_epilogue_launch(g1, stream);
   gemm_epilogue_launch(g2, stream);
+}
+
+// BN backward workgroups first (the narrow latency-bound part starts at once; g_bnb_first = 0: after the GEMM's
+// tiles), COLS columns per BN workgroup (g_bnb_cols: 4 or 8)
+int g_bnb_first = 1;
+int g_bnb_cols = 4;
+
+template <bool V, int T, int COLS, int MAXR>
+__global__ __launch_bounds__(NT) void gemm_bnbwd_kernel(GemmArgs g, Grid3 gd, BnBwdArgs bn, int nbn, int first) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * Cfg<false, T, T>::STAGE];
+  const int nt = gd.x * gd.y * gd.z;
+  const int b = (int)blockIdx.x;
+  const bool is_bn = first ? b < nbn : b >= nt;
+  if (is_bn) {
+    bn_bwd_block<COLS, MAXR, NT>(bn, first ? b : b - nt, reinterpret_cast<float*>(smem));
+    return;
+  }
+  const int t = first ? b - nbn : b;
+  gemm_tile<true, false, false, V, T, T>(g, t % gd.x, (t / gd.x) % gd.y, t / (gd.x * gd.y), gd.x, gd.y, gd.z, smem);
+}
+
+bool launch_gemm_bnbwd(GemmArgs g, const BnBwdArgs& b, hipStream_t stream) {
+  if (g.M <= 0 || g.N <= 0 || b.rows <= 0 || b.cols <= 0) return false;
+  if (client_batch().k > 1 || g.f32 || g.bin || g.c16 || !g.ta || g.tb || g.chain || g.nbnl > 0 || g.bn_part) return false;
+  const int cols = g_bnb_cols == 8 ? 8 : 4;
+  const int groups = NT / cols;
+  const int maxr = (b.rows + groups - 1) / groups;
+  if (maxr > 16) return false;
+  static_assert(3 * (NT / 64) * 8 * 4 <= 2 * Cfg<false, 32, 32>::STAGE, "BN scratch fits the GEMM stage buffer");
+  check_slab(g);
+  const dim3 d = gemm_prepare(g);
+  if (g.tile != 32 && g.tile != 64) return false;
+  const Grid3 gd{(int)d.x, (int)d.y, (int)d.z};
+  const int nbn = (b.cols + cols - 1) / cols;
+  const dim3 grid(nbn + gd.x * gd.y * gd.z), block(NT);
+  const int first = g_bnb_first;
+#define FEDTGAN_BNB(V, T, C, R) \
+  hipLaunchKernelGGL((gemm_bnbwd_kernel<V, T, C, R>), grid, block, 0, stream, g, gd, b, nbn, first)
+#define FEDTGAN_BNB_R(V, T, C)              \
+  if (maxr <= 4) FEDTGAN_BNB(V, T, C, 4);    \
+  else if (maxr <= 8) FEDTGAN_BNB(V, T, C, 8); \
+  else FEDTGAN_BNB(V, T, C, 16);
+#define FEDTGAN_BNB_C(V, T) \
+  if (cols == 8) { FEDTGAN_BNB_R(V, T, 8) } else { FEDTGAN_BNB_R(V, T, 4) }
+  if (g.vec) {
+    if (g.tile == 32) { FEDTGAN_BNB_C(true, 32) } else { FEDTGAN_BNB_C(true, 64) }
+  } else {
+    if (g.tile == 32) { FEDTGAN_BNB_C(false, 32) } else { FEDTGAN_BNB_C(false, 64) }
+  }
+#undef FEDTGAN_BNB_C
+#undef FEDTGAN_BNB_R
+#undef FEDTGAN_BNB
+  gemm_epilogue_launch(g, stream);
+  return true;
 }
 
 bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v, const float* step, int64_t n,

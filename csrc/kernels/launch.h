@@ -371,6 +371,29 @@ void launch_bn_relu_apply(const float* a, int lda, const float* part, int n_tile
 void launch_bn_relu_bwd(const float* dr, int lddr, const float* r, int ldr, const float* nhat, int ldn,
                         const float* gamma, const float* invstd, float* da, int ldda, float* dgamma, float* dbeta,
                         float* dbias, int rows, int cols, hipStream_t stream);
+// operands of one BatchNorm(train) + ReLU backward (bn_bwd.h)
+struct BnBwdArgs {
+  const float* dr;
+  int lddr;
+  const float* r;
+  int ldr;
+  const float* nhat;
+  int ldn;
+  const float* gamma;
+  const float* invstd;
+  float* da;
+  int ldda;
+  float* dgamma;
+  float* dbeta;
+  float* dbias;   // nullable
+  int rows, cols;
+};
+// the BN backward's column workgroups and an INDEPENDENT weight-gradient GEMM (op(A) = A^T, bf16 MFMA, 32/64
+// tile) in ONE launch (horizontal fusion: the 32-64 narrow, latency-bound BN workgroups no longer run alone on the
+// chip).  Returns false (nothing launched) where that combination is not instantiated.
+bool launch_gemm_bnbwd(GemmArgs g, const BnBwdArgs& b, hipStream_t stream);
+extern int g_bnb_first;   // gemm_bnbwd_kernel: BN workgroups before (1) or after (0) the GEMM tiles
+extern int g_bnb_cols;    // gemm_bnbwd_kernel: columns per BN workgroup (4 or 8)
 
 void launch_adam(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
                  float b2, float eps, float wd, uint64_t* rng_ctr_bump, hipStream_t stream);

@@ -158,6 +158,12 @@ class EngineConfig:
     # batches of all graph_unroll steps (step k keyed on RNG step ctr + k, into batch-buffer set k) instead of a
     # sampler launch heading every step -- bitwise the same draws; the launch is off the per-step serial path
     multi_draw: bool = True
+    # HIP, paired step: each generator layer's BatchNorm + ReLU backward shares its launch with the weight gradient
+    # of the layer above (independent of it; csrc gemm_bnbwd_kernel) instead of the weight gradient sharing a launch
+    # with that layer's dH product -- the BN backward's 32-64 narrow workgroups then no longer run alone on the chip.
+    # Off: measured no gain (189.6-191.0 us/step in every layout vs 189.0-190.2 without; profiles/bn_pair_r6.txt) --
+    # the dH products lose the launch they shared with the weight gradients as much as the BN backward gains
+    bn_pair: bool = False
 
 
 def get_ops(backend: str, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
@@ -994,6 +1000,32 @@ class CTGANEngine:
             if oh_w is not None and len(oh_w) > n0:
                 oh_dy.append(dy)
             return x, dW
+        # bn_pair: [dH_out] -> [BN_{L-1} bwd | dW_out] -> [dH_{L-1}] -> [BN_{L-2} bwd | dW_{L-1}] ... -> [dW_0 + Adam]
+        bn_pair = pair and bool(self.cfg.bn_pair) and getattr(o, "bn_pair_capable", False)
+        if bn_pair:
+            jobs = self._g_colsum_jobs()
+            if not fold_colsum:
+                o.colsum_many(*jobs)
+            o.gemm(self.dlogits, self.p["G.out.W"][:, :top], self.dH[:, :top])
+            x, dW = wgrad(self.dlogits, 0, self.g["G.out.W"])
+            o.gemm(self.dlogits, x, dW, ta=True, group=1)        # launched with the next BN backward
+            for i in range(Lg - 1, -1, -1):
+                a, b_ = self.off[i], self.off[i + 1]
+                o.bn_relu_bwd(self.dH[:, b_:a], self.H[:, b_:a], self.nhat[i], self.p[f"G.{i}.gamma"],
+                              self.bn_invstd[i], self.da[i], self.g[f"G.{i}.gamma"], self.g[f"G.{i}.beta"],
+                              self.g[f"G.{i}.b"], paired=True)
+                x, dW = wgrad(self.da[i], a, self.g[f"G.{i}.W"])
+                if i > 0:
+                    o.gemm(self.da[i], self.p[f"G.{i}.W"][:, :top - a], self.dH[:, a:top], beta=1.0)
+                    o.gemm(self.da[i], x, dW, ta=True, group=1)   # launched with the next BN backward
+                else:
+                    fuse = fold_colsum and self.cfg.fuse_g_adam and self._adam_fusable(self.nG) and \
+                        getattr(o, "gemm_adam", False)
+                    o.gemm(self.da[i], x, dW, ta=True, group=3 if fuse else 0)
+            if oh_w:
+                o.onehot_wgrad(oh_dy, oh_w, self.col, self.opt, self._cond_off)
+                self._oh_pending = (oh_dy, oh_w)
+            return jobs if fold_colsum else None
         with self._lane(1):
             x, dW = wgrad(self.dlogits, 0, self.g["G.out.W"])
             o.gemm(self.dlogits, x, dW, ta=True, group=1 if pair else 0)

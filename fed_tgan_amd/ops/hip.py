@@ -378,8 +378,12 @@ class HipOps:
         self.L.bn_relu_train(a, gamma, beta, out, nhat, mean, invstd, rmean, rvar, float(momentum), float(eps),
                              int(groups))
 
-    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None):
-        self.L.bn_relu_bwd(dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias)
+    bn_pair_capable = True
+
+    def bn_relu_bwd(self, dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias=None, paired=False):
+        """paired: the GEMM held with gemm(..., group=1) runs in the same launch (an independent weight gradient
+        beside the BN backward's narrow column workgroups, csrc gemm_bnbwd_kernel)."""
+        self.L.bn_relu_bwd(dr, r, nhat, gamma, invstd, da, dgamma, dbeta, dbias, bool(paired))
 
     # ------------------------------------------------------------------ samplers
     def sample_train(self, t, h, z_cols, c_cols, x_fake, x_real, Dd, col_out, opt_out, step_counter=None,

@@ -181,7 +181,10 @@ def test_side_stream_overlap_is_race_free():
         torch.manual_seed(0)
         # (both per-phase: the lanes path draws each phase's batch separately; both with R1 as its own GEMM,
         # as the lanes path does not ride it on R0's reduction launch)
-        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, streams=streams, paired=False, fuse_d_adam=False),
+        # (bn_pair off: the lanes path keeps each weight gradient beside its layer's dH product, and only the
+        # same GEMM launches give bitwise the same sums)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, streams=streams, paired=False, fuse_d_adam=False,
+                                                  bn_pair=False),
                           DEV, backend="hip", seed=5)
         eng.set_training_data(X)
         eng.train_steps(6, use_graph=True)
@@ -582,3 +585,23 @@ def test_multi_draw_matches_per_step_sampler():
         else:
             assert torch.equal(a, b), name
     assert float(out[1][3]) == 10.0 and float(out[1][4]) == 10.0
+
+
+@pytest.mark.gpu
+def test_bn_pair_matches_unpaired():
+    """EngineConfig.bn_pair (BN backward + the weight gradient of the layer above in one launch, csrc
+    gemm_bnbwd_kernel) computes the same G update as the default schedule (fp32: to summation order)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    out = []
+    for bp in (False, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32", bn_pair=bp), DEV, backend="hip",
+                          seed=4)
+        eng.set_training_data(X)
+        eng.train_steps(2, use_graph=False)
+        torch.cuda.synchronize()
+        out.append((eng.flat.clone(), eng.gradG.clone()))
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-5, atol=1e-6)
