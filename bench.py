@@ -51,6 +51,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--sync-csv", action="store_true", help="write each epoch CSV inside its round")
+    ap.add_argument("--device-reset-at-exit", action="store_true",
+                    help="tear the HIP device down (hipDeviceReset) before interpreter exit: a run under rocprofv3 "
+                         "otherwise segfaults in libamdhip64's exit-time destructor (profiles/exit_r6.txt)")
     ap.add_argument("--check", action=argparse.BooleanOptionalAction, default=None,
                     help="after the timed rounds: assert every rank holds a bit-identical aggregate and the "
                          "last epoch CSV has n_sample rows (reported as 'consistency'); default on for N > 1")
@@ -291,6 +294,9 @@ def run_rank(args) -> None:
             rec["tuning"] = args.tuning
         print(json.dumps(rec), flush=True)
     rt.close()           # writers joined, graphs released, communicators destroyed -- before interpreter exit
+    if args.device_reset_at_exit and device.type == "cuda":
+        from fed_tgan_amd.ops import native
+        native.require().device_reset()
     maps = os.environ.get("FEDTGAN_DUMP_MAPS")
     if maps:             # (diagnostics: the loaded libraries' address ranges, to symbolise a crash in exit())
         with open("/proc/self/maps") as src, open(f"{maps}.{rank}", "w") as dst:

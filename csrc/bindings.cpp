@@ -122,6 +122,15 @@ thread_local BnPubPending g_bnpub{};
 // the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
 // (whose operand pointers may since have been freed) can never be launched or block the next step.
 // Returns the number of holds that were dropped.
+// hipDeviceSynchronize + hipDeviceReset of the current device: the process' HIP queues, events and memory are
+// torn down NOW, while every component attached to the runtime (e.g. rocprofv3's tool library) is still live,
+// instead of by libamdhip64's exit-time destructor (bench.py --device-reset-at-exit; profiles/exit_r6.txt).
+// Nothing may touch the device afterwards; returns the hipError_t of the reset.
+int64_t device_reset() {
+  (void)hipDeviceSynchronize();
+  return (int64_t)hipDeviceReset();
+}
+
 int64_t reset_held() {
   const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0) +
                     (g_bnl.active ? 1 : 0) + (g_bnpub.active ? 1 : 0);
@@ -1476,6 +1485,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy_op);
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
+  m.def("device_reset() -> int", &device_reset);
   m.def("gemm_bnpub_next(Tensor cnt, Tensor mean, Tensor invstd, Tensor rm, Tensor rv, float momentum, float eps) -> ()",
         &gemm_bnpub_next);
   m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "

@@ -496,14 +496,15 @@ int vgm_fit_split(int n_cols, int max_rows) {
 void launch_vgm_fit(const VgmFitAllArgs& a, hipStream_t stream) {
   if (a.n_cols == 0) return;
   if (a.split > 1) {
-    // the workgroups of a column wait for each other: a cooperative launch guarantees they are co-resident
-    // (or fails instead of deadlocking)
+    // The workgroups of a column wait for each other.  The grid is sized to what the device holds at once
+    // (vgm_fit_split: <= one workgroup per CU per column at the kernel's occupancy), so on an idle device every
+    // workgroup is resident; where one is not, its siblings' bounded spin times out, the column is marked dead
+    // (sticky, cluster_sum) and the host refits it unsplit (features/vgm_fit.py).  A plain launch, not
+    // hipLaunchCooperativeKernel: a process that had made a cooperative launch segfaulted in libamdhip64's
+    // exit-time teardown under rocprofv3 (exit 139 after the tool's finalisation; plain launches exit 0,
+    // profiles/exit_r6.txt).
     if (!a.xpart || !a.sync) throw std::runtime_error("vgm_fit: split fit without its record / counter buffers");
-    VgmFitAllArgs arg = a;
-    void* args[] = {&arg};
-    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(vgm_fit_kernel),
-                                                    dim3(a.n_cols * a.split), dim3(WF_THREADS), args, 0, stream);
-    if (e != hipSuccess) throw std::runtime_error(std::string("vgm_fit: cooperative launch: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(vgm_fit_kernel, dim3(a.n_cols * a.split), dim3(WF_THREADS), 0, stream, a);
     return;
   }
   hipLaunchKernelGGL(vgm_fit_kernel, dim3(a.n_cols), dim3(WF_THREADS), 0, stream, a);

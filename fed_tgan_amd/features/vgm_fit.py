@@ -204,9 +204,9 @@ def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: fl
         ic = (torch.as_tensor(np.asarray(init_centers, dtype=np.float64), device=dev)
               - shift.unsqueeze(1)).contiguous()
     args = (int(seed) & ((1 << 62) - 1), WEIGHT_PRIOR, float(tol), REG_COVAR, int(max_iter), 300)
-    # the split fit is a cooperative launch sized to about one workgroup per CU: fits of concurrent client
-    # threads (fed/local.py) are serialised process-wide, and each waits for its grid to drain (the info
-    # read) before the next may launch
+    # the split fit's workgroups wait for each other (a grid sized to about one workgroup per CU): fits of
+    # concurrent client threads (fed/local.py) are serialised process-wide, and each waits for its grid to
+    # drain (the info read) before the next may launch
     with _FIT_LOCK:
         L.vgm_fit(X.contiguous(), n, ic, *args, out, info, lbs)
         info_h = info.cpu().numpy()
