@@ -122,6 +122,46 @@ thread_local BnPubPending g_bnpub{};
 // the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
 // (whose operand pointers may since have been freed) can never be launched or block the next step.
 // Returns the number of holds that were dropped.
+void pool_sample(const Tensor& pool, const Tensor& seg_off, const Tensor& mean, const Tensor& sd, int64_t seed) {
+  TORCH_CHECK(pool.is_cuda() && pool.scalar_type() == at::kDouble && pool.is_contiguous(), "pool_sample: pool");
+  TORCH_CHECK(seg_off.is_cuda() && seg_off.scalar_type() == at::kLong && seg_off.is_contiguous() && seg_off.numel() >= 2,
+              "pool_sample: seg_off");
+  const int64_t nseg = seg_off.numel() - 1;
+  TORCH_CHECK(mean.is_cuda() && sd.is_cuda() && mean.scalar_type() == at::kDouble && sd.scalar_type() == at::kDouble &&
+                  mean.is_contiguous() && sd.is_contiguous() && mean.numel() == nseg && sd.numel() == nseg,
+              "pool_sample: mean / sd [nseg] fp64");
+  fedtgan::PoolSampleArgs a{pool.data_ptr<double>(), seg_off.data_ptr<int64_t>(), mean.data_ptr<double>(),
+                            sd.data_ptr<double>(), (int)nseg, pool.numel(), (uint64_t)seed};
+  fedtgan::launch_pool_sample(a, cur_stream());
+}
+
+void row_center(const Tensor& x, const Tensor& shift) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.is_contiguous(), "row_center: x");
+  TORCH_CHECK(shift.is_cuda() && shift.scalar_type() == at::kDouble && shift.numel() == x.size(0) && shift.is_contiguous(),
+              "row_center: shift [rows] fp64");
+  fedtgan::launch_row_center(x.data_ptr<double>(), shift.data_ptr<double>(), (int)x.size(0), x.size(1), cur_stream());
+}
+
+void csr_rows(const Tensor& opt, const Tensor& width, int64_t maxw, const Tensor& part, const Tensor& count,
+              const Tensor& offset, const Tensor& rows, int64_t chunk) {
+  TORCH_CHECK(opt.is_cuda() && opt.scalar_type() == at::kInt && opt.dim() == 2 && opt.stride(1) == 1, "csr_rows: opt");
+  const int64_t n = opt.size(0), n_col = opt.size(1);
+  const int64_t chunks = (n + chunk - 1) / std::max<int64_t>(chunk, 1);
+  TORCH_CHECK(chunk > 0 && maxw > 0, "csr_rows: chunk / maxw");
+  TORCH_CHECK(width.is_cuda() && width.scalar_type() == at::kInt && width.numel() == n_col, "csr_rows: width");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kInt && part.is_contiguous() && part.numel() >= n_col * chunks * maxw,
+              "csr_rows: part scratch [n_col, chunks, maxw] int32");
+  for (const Tensor* t : {&count, &offset})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->is_contiguous() && t->numel() == n_col * maxw,
+                "csr_rows: count / offset [n_col, maxw] int64");
+  TORCH_CHECK(rows.is_cuda() && rows.scalar_type() == at::kLong && rows.is_contiguous() && rows.numel() == n * n_col,
+              "csr_rows: rows [n_col * n] int64");
+  fedtgan::CsrArgs a{opt.data_ptr<int>(), (int)opt.stride(0), width.data_ptr<int>(), (int)n, (int)n_col, (int)maxw,
+                     (int)chunk, (int)chunks, part.data_ptr<int>(), count.data_ptr<int64_t>(), offset.data_ptr<int64_t>(),
+                     rows.data_ptr<int64_t>()};
+  fedtgan::launch_csr_rows(a, cur_stream());
+}
+
 // hipDeviceSynchronize + hipDeviceReset of the current device: the process' HIP queues, events and memory are
 // torn down NOW, while every component attached to the runtime (e.g. rocprofv3's tool library) is still live,
 // instead of by libamdhip64's exit-time destructor (bench.py --device-reset-at-exit; profiles/exit_r6.txt).
@@ -1128,7 +1168,9 @@ void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Ten
                 const Tensor& col_aux, const Tensor& col_span, const Tensor& col_lut_n, const Tensor& consts, const Tensor& means,
                 const Tensor& prec, const Tensor& stds, const Tensor& vrank, const Tensor& lut, int64_t seed,
                 int64_t stream) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 && x.stride(1) == 1, "vgm_encode: x");
+  // row-major, or column-major (a table uploaded as its [cols, rows] transpose: no device transposing copy)
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kDouble && x.dim() == 2 &&
+                  (x.stride(1) == 1 || x.stride(0) == 1 || x.size(0) <= 1 || x.size(1) <= 1), "vgm_encode: x");
   check_f32_2d(out, "out");
   TORCH_CHECK(opt.is_cuda() && opt.scalar_type() == at::kInt && opt.is_contiguous() && opt.size(0) == x.size(0),
               "vgm_encode: opt");
@@ -1143,6 +1185,7 @@ void vgm_encode(const Tensor& x, const Tensor& out, const Tensor& opt, const Ten
   fedtgan::VgmEncodeArgs a{};
   a.x = x.data_ptr<double>();
   a.ldx = (int)x.stride(0);
+  a.ldc = x.stride(1);
   a.n_rows = (int)x.size(0);
   a.n_cols = (int)n_cols;
   a.out = fp(out);
@@ -1486,6 +1529,10 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("set_tuning(str key, int value) -> int", &set_tuning);
   m.def("reset_held() -> int", &reset_held);
   m.def("device_reset() -> int", &device_reset);
+  m.def("pool_sample(Tensor(a!) pool, Tensor seg_off, Tensor mean, Tensor sd, int seed) -> ()");
+  m.def("row_center(Tensor(a!) x, Tensor(b!) shift) -> ()");
+  m.def("csr_rows(Tensor opt, Tensor width, int maxw, Tensor(a!) part, Tensor(b!) count, Tensor(c!) offset, "
+        "Tensor(d!) rows, int chunk) -> ()");
   m.def("gemm_bnpub_next(Tensor cnt, Tensor mean, Tensor invstd, Tensor rm, Tensor rv, float momentum, float eps) -> ()",
         &gemm_bnpub_next);
   m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "
@@ -1520,6 +1567,9 @@ TORCH_LIBRARY_IMPL(fedtgan, CUDA, m) {
   m.impl("vgm_estep", &vgm_estep);
   m.impl("kmeans_step", &kmeans_step);
   m.impl("vgm_fit", &vgm_fit);
+  m.impl("pool_sample", &pool_sample);
+  m.impl("row_center", &row_center);
+  m.impl("csr_rows", &csr_rows);
 }
 
 TORCH_LIBRARY_IMPL(fedtgan, CPU, m) { m.impl("write_csv", &write_csv); }

@@ -441,8 +441,9 @@ void launch_gen_weight_prep(const GenWeightPrep& a, hipStream_t stream);
 
 // VGM encode (kernels/vgm.hip): one thread per (row, column) cell of the label-encoded table
 struct VgmEncodeArgs {
-  const double* x;      // [n_rows, ldx] label codes / continuous values
+  const double* x;      // label codes / continuous values: x[r * ldx + j * ldc] (row- or column-major)
   int ldx, n_rows, n_cols;
+  int64_t ldc;
   float* out;           // [n_rows, ldo] encoded matrix (zero-filled by the caller)
   int ldo;
   int* opt;             // [n_rows, n_span] option index per conditional span
@@ -462,6 +463,35 @@ struct VgmEncodeArgs {
   uint32_t stream;
 };
 void launch_vgm_encode(const VgmEncodeArgs& a, hipStream_t stream);
+
+// init_ops.hip: the federator's pooled GMM sample (segment s = (column, client, component) covers pool elements
+// [seg_off[s], seg_off[s + 1]); element e = mean[s] + sd[s] * N(0, 1) keyed on (seed, e))
+struct PoolSampleArgs {
+  double* pool;
+  const int64_t* seg_off;   // [nseg + 1]
+  const double* mean;       // [nseg]
+  const double* sd;         // [nseg]
+  int nseg;
+  int64_t n;
+  uint64_t seed;
+};
+void launch_pool_sample(const PoolSampleArgs& a, hipStream_t stream);
+// init_ops.hip: rows of a contiguous fp64 x [rows, n] centred in place; shift[row] = the row's mean
+void launch_row_center(double* x, double* shift, int rows, int64_t n, hipStream_t stream);
+// init_ops.hip: CSR real-row lists of an option matrix opt [n, n_col] (row-major, ldo): rows[s * n + ...] holds,
+// for every span s and option o < width[s], the rows with that option in ascending order starting at offset[s, o];
+// count[s, o] their number (offset / count 0 on padding slots o >= width[s]).  part: [n_col, chunks, maxw] scratch.
+struct CsrArgs {
+  const int* opt;
+  int ldo;
+  const int* width;
+  int n, n_col, maxw, chunk, chunks;
+  int* part;
+  int64_t* count;
+  int64_t* offset;
+  int64_t* rows;
+};
+void launch_csr_rows(const CsrArgs& a, hipStream_t stream);
 
 // Batched 1-D DP-GMM fit passes (kernels/vgm_fit.hip)
 struct VgmFitArgs {

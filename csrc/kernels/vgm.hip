@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void vgm_encode_kernel(VgmEncodeArgs a) {
   const int64_t total = (int64_t)a.n_rows * a.n_cols;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / a.n_cols), j = (int)(e % a.n_cols);
-    const double xv = a.x[(size_t)r * a.ldx + j];
+    const double xv = a.x[(size_t)r * a.ldx + (size_t)j * a.ldc];
     float* row = a.out + (size_t)r * a.ldo;
     const int pos = a.col_pos[j], aux = a.col_aux[j], span = a.col_span[j];
     int opt;

@@ -98,7 +98,29 @@ def _tables(tr: VGMTransformer, device) -> Dict[str, torch.Tensor]:
 
 
 def row_index_on_device(opt: torch.Tensor, layout) -> tuple:
-    """CSR row lists per (span, option) + one-hot counts from the option matrix [N, n_col]."""
+    """CSR row lists per (span, option) + one-hot counts from the option matrix [N, n_col]: this library's
+    counting sort (csrc/kernels/init_ops.hip csr_rows; rows ascending in every list, deterministic) on a GPU,
+    the torch formulation below elsewhere (and as its test oracle)."""
+    n, n_col = opt.shape
+    maxw = int(layout.cond_width.max()) if layout.n_col else 0
+    if opt.is_cuda and n and n_col and maxw:
+        from ..ops import native
+        dev = opt.device
+        chunk = 4096
+        chunks = -(-n // chunk)
+        part = torch.empty(n_col * chunks * maxw, dtype=torch.int32, device=dev)
+        count = torch.empty(n_col, maxw, dtype=torch.int64, device=dev)
+        offset = torch.empty(n_col, maxw, dtype=torch.int64, device=dev)
+        rows = torch.empty(n_col * n, dtype=torch.int64, device=dev)
+        width = torch.as_tensor(np.asarray(layout.cond_width, dtype=np.int32), device=dev)
+        native.require().csr_rows(opt.contiguous(), width, maxw, part, count, offset, rows, chunk)
+        return ({"row_offset": offset, "row_count": count, "rows": rows},
+                count.cpu().numpy().astype(np.float64))
+    return row_index_torch(opt, layout)
+
+
+def row_index_torch(opt: torch.Tensor, layout) -> tuple:
+    """row_index_on_device as torch ops (argsort per span)."""
     n, n_col = opt.shape
     maxw = int(layout.cond_width.max()) if layout.n_col else 0
     o = opt.long()
@@ -123,19 +145,17 @@ def encode_on_device(tr: VGMTransformer, data: np.ndarray, device, seed: int = 0
         raise ValueError(f"expected a [rows, {len(tr.meta)}] table")
     # a column-major table (TablePreprocessor.encode) is uploaded as its [cols, rows] transpose and
     # turned row-major on the device: no host-side transposing copy of the (wide: 400 MB) matrix
+    if t["cat_cols"]:
+        # every code must index its LUT row (checked on the host, column by column: no ATen kernel)
+        for j, nc in zip(t["cat_cols"], t["cat_n"]):
+            v = data[:, j]
+            bad = ~np.isfinite(v) | (v < 0) | (v >= nc) | (v != np.floor(v))
+            if len(v) and bad.any():
+                raise ValueError(f"column {j}: category codes outside 0..{int(nc) - 1}")
     if data.flags.f_contiguous and not data.flags.c_contiguous:
-        x = torch.as_tensor(data.T, device=device).t().contiguous()
+        x = torch.as_tensor(data.T, device=device).t()     # read column-major by the kernel (ldc = rows)
     else:
         x = torch.as_tensor(np.ascontiguousarray(data), device=device)
-    if t["cat_cols"]:
-        # every code must index its LUT row (checked on the device: one host read of the verdict)
-        cc = torch.as_tensor(np.asarray(t["cat_cols"], dtype=np.int64), device=device)
-        nc = torch.as_tensor(np.asarray(t["cat_n"], dtype=np.float64), device=device)
-        v = x.index_select(1, cc)
-        bad = (~torch.isfinite(v)) | (v < 0) | (v >= nc) | (v != torch.floor(v))
-        if len(v) and bool(bad.any()):
-            j = int(cc[bad.any(0).nonzero()[0, 0]])
-            raise ValueError(f"column {j}: category codes outside 0..{int(t['cat_n'][t['cat_cols'].index(j)]) - 1}")
     n = x.shape[0]
     lay = tr.layout
     out = torch.zeros(n, lay.data_dim, dtype=torch.float32, device=device)

@@ -136,6 +136,19 @@ def sample_pool(banks: Sequence[VGMBank], n_per_client: Sequence[int], rng: np.r
     mean = np.stack([b.means for b in banks], axis=1)                      # [n_cont, K, nk]
     std = np.sqrt(np.stack([b.covariances for b in banks], axis=1))
     dev = torch.device(device) if device is not None else torch.device("cpu")
+    if dev.type == "cuda":
+        # one launch of this library's pool_sample kernel (csrc/kernels/init_ops.hip): segment (j, i, k) of the
+        # row-major pool is [seg_off[s], seg_off[s + 1]) -- the flattened counts' prefix sums, as row j holds every
+        # client's draws of column j back to back.  Its normals are Philox keyed on (seed, element), not torch's
+        # generator (no ATen kernel on the initialisation path)
+        from ..ops import native
+        seg_off = np.concatenate([[0], np.cumsum(counts.reshape(-1))]).astype(np.int64)
+        pool = torch.empty(n_cont, int(off[-1]), dtype=torch.float64, device=dev)
+        native.require().pool_sample(pool, torch.as_tensor(seg_off, device=dev),
+                                     torch.as_tensor(np.ascontiguousarray(mean.reshape(-1)), device=dev),
+                                     torch.as_tensor(np.ascontiguousarray(std.reshape(-1)), device=dev),
+                                     int(seed) & ((1 << 62) - 1))
+        return pool, off.tolist()
     seg = torch.arange(n_cont * len(banks) * nk, device=dev)
     idx = torch.repeat_interleave(seg, torch.as_tensor(counts.reshape(-1), device=dev),
                                   output_size=int(n_cont * off[-1]))

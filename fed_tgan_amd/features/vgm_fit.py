@@ -187,7 +187,34 @@ def _lower_bound(ent, s):
     return ent - log_wishart - log_norm_weight - 0.5 * torch.log(s.beta).sum(1)
 
 
-def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: float) -> VGMBank:
+def _fit_vgm_device_prep(columns, dev, seed, init_centers, max_iter: int, tol: float) -> VGMBank:
+    """The fused fit's inputs without ATen compute kernels: host columns are padded and centred with numpy and
+    uploaded once; a device matrix (the federator's pool, every entry live) is centred in place by this library's
+    row_center kernel."""
+    from ..ops import native
+    seed = int(seed) if seed is not None else int(np.random.SeedSequence().generate_state(1)[0] & 0x7FFFFFFF)
+    if isinstance(columns, torch.Tensor):
+        X = columns.to(device=dev, dtype=torch.float64).contiguous()
+        if X is columns:
+            X = X.clone()          # (centred in place)
+        shift = torch.empty(X.shape[0], dtype=torch.float64, device=dev)
+        native.require().row_center(X, shift)
+        n = torch.full((X.shape[0],), int(X.shape[1]), dtype=torch.int32).to(dev)
+        return _fit_vgm_device(X, n, shift, seed, init_centers, max_iter, tol)
+    n_rows = max(len(c) for c in columns)
+    Xh = np.zeros((len(columns), n_rows), dtype=np.float64)
+    cnt = np.zeros(len(columns), dtype=np.int64)
+    for j, c in enumerate(columns):
+        c = np.asarray(c, dtype=np.float64)
+        cnt[j] = len(c)
+        Xh[j, :len(c)] = c - c.sum() / max(len(c), 1)
+    shift_h = np.asarray([np.asarray(c, dtype=np.float64).sum() / max(len(c), 1) for c in columns])
+    X = torch.from_numpy(Xh).to(dev)
+    n = torch.from_numpy(cnt.astype(np.int32)).to(dev)
+    return _fit_vgm_device(X, n, torch.from_numpy(shift_h), seed, init_centers, max_iter, tol)
+
+
+def _fit_vgm_device(X, n, shift, seed: int, init_centers, max_iter: int, tol: float) -> VGMBank:
     """The whole fit as ONE launch of ``vgm_fit_kernel`` (csrc/kernels/vgm_fit.hip): one workgroup
     per column runs seeding, Lloyd and the EM loop with its M-step, lower bound and convergence test
     on the device."""
@@ -195,14 +222,13 @@ def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: fl
     L = native.require()
     nc = X.shape[0]
     dev = X.device
-    n = W.sum(1).to(torch.int32).contiguous()
     out = torch.empty(nc, 6, 10, dtype=torch.float64, device=dev)
     info = torch.empty(nc, 2, dtype=torch.int32, device=dev)
     lbs = torch.empty(nc, dtype=torch.float64, device=dev)
     ic = None
+    shift_h = shift.cpu().numpy()
     if init_centers is not None:
-        ic = (torch.as_tensor(np.asarray(init_centers, dtype=np.float64), device=dev)
-              - shift.unsqueeze(1)).contiguous()
+        ic = torch.as_tensor(np.asarray(init_centers, dtype=np.float64) - shift_h[:, None], device=dev).contiguous()
     args = (int(seed) & ((1 << 62) - 1), WEIGHT_PRIOR, float(tol), REG_COVAR, int(max_iter), 300)
     # the split fit's workgroups wait for each other (a grid sized to about one workgroup per CU): fits of
     # concurrent client threads (fed/local.py) are serialised process-wide, and each waits for its grid to
@@ -233,7 +259,7 @@ def _fit_vgm_device(X, W, shift, seed: int, init_centers, max_iter: int, tol: fl
     fit_vgm_torch.last_info = info_h
     fit_vgm_torch.last_refit_columns = dead
     fit_vgm_torch.last_lower_bound = lbs.cpu().numpy()
-    return VGMBank(wc_a=o[:, 0], wc_b=o[:, 1], mean_precision=o[:, 2], means=o[:, 3] + shift.cpu().numpy()[:, None],
+    return VGMBank(wc_a=o[:, 0], wc_b=o[:, 1], mean_precision=o[:, 2], means=o[:, 3] + shift_h[:, None],
                    dof=o[:, 4], covariances=o[:, 5])
 
 
@@ -245,6 +271,10 @@ def fit_vgm_torch(columns, n_clusters: int = 10, seed: int | None = None, device
     makes the fit follow sklearn's ``BayesianGaussianMixture`` from the same initialisation."""
     dev = torch.device(device) if device is not None else torch.device("cpu")
     dt = torch.float64
+    if use_hip is None:
+        use_hip = dev.type == "cuda" and n_clusters == 10
+    if use_hip and fused:
+        return _fit_vgm_device_prep(columns, dev, seed, init_centers, max_iter, tol)
     X, W = _pad(columns, dev, dt)
     gen = torch.Generator(device=dev)
     seed = int(seed) if seed is not None else int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
@@ -252,10 +282,6 @@ def fit_vgm_torch(columns, n_clusters: int = 10, seed: int | None = None, device
     counts = W.sum(1)
     shift = (X * W).sum(1) / counts                       # centre every column (prior mean 0)
     X = (X - shift.unsqueeze(1)) * W
-    if use_hip is None:
-        use_hip = dev.type == "cuda" and n_clusters == 10
-    if use_hip and fused:
-        return _fit_vgm_device(X, W, shift, seed, init_centers, max_iter, tol)
     passes = _HipPasses(X, W) if use_hip else _TorchPasses(X, W)
     pri = _State()
     pri.wprior = WEIGHT_PRIOR

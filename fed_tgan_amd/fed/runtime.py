@@ -157,9 +157,13 @@ def _log(cfg: FedConfig, rank: int, *msg):
 
 
 def _warm_device(device):
-    x = torch.arange(64, device=device, dtype=torch.int64).flip(0)
-    torch.where(x > 3, torch.argsort(x.view(8, 8), dim=0, stable=True).view(-1), x)
-    torch.sort(x.double()).values.cumsum(0)
+    """HIP context creation and the first load of this library's code objects (one tiny launch of ours) while
+    stage A's pandas work runs.  The initialisation path launches no ATen compute kernel any more (pooled GMM
+    sample, row index, code checks and centring are this library's kernels or host numpy), so none of torch's
+    code objects -- tens to hundreds of ms each on a box's first GPU process -- is loaded before round 0."""
+    from ..ops import native
+    ctr = torch.zeros(1, dtype=torch.int64, device=device)
+    native.require().rng_bump(ctr)
     torch.cuda.synchronize(device)
 
 
@@ -278,8 +282,8 @@ class FedRuntime:
         t0 = time.time()
         warm = None
         if self.device.type == "cuda":
-            # HIP context creation and the first loads of torch's sort / select code objects take
-            # ~0.3 s; they overlap the pandas work of stage A on a side thread
+            # HIP context creation and the first load of this library's code objects overlap the pandas work
+            # of stage A on a side thread
             warm = threading.Thread(target=_warm_device, args=(self.device,), daemon=True)
             warm.start()
         # ---- A. categorical meta

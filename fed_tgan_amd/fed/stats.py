@@ -79,6 +79,8 @@ def continuous_client_distances_device(pooled, offsets: Sequence[int]) -> np.nda
     k = len(offsets) - 1
     if pooled.shape[0] == 0:
         return np.zeros((k, 0))
+    if k == 1:      # one client: the pool IS its sample, W1 = 0 exactly (normalised: 0 as well)
+        return np.zeros((1, int(pooled.shape[0])))
     us = torch.sort(pooled, dim=1).values
     e = torch.stack([wasserstein_1d_rows(us, pooled[:, offsets[i]:offsets[i + 1]], u_sorted=True)
                      for i in range(k)])
