@@ -66,7 +66,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--phase-timer", default="events", choices=["events", "sync"],
                     help="phase timers: HIP events (no host sync) or stream-synchronised wall time")
     ap.add_argument("--native-rccl", action="store_true",
-                    help="the weight all-reduce through the native RCCL plane (csrc/comm) instead of torch.distributed")
+                    help="the weight all-reduce through the native RCCL plane (csrc/comm; the default)")
+    ap.add_argument("--torch-rccl", action="store_true",
+                    help="the weight all-reduce through torch.distributed's RCCL ProcessGroup instead")
     ap.add_argument("--force-dist", action="store_true",
                     help="build real process groups even for one rank (1 GPU: the aggregation runs as an "
                          "RCCL all-reduce on a one-rank communicator)")
@@ -186,6 +188,8 @@ def run_rank(args) -> None:
     rccl_dir = _rccl_log_setup() if (device.type == "cuda" and (world > 1 or args.force_dist)) else None
     if args.native_rccl:
         os.environ["FEDTGAN_NATIVE_RCCL"] = "1"
+    if args.torch_rccl:
+        os.environ["FEDTGAN_NATIVE_RCCL"] = "0"
     comm = Comm.from_env("auto", device, force_dist=args.force_dist)
     n_data = comm.data_world_size()
     if n_data != world:

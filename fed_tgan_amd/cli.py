@@ -97,7 +97,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="-local_clients K: the K clients as one batched launch sequence (on) or one engine and HIP "
                         "stream per client thread (off; what auto picks, see FedConfig.batched_clients)")
     p.add_argument("-native_rccl", action="store_true",
-                   help="the weight all-reduce through the native RCCL plane (csrc/comm) instead of torch.distributed")
+                   help="the weight all-reduce through the native RCCL plane (csrc/comm; the default, kept for "
+                        "compatibility)")
+    p.add_argument("-torch_rccl", action="store_true",
+                   help="the weight all-reduce through torch.distributed's RCCL ProcessGroup instead of the native plane")
     p.add_argument("-pipeline_sample", default="auto", choices=["auto", "on", "off"],
                    help="generate round r's table on a side stream after a model snapshot (FedConfig.pipeline_sample)")
     p.add_argument("-table_reader", default="auto", choices=["auto", "pandas", "arrow"],
@@ -215,7 +218,7 @@ def run_rank(rank: int, args, on_done=None) -> None:
         # (Comm.share_with_federator)
         data_backend = "auto_all" if args.mode == "mdgan" else "auto"
     comm = Comm(rank, world, client_ranks, data_backend, args.ip, args.port, timeout_s=args.timeout, device=device,
-                native_rccl=bool(args.native_rccl))
+                native_rccl=False if args.torch_rccl else (True if args.native_rccl else None))
     if not args.quiet:
         print(f"[rank {rank}] data plane {comm.data_backend} over client ranks {client_ranks}", flush=True)
     try:

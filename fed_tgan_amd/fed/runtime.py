@@ -133,6 +133,9 @@ class FedConfig:
     # HIP maps streams onto hardware queues round-robin in creation order, so a normal-priority side stream can
     # share the training stream's in-order queue (seen in a kernel trace: both on queue 1)
     gen_stream_priority: int = 0
+    # sample_round: gather the epoch table's shares even when one rank samples it all (a one-rank RCCL run then
+    # exercises the multi-rank data path -- the side-stream gather over the communicator -- on one GPU; tests)
+    force_gather: bool = False
     # after the last round the federator writes models/{name}_generator.pt (python -m dtds.sample)
     save_generator: bool = True
     # several clients on one GPU (in-process emulation): "on" runs their training steps as ONE batched launch
@@ -748,7 +751,7 @@ class FedRuntime:
         gen = (lambda k: self.engine.generate_decoded_split(k, self._gen_stream)) if pipe \
             else self.engine.generate_decoded
         on_gen = (lambda: torch.cuda.stream(self._gen_stream)) if pipe else contextlib.nullcontext
-        if len(samplers) == 1:
+        if len(samplers) == 1 and not self._force_gather(samplers):
             if self.rank in samplers:
                 with self._sub("generate"):
                     vals = gen(per[0])
@@ -794,6 +797,12 @@ class FedRuntime:
             if getattr(self, "comm", None) is not None:
                 self.comm.destroy()
 
+    def _force_gather(self, samplers) -> bool:
+        """FedConfig.force_gather applies: a real process group whose every client samples (co-located federator)."""
+        c = self.comm
+        return bool(self.cfg.force_gather) and c.dist_active and list(samplers) == list(c.client_ranks) and \
+            self.federator in c.client_ranks
+
     def _complete_handoff(self):
         """Issue the deferred part of the last pipelined sample_round: the generation body on the side stream,
         the gather to the federator, the pinned copy and the CSV writer hand-off."""
@@ -805,7 +814,7 @@ class FedRuntime:
         share = None
         with torch.cuda.stream(self._gen_stream):
             vals = self.engine.generation_body(k, self._gen_stream)
-            if len(samplers) == 1:
+            if len(samplers) == 1 and not self._force_gather(samplers):
                 share = self._host(vals)
             else:
                 rows = self.comm.gather_rows(vals, per, samplers, dst=self.federator, to_host=False)

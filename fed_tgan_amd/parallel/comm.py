@@ -51,8 +51,11 @@ class Comm:
         # buffer first (tools/premul_probe.py checks it against x * w on the box)
         self.premul_sum = True
         # the weight all-reduce through the native RCCL plane (parallel/rccl.py, csrc/comm) instead of
-        # torch.distributed's ProcessGroup (None: FEDTGAN_NATIVE_RCCL=1 in the environment)
-        self.native_rccl = (os.environ.get("FEDTGAN_NATIVE_RCCL", "0") == "1") if native_rccl is None else native_rccl
+        # torch.distributed's ProcessGroup.  None: on unless FEDTGAN_NATIVE_RCCL=0 -- the default since round 6: a
+        # one-rank RCCL round costs plain + 0.0-0.04 ms with it, + 0.1-0.3 ms through the ProcessGroup (whose
+        # all-reduce holds the next round's generation back, profiles/sync_r6.txt); bitwise the same aggregate and
+        # tables (tests/test_gpu_federation.py::test_gpu_one_rank_rccl_pipelined_gather_matches_unpipelined)
+        self.native_rccl = (os.environ.get("FEDTGAN_NATIVE_RCCL", "1") == "1") if native_rccl is None else native_rccl
         self._native = None
         # ``force_dist``: build real process groups even for one rank, so the collective branches
         # (RCCL all-reduce / gather / send-recv) execute on a single-GPU box instead of the
@@ -229,16 +232,27 @@ class Comm:
         nccl = self.data_backend == "nccl"
         width = t.shape[1]
         m = max(counts)
-        buf = torch.zeros(m, width, dtype=t.dtype, device=t.device if nccl else "cpu")
-        buf[:t.shape[0]] = t if nccl else t.cpu()
+        if nccl and t.shape[0] == m and t.is_contiguous():
+            buf = t                     # a full share: sent as it is (no padded copy, no fill)
+        else:
+            buf = torch.zeros(m, width, dtype=t.dtype, device=t.device if nccl else "cpu")
+            buf[:t.shape[0]] = t if nccl else t.cpu()
         group = self.data if nccl else self.ctrl
-        gl = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))] if self.rank == dst else None
+        nw = dist.get_world_size(group)
+        whole = gl = None
+        if self.rank == dst:
+            # the receive slots are views of ONE buffer: with equal shares in group order it already is the table
+            whole = torch.empty(nw, m, width, dtype=buf.dtype, device=buf.device)
+            gl = list(whole.unbind(0))
         dist.gather(buf, gl, dst=dst, group=group)
         if self.rank != dst:
             return None
         order = dist.get_process_group_ranks(group) if group is not dist.group.WORLD else list(range(self.world_size))
-        parts = {r: g for r, g in zip(order, gl)}
-        out = torch.cat([parts[r][:n] for r, n in zip(ranks, counts)])
+        if list(ranks) == list(order) and all(int(n) == m for n in counts):
+            out = whole.view(nw * m, width)
+        else:
+            parts = {r: g for r, g in zip(order, gl)}
+            out = torch.cat([parts[r][:n] for r, n in zip(ranks, counts)])
         return out.cpu() if to_host else out
 
     def weighted_all_reduce(self, flat: torch.Tensor, weight: float) -> torch.Tensor:

@@ -386,3 +386,55 @@ def test_gpu_two_ranks_pipelined_sampling_gathers_the_same_tables(tmp_path):
         assert recs[0]["flat"] == recs[1]["flat"]
         res[pipe] = [(out / "Intrusion_result" / f"Intrusion_synthesis_epoch_{e}.csv").read_bytes() for e in range(3)]
     assert res["0"] == res["1"]
+
+
+_ONE_RANK_RCCL_SCRIPT = r"""
+import json, sys, torch
+from fed_tgan_amd.data.schema import intrusion_spec
+from fed_tgan_amd.fed.runtime import FedConfig, FedRuntime
+from fed_tgan_amd.parallel.comm import Comm
+port, out, pipe, native = int(sys.argv[1]), sys.argv[2], sys.argv[3] == "1", sys.argv[4] == "1"
+dev = torch.device("cuda:0")
+torch.cuda.set_device(dev)
+comm = Comm(0, 1, [0], "auto", port=port, device=dev, force_dist=True, native_rccl=native)
+cfg = FedConfig(spec=intrusion_spec(), epochs=3, synthetic_rows=4000, out_dir=out, backend="hip", gmm_backend="torch",
+                verbose=False, pipeline_sample=pipe, force_gather=True)
+rt = FedRuntime(cfg, comm, dev)
+rt.initialize()
+rt.fit()
+torch.cuda.synchronize()
+print(json.dumps({"pipe": bool(getattr(rt, "_pipe", False)), "backend": comm.data_backend,
+                  "native": getattr(comm, "_native", None) is not None,
+                  "flat": float(rt.engine.flat.double().sum())}), flush=True)
+rt.close()
+"""
+
+
+def test_gpu_one_rank_rccl_pipelined_gather_matches_unpipelined(tmp_path):
+    """on a one-rank RCCL data plane (force_dist) with FedConfig.force_gather, every round's
+    table goes through Comm.gather_rows over the RCCL communicator -- on the generation side stream when sampling is
+    pipelined.  The epoch CSVs equal the unpipelined run's byte for byte, and the native RCCL plane for the weight
+    all-reduce gives the same model and tables as torch's."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    res = {}
+    for pipe, native in (("0", "0"), ("1", "0"), ("1", "1")):
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        out = tmp_path / f"p{pipe}n{native}"
+        p = subprocess.run([sys.executable, "-c", _ONE_RANK_RCCL_SCRIPT, str(port), str(out), pipe, native],
+                           capture_output=True, text=True, env=env, cwd=root, timeout=150)
+        assert p.returncode == 0, p.stderr[-3000:]
+        rec = json.loads(p.stdout.strip().splitlines()[-1])
+        assert rec["backend"] == "nccl" and rec["pipe"] == (pipe == "1") and rec["native"] == (native == "1")
+        res[(pipe, native)] = (rec["flat"], [(out / "Intrusion_result" / f"Intrusion_synthesis_epoch_{e}.csv").read_bytes()
+                                             for e in range(3)])
+    base = res[("0", "0")]
+    for key, val in res.items():
+        assert val[0] == base[0], key
+        assert val[1] == base[1], key
