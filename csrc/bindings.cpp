@@ -118,6 +118,13 @@ struct BnPubPending {
 };
 thread_local BnPubPending g_bnpub{};
 
+// The fused A-chain for the NEXT chain tail held by this thread (gemm_achain_next, launch.h GemmArgs::ach_*)
+struct AchPending {
+  Tensor out, ws, cnt;
+  bool active;
+};
+thread_local AchPending g_ach{};
+
 // drop every GEMM held by this thread (pairing, chain tail, Adam fusion) without launching it: called at
 // the start of every step and when a step raises between a hold and its consumer, so a stale held GEMM
 // (whose operand pointers may since have been freed) can never be launched or block the next step.
@@ -173,7 +180,8 @@ int64_t device_reset() {
 
 int64_t reset_held() {
   const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0) +
-                    (g_bnl.active ? 1 : 0) + (g_bnpub.active ? 1 : 0);
+                    (g_bnl.active ? 1 : 0) + (g_bnpub.active ? 1 : 0) + (g_ach.active ? 1 : 0);
+  g_ach = AchPending{};
   g_bnl.active = false;
   g_bnpub.active = false;
   has_held = false;
@@ -218,6 +226,19 @@ void gemm_bnpub_next(const Tensor& cnt, const Tensor& mean, const Tensor& invstd
   g_bnpub = BnPubPending{mean.data_ptr<float>(), invstd.data_ptr<float>(), rm.data_ptr<float>(), rv.data_ptr<float>(),
                          reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), w, cnt.numel(), (float)momentum, (float)eps,
                          true};
+}
+
+// The next chain tail (gemm(..., group=4) with a head seed head_a = A1 [M, N1], weights W1 [N1, K1]) also forms
+// out [M, K1] = (A1 W1) . MS0 in the chain launch, MS0 = the chain head's mask; ws = fp32 scratch of at least
+// ceil(N1 / 64) * M * K1 elements, cnt = int32 counters, at least one per head row, all zero (kept zero by the kernel).
+void gemm_achain_next(const Tensor& out, const Tensor& ws, const Tensor& cnt) {
+  TORCH_CHECK(!g_ach.active, "gemm_achain_next: already pending");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.dim() == 2 && out.stride(1) == 1,
+              "gemm_achain_next: out fp32 [M, K] rows");
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous(), "gemm_achain_next: ws fp32");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous(), "gemm_achain_next: cnt int32");
+  TORCH_CHECK(fedtgan::client_batch().k == 1, "gemm_achain_next: one client");
+  g_ach = AchPending{out, ws, cnt, true};
 }
 
 void gemm_bnl_next(const std::vector<optional<Tensor>>& part, const std::vector<Tensor>& mean,
@@ -466,9 +487,21 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
                 "gemm: a chain tail is C = A B^T with fp32 16-B aligned B rows (ld % 4 == 0), K <= 1024, K % 16 == 0, "
                 "no one-hot block / BN partials");
     g.splitk = 1;
+    if (g_ach.active) {
+      AchPending q = g_ach;
+      g_ach = AchPending{};
+      TORCH_CHECK(g.head_a && epi == fedtgan::EPI_LRELU_DROPOUT, "gemm: the fused A-chain needs a tail with a head seed");
+      TORCH_CHECK(q.out.size(0) == M && q.out.size(1) == K && q.ws.numel() >= ((N + 63) / 64) * M * K && q.cnt.numel() >= M,
+                  "gemm: fused A-chain out [M, K] / ws [ceil(N / 64), M, K] / cnt [M]");
+      g.ach_out = q.out.data_ptr<float>();
+      g.ld_ach = (int)q.out.stride(0);
+      g.ach_ws = q.ws.data_ptr<float>();
+      g.ach_cnt = reinterpret_cast<unsigned*>(q.cnt.data_ptr<int>());
+    }
     g_chain_tail = ChainTail{g, a.data_ptr(), (int64_t)M, (int64_t)K, true};
     return;
   }
+  TORCH_CHECK(!g_ach.active, "gemm: gemm_achain_next is pending but this GEMM is no chain tail");
   if (chain) {
     TORCH_CHECK(g_chain_tail.active && group != 1, "gemm: chain=True needs a tail held with group=4 (and no group 1)");
     const ChainTail& t = g_chain_tail;
@@ -1533,6 +1566,7 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("row_center(Tensor(a!) x, Tensor(b!) shift) -> ()");
   m.def("csr_rows(Tensor opt, Tensor width, int maxw, Tensor(a!) part, Tensor(b!) count, Tensor(c!) offset, "
         "Tensor(d!) rows, int chunk) -> ()");
+  m.def("gemm_achain_next(Tensor out, Tensor ws, Tensor cnt) -> ()", &gemm_achain_next);
   m.def("gemm_bnpub_next(Tensor cnt, Tensor mean, Tensor invstd, Tensor rm, Tensor rv, float momentum, float eps) -> ()",
         &gemm_bnpub_next);
   m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "

@@ -1436,9 +1436,15 @@ int g_chain_rows = 2;        // 2: a grid too large for the prefetch runs two he
 // PRE: the tail's weights are prefetched (K = 256; host: grids that stay resident at the larger register count).
 // ROWS (PRE only): head rows per workgroup -- 2 halves the workgroups and the tail-weight traffic of a grid that
 // would not stay resident with one row each (the 150-row D phase).
-template <int SMAX, bool MASK = false, bool BT_ = false, bool PRE = false, int ROWS = 1>
+// ACH: the tail also forms the head's backward link A0 = (A1 W1) . MS0 (GemmArgs::ach_*; one client, per-row
+// weights rows, no coalesced variant): A1 = the tail's head seed is in registers of the kq == 0 threads right
+// after the tail's epilogue, the W1 rows of the workgroup's 64-column slab are the ones it just multiplied, so
+// each workgroup adds a [ROWS, 64] x [64, K] partial and the row group's last arriver sums the nb partials --
+// the separate A-chain GEMM launch after the chain is gone.
+template <int SMAX, bool MASK = false, bool BT_ = false, bool PRE = false, int ROWS = 1, bool ACH = false>
 __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArgs t) {
   static_assert(ROWS == 1 || PRE, "two rows per workgroup only with the prefetched tail");
+  static_assert(!ACH || (!MASK && !BT_), "the fused A-chain takes the D-head chain of one client");
   const BIdx bi_ = batch_bidx<BT_>(g.xcd_cl);
   __shared__ __attribute__((aligned(16))) float row[ROWS][CH_MAXK];
   __shared__ float part[ROWS][4][CH_COLS];
@@ -1482,7 +1488,7 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
   __syncthreads();
   const int jl = threadIdx.x & (CH_COLS - 1), kq = threadIdx.x >> 6;
   const int j = s * CH_COLS + jl;
-  if (!PRE && t.chain_co) {
+  if (!PRE && !ACH && t.chain_co) {
     // wave kq owns 16 of the block's 64 output columns; for each, the 64 lanes read the column's weight row as
     // consecutive float4 (one coalesced 1 KB request per 256 K values, instead of 64 rows 1 KB apart per
     // request) and a wave sum finishes the dot product
@@ -1563,6 +1569,61 @@ __global__ __launch_bounds__(256) void chain_epilogue_kernel(GemmArgs g, GemmArg
       if (t.bias) v += t.bias[j];
       if constexpr (MASK) t.c[(size_t)m * t.ldc + j] = v * t.ms[(size_t)m * t.ldms + j];
       else t.c[(size_t)m * t.ldc + j] = apply_epi(t, v, m, j, st, (uint64_t)m * t.N + j);
+    }
+  }
+  if constexpr (ACH) {
+    __shared__ float a1s[ROWS][CH_COLS];
+    __shared__ unsigned ach_last;
+    if (kq == 0) {
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) {
+        const int m = m0 + r;   // the seed this thread's apply_epi just stored (same-thread read-back)
+        a1s[r][jl] = (j < t.N && (ROWS == 1 || m < g.M)) ? t.head_a[(size_t)m * t.ldha + j] : 0.f;
+      }
+    }
+    __syncthreads();
+    const int jn = min(CH_COLS, t.N - s * CH_COLS);
+    for (int i = threadIdx.x; i < g.N; i += blockDim.x) {
+      float acc[ROWS];
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+      const float* wc = t.b + (size_t)s * CH_COLS * t.ldb + i;   // W1[64 s + c, i]: coalesced over i
+      for (int c = 0; c < jn; ++c) {
+        const float w = wc[(size_t)c * t.ldb];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(a1s[r][c], w, acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) {
+        const int m = m0 + r;
+        if (ROWS == 1 || m < g.M)
+          __hip_atomic_store(&t.ach_ws[((size_t)s * g.M + m) * g.N + i], acc[r], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(&t.ach_cnt[bi_.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned last = tk == gridDim.y - 1 ? 1u : 0u;
+      if (last) __hip_atomic_store(&t.ach_cnt[bi_.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ach_last = last;
+    }
+    __syncthreads();
+    if (ach_last == 0u) return;
+    // the slabs in order (the same bits every run); MS0[m, i] was stored by this thread (SMAX > 0: its row loop
+    // above covers column i) or by an earlier launch
+    for (int i = threadIdx.x; i < g.N; i += blockDim.x) {
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) {
+        const int m = m0 + r;
+        if (ROWS > 1 && m >= g.M) break;
+        float sum = 0.f;
+        for (int q = 0; q < (int)gridDim.y; ++q)
+          sum += __hip_atomic_load(&t.ach_ws[((size_t)q * g.M + m) * g.N + i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        t.ach_out[(size_t)m * t.ld_ach + i] = sum * g.ms[(size_t)m * g.ldms + i];
+      }
     }
   }
 }
@@ -1744,7 +1805,7 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     t.nclient = g.nclient;
     // float4 loads from t.b + jc * t.ldb + k: the row stride and the base must keep them 16-B aligned
     t.chain_co = g_chain_coalesced && (g.N % 4 == 0) && (t.ldb % 4 == 0) &&
-                 ((reinterpret_cast<uintptr_t>(t.b) & 15) == 0);
+                 ((reinterpret_cast<uintptr_t>(t.b) & 15) == 0) && !t.ach_out;
     const int nb = (t.N + CH_COLS - 1) / CH_COLS;
     const bool mk = g.epi == EPI_MASK && t.epi == EPI_MASK && t.head_a == nullptr && t.bias == nullptr && t.alpha == 1.f;
     // prefetched tail weights (K = 256) where the grid stays resident at 194 VGPRs (<= 512 workgroups): one row
@@ -1761,17 +1822,27 @@ static void gemm_epilogue_launch(const GemmArgs& g, hipStream_t stream) {
     else if (pre) hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, false, true>), grid, block, 0, stream, h, t);     \
     else hipLaunchKernelGGL((chain_epilogue_kernel<S, MK, false>), grid, block, 0, stream, h, t);                    \
   } while (0)
+#define FEDTGAN_CHAIN_ACH(S)                                                                                         \
+  do {                                                                                                               \
+    if (rows == 2) hipLaunchKernelGGL((chain_epilogue_kernel<S, false, false, true, 2, true>), grid, block, 0, stream, h, t); \
+    else if (pre) hipLaunchKernelGGL((chain_epilogue_kernel<S, false, false, true, 1, true>), grid, block, 0, stream, h, t); \
+    else hipLaunchKernelGGL((chain_epilogue_kernel<S, false, false, false, 1, true>), grid, block, 0, stream, h, t);       \
+  } while (0)
 #define FEDTGAN_CHAIN(S)              \
   do {                                \
-    if (mk) FEDTGAN_CHAIN_K(S, true);  \
+    if (t.ach_out) FEDTGAN_CHAIN_ACH(S); \
+    else if (mk) FEDTGAN_CHAIN_K(S, true);  \
     else FEDTGAN_CHAIN_K(S, false);    \
   } while (0)
+    if (t.ach_out && (g.nclient > 1 || g.xcd_cl || !t.head_a || mk))
+      throw std::runtime_error("gemm: the fused A-chain needs one client and a chain tail with a head seed");
     if (g.splitk <= 1 || g.red_inl) FEDTGAN_CHAIN(0);
     else if (g.splitk <= 8) FEDTGAN_CHAIN(8);
     else if (g.splitk <= 16) FEDTGAN_CHAIN(16);
     else if (g.splitk <= 32) FEDTGAN_CHAIN(32);
     else FEDTGAN_CHAIN(64);
 #undef FEDTGAN_CHAIN
+#undef FEDTGAN_CHAIN_ACH
 #undef FEDTGAN_CHAIN_K
     return;
   }

@@ -153,6 +153,14 @@ struct GemmArgs {
   int nclient;
   int xcd_cl;   // ClientBatch::xcd
   int chain_co;   // chained tail (chain_epilogue_kernel): lane-contiguous weight rows + wave sums (g_chain_coalesced)
+  // chained tail with a head seed (head_a = A1) only, nullable: the backward link A0 = (A1 W1) . MS0 formed in the
+  // same launch (gemm_achain_next): each (row group, 64-column slab) workgroup stores its slab's partial product
+  // A1[:, slab] W1[slab, :] into ach_ws [slabs, M, K] write-through and takes a ticket on ach_cnt[row group] (zero
+  // between launches); the row group's last workgroup sums the slabs in order and applies the head's mask MS0
+  float* ach_out;
+  float* ach_ws;
+  unsigned* ach_cnt;
+  int ld_ach;
 };
 
 void launch_gemm(GemmArgs g, hipStream_t stream);

@@ -290,7 +290,8 @@ def read_csv_table(path: str, reader: str = "auto") -> pd.DataFrame:
     8-CPU host).  Files with date / time columns or duplicate names (which pandas parses or renames its own
     way) fall back to pandas.  "auto" is pandas: arrow's float parser rounds correctly and pandas' default one
     does not, so the two disagree in the last ulp of ~15-45 % of random doubles (measured on a 400k-row table;
-    tests/test_data.py::test_auto_reader_is_pandas_bitwise) and the VGM fits / encodings would differ from the reference's load path.
+    tests/test_data.py::test_auto_reader_is_pandas_bitwise) and the VGM fits / encodings would differ from the
+    reference's load path.
     Arrow stays an explicit opt-in (``-table_reader arrow``) for tables where that does not matter."""
     if reader == "auto":
         reader = "pandas"

@@ -120,6 +120,12 @@ class EngineConfig:
     # HIP, two hidden D layers: the second layer's forward is computed row by row in the first layer's
     # split-K reduction launch (chain_epilogue_kernel)
     chain_d1: bool = True
+    # HIP, with chain_d1 on one client: the backward link A0 = (A1 W1) . MS0 is formed in the same chain launch
+    # (each workgroup's 64-column slab of A1 times the W1 rows it just used, slabs summed by the row group's last
+    # workgroup) instead of an A-chain GEMM launch after it.  A/B knob, default off: measured 191.0-192.1 us/step
+    # with it vs 188.6-192.4 without (two fewer launches, but every chain workgroup re-reads its 64 W1 rows and
+    # the row group's last one sums the slabs serially; profiles/achain_r6.txt)
+    fuse_achain: bool = False
     # HIP, where fuse_d_adam does not apply (the batched multi-client step): D0's weight gradient -- the
     # largest gradient, 256 x 10 Din -- is held for the D Adam launch instead of sharing a launch with R0, so
     # it is never written and re-read through HBM (gemm_adam_kernel's tiles update it in place).  A/B knob,
@@ -517,6 +523,14 @@ class CTGANEngine:
         self.dl = [z(3 * nP, h) for h in self.ddims]
         self.ms = [z(3 * nP, h) for h in self.ddims]
         self.A = [z(3 * nP, h) for h in self.ddims]
+        # fused A-chain scratch (EngineConfig.fuse_achain), one set per call site (the D phase, stream base 4, and the
+        # G phase, 14): slab partials [ceil(d1 / 64), rows, d0] and one arrival counter per head row (kept zero by
+        # the kernel)
+        self._ach = {}
+        if len(self.ddims) == 2 and self.cfg.fuse_achain and getattr(self.ops, "achain_capable", False):
+            for sb in (4, 14):
+                self._ach[sb] = (z(-(-self.ddims[1] // 64) * 3 * nP * self.ddims[0]),
+                                 self.mem.zeros(3 * nP, dtype=torch.int32))
         self.y = z(3 * nP)
         self.gbuf = z(nP, self.K1)
         inv = 1.0 / nP
@@ -757,10 +771,11 @@ class CTGANEngine:
             o.linear_activate(x, W, p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
                               slerp=slerp, onehot=oh, tile=min(tile, 64), splitk=1)
 
-    def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None):
+    def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None) -> bool:
         """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
         writes the head's backward seed A_{L-1} = coef * v * MS_{L-1} (no separate head launch;
-        the head's WGAN value is folded into a later column-sum launch, see _wgan_job)."""
+        the head's WGAN value is folded into a later column-sum launch, see _wgan_job).
+        Returns True when the A chain (A_0) was formed too (EngineConfig.fuse_achain)."""
         o = self.ops
         Xs = self.X if X is None else X
         inp = Xs[rows]
@@ -771,6 +786,7 @@ class CTGANEngine:
         chain = L == 2 and self.cfg.chain_d1 and hasattr(o, "gemm_is_split") and self.ddims[0] % 16 == 0 and \
             self.ddims[0] <= 1024 and o.gemm_is_split(inp.shape[0], self.ddims[0], inp.shape[1]) and \
             getattr(o, "batch_k", 1) == 1
+        fused = False
         for i in range(L):
             head = None
             if coef is not None and i == L - 1:
@@ -778,6 +794,10 @@ class CTGANEngine:
             kw = {"chain": True} if (chain and i == 0) else {}
             if chain and i == 0:
                 h1 = (coef, self.p["D.out.W"].view(-1), self.A[1][rows]) if coef is not None else None
+                ach = self._ach.get(stream_base) if coef is not None else None
+                if ach is not None:
+                    o.gemm_achain_next(self.A[0][rows], *ach)
+                    fused = True
                 o.gemm(self.dl[0][rows], self.p["D.1.W"], self.dl[1][rows], tb=True, bias=self.p["D.1.b"],
                        epi=EPI_LRELU_DROPOUT, ms=self.ms[1][rows], slope=self.cfg.lrelu_slope,
                        p_drop=self.cfg.dropout_p, stream_id=stream_base + 1, head=h1, group=4)
@@ -787,6 +807,7 @@ class CTGANEngine:
             if chain:
                 break
             inp = self.dl[i][rows]
+        return fused
 
     def _g_loss_metric(self):
         """The G-phase WGAN value alone (split roles: the client has no generator backward)."""
@@ -871,8 +892,8 @@ class CTGANEngine:
         L = len(self.ddims)
         allr = slice(0, 3 * nP)
         I = self.rows_i
-        self._d_forward(allr, stream_base=4, coef=self.coef3)
-        self._a_chain(allr)
+        if not self._d_forward(allr, stream_base=4, coef=self.coef3):
+            self._a_chain(allr)
         # gradient penalty: g = q_0 V_0 ; Gs written over the interpolates' input rows
         o.gemm(self.A[0][I], self.p["D.0.W"], self.gbuf)
         o.gp_scale(self.gbuf, self.X[I], self.cfg.gp_lambda, self.pen_rows)
@@ -959,8 +980,8 @@ class CTGANEngine:
         o, B, nP = self.ops, self.B, self.nP
         L = len(self.ddims)
         fk = slice(0, nP)
-        self._d_forward(fk, stream_base=14, X=self.XgP, coef=self.coefg)
-        self._a_chain(fk)
+        if not self._d_forward(fk, stream_base=14, X=self.XgP, coef=self.coefg):
+            self._a_chain(fk)
         o.gemm(self.A[0][fk], self.p["D.0.W"], self.gbuf)            # d(-mean D)/dX, packed
         dx = self.gbuf.view(B, self.Din)
         o.act_bwd_ce(dx[:, :self.Dd], self.Xg[:, :self.Dd], self.logits, self.spans, self.cond_spans, self.col,

@@ -114,6 +114,7 @@ class HipOps:
     bn_publish_capable = True    # EngineConfig.bn_fold_publish (gemm_bnpub_next)
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
     gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
+    achain_capable = True        # EngineConfig.fuse_achain (gemm_achain_next)
 
     def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
         self.L = native.require()
@@ -328,6 +329,11 @@ class HipOps:
         """The next gemm() with bn_part also publishes the final BatchNorm statistics from its last workgroup per
         column tile (csrc/kernels/launch.h GemmArgs::bnf_*, EngineConfig.bn_fold_publish)."""
         self.L.gemm_bnpub_next(cnt, mean, invstd, rm, rv, float(momentum), float(eps))
+
+    def gemm_achain_next(self, out, ws, cnt):
+        """The next chain tail (gemm(..., group=4) with a head seed) also forms the head's backward link
+        out = (A1 W1) . MS0 in the chain launch (csrc/kernels/launch.h GemmArgs::ach_*, EngineConfig.fuse_achain)."""
+        self.L.gemm_achain_next(out, ws, cnt)
 
     def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
         """The next gemm() stages relu(BatchNorm(a)) for the given column ranges of its A operand (see

@@ -605,3 +605,26 @@ def test_bn_pair_matches_unpaired():
         out.append((eng.flat.clone(), eng.gradG.clone()))
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_fused_achain_matches_gemm_chain():
+    """EngineConfig.fuse_achain (A0 = (A1 W1) . MS0 formed in D0's chain launch from per-slab partials,
+    csrc/kernels/gemm.hip chain_epilogue_kernel<..., ACH>) gives the D and G updates of the separate A-chain GEMM
+    (fp32: to summation order), and is deterministic (slabs summed in a fixed order)."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    out = []
+    for fa in (False, True, True):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision="fp32", fuse_achain=fa), DEV,
+                          backend="hip", seed=5)
+        assert bool(eng._ach) == fa
+        eng.set_training_data(X)
+        eng.train_steps(3, use_graph=False)
+        torch.cuda.synchronize()
+        out.append((eng.flat.clone(), eng.gradD.clone(), eng.gradG.clone(), eng.A[0].clone()))
+    for k in range(4):
+        torch.testing.assert_close(out[1][k], out[0][k], rtol=1e-4, atol=1e-5 if k == 0 else 1e-6)
+        assert torch.equal(out[1][k], out[2][k]), k

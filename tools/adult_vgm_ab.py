@@ -84,7 +84,8 @@ def main():
             res = [stat_sim_normalize(train_path, os.path.join(res_dir, f"{spec.name}_synthesis_epoch_{ep}.csv"),
                                       list(spec.categorical_list)) for ep in range(args.epochs)]
             tr = rt.transformer
-            r = {"variant": var + args.tag, "seed": seed, "backend": args.backend, "precision": args.precision, "avg_jsd": [float(x[0]) for x in res],
+            r = {"variant": var + args.tag, "seed": seed, "backend": args.backend, "precision": args.precision,
+                 "avg_jsd": [float(x[0]) for x in res],
                  "avg_wd": [float(x[1]) for x in res], "fits_modes": list(fits),
                  "global_modes": [int(c.sum()) for c in tr.components], "n_opt": int(tr.layout.n_opt),
                  "global_weights": np.round(tr.bank.weights, 4).tolist(),
