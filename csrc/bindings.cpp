@@ -6,6 +6,7 @@
 #include <torch/library.h>
 
 #include <cstring>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -81,6 +82,9 @@ struct AdamHeld {
   bool active;
 };
 thread_local AdamHeld g_adam_held{};
+// a short-K weight gradient held for the next adam_cs launch (gemm(..., group=6)): launched just before it, with
+// Adam in its own epilogue (launch_gemm_shortk_adam), its range cut out of the optimizer launch
+thread_local AdamHeld g_adam_pre{};
 // a chain tail (gemm(..., group=4)) waiting for its head (gemm(..., chain=True)); the head's launch copies
 // the tail's arguments by value when it enqueues the reduction kernel
 struct ChainTail {
@@ -91,32 +95,6 @@ struct ChainTail {
 };
 thread_local ChainTail g_chain_tail{};
 thread_local fedtgan::GemmArgs g_chain_args{};
-
-// BatchNorm on load for the NEXT gemm() call of this thread (gemm_bnl_next): the ranges of op(A) that hold a
-// layer's pre-BatchNorm output, their statistics' source and where the consumer materialises relu(BN(a))
-struct BnlPending {
-  fedtgan::GemmArgs::BnLoad r[2];
-  int n, rpg;
-  float mom, eps;
-  float* out;
-  int ldo;
-  int64_t out_rows, out_cols;
-  int64_t nhat_rows[2];
-  int64_t part_numel[2];
-  bool active;
-};
-thread_local BnlPending g_bnl{};
-
-// Published BatchNorm statistics for the NEXT gemm() with bn_part of this thread (gemm_bnpub_next, launch.h
-// GemmArgs::bnf_*): the producing GEMM's last workgroup per column tile writes mean / invstd and the running stats
-struct BnPubPending {
-  float *mean, *invstd, *rm, *rv;
-  unsigned* cnt;
-  int64_t width, cnt_numel;
-  float mom, eps;
-  bool active;
-};
-thread_local BnPubPending g_bnpub{};
 
 // The fused A-chain for the NEXT chain tail held by this thread (gemm_achain_next, launch.h GemmArgs::ach_*)
 struct AchPending {
@@ -179,14 +157,14 @@ int64_t device_reset() {
 }
 
 int64_t reset_held() {
-  const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_chain_tail.active ? 1 : 0) +
-                    (g_bnl.active ? 1 : 0) + (g_bnpub.active ? 1 : 0) + (g_ach.active ? 1 : 0);
+  const int64_t n = (has_held ? 1 : 0) + (g_adam_held.active ? 1 : 0) + (g_adam_pre.active ? 1 : 0) +
+                    (g_chain_tail.active ? 1 : 0) +
+                    (g_ach.active ? 1 : 0);
   g_ach = AchPending{};
-  g_bnl.active = false;
-  g_bnpub.active = false;
   has_held = false;
   held_stream = nullptr;
   g_adam_held.active = false;
+  g_adam_pre.active = false;
   g_chain_tail.active = false;
   return n;
 }
@@ -209,25 +187,6 @@ int64_t set_client_batch(int64_t k, int64_t stride, int64_t seed_step, int64_t b
   return prev;
 }
 
-// The next gemm() of this thread stages relu(BatchNorm(a)) for op(A) columns [k0[j], k0[j] + width_j) (see
-// launch.h GemmArgs::bnl): part[j] = the producing GEMM's partials (None: mean / invstd are final), ptm[j] its
-// rows per tile; mean / invstd [2, width] (written by the consumer from partials); out (nullable): materialise
-// relu(BN(a)) (raw outside the ranges) as [M, K] rows, with nhat[j] [M, width_j] alongside.
-// The next gemm() with bn_part publishes its BatchNorm statistics (GemmArgs::bnf_*): mean / invstd [2, N], the
-// running statistics [N] (advanced batch after batch) and cnt (int32, one zeroed counter per column tile).
-void gemm_bnpub_next(const Tensor& cnt, const Tensor& mean, const Tensor& invstd, const Tensor& rm, const Tensor& rv,
-                     double momentum, double eps) {
-  TORCH_CHECK(!g_bnpub.active, "gemm_bnpub_next: already pending");
-  const int64_t w = rm.numel();
-  for (const Tensor* t : {&mean, &invstd, &rm, &rv})
-    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "gemm_bnpub_next: fp32 contiguous");
-  TORCH_CHECK(mean.numel() >= 2 * w && invstd.numel() >= 2 * w && rv.numel() == w, "gemm_bnpub_next: mean / invstd [2, N]");
-  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous(), "gemm_bnpub_next: cnt int32");
-  g_bnpub = BnPubPending{mean.data_ptr<float>(), invstd.data_ptr<float>(), rm.data_ptr<float>(), rv.data_ptr<float>(),
-                         reinterpret_cast<unsigned*>(cnt.data_ptr<int>()), w, cnt.numel(), (float)momentum, (float)eps,
-                         true};
-}
-
 // The next chain tail (gemm(..., group=4) with a head seed head_a = A1 [M, N1], weights W1 [N1, K1]) also forms
 // out [M, K1] = (A1 W1) . MS0 in the chain launch, MS0 = the chain head's mask; ws = fp32 scratch of at least
 // ceil(N1 / 64) * M * K1 elements, cnt = int32 counters, at least one per head row, all zero (kept zero by the kernel).
@@ -239,75 +198,6 @@ void gemm_achain_next(const Tensor& out, const Tensor& ws, const Tensor& cnt) {
   TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kInt && cnt.is_contiguous(), "gemm_achain_next: cnt int32");
   TORCH_CHECK(fedtgan::client_batch().k == 1, "gemm_achain_next: one client");
   g_ach = AchPending{out, ws, cnt, true};
-}
-
-void gemm_bnl_next(const std::vector<optional<Tensor>>& part, const std::vector<Tensor>& mean,
-                   const std::vector<Tensor>& invstd, const std::vector<Tensor>& gamma, const std::vector<Tensor>& beta,
-                   const std::vector<Tensor>& rm, const std::vector<Tensor>& rv, const std::vector<optional<Tensor>>& nhat,
-                   const std::vector<int64_t>& k0, const std::vector<int64_t>& ptm, int64_t rpg, double momentum,
-                   double eps, const optional<Tensor>& out) {
-  const size_t n = k0.size();
-  TORCH_CHECK(n >= 1 && n <= 2 && part.size() == n && mean.size() == n && invstd.size() == n && gamma.size() == n &&
-                  beta.size() == n && rm.size() == n && rv.size() == n && nhat.size() == n && ptm.size() == n,
-              "gemm_bnl_next: one entry per range (1 or 2 ranges)");
-  TORCH_CHECK(!g_bnl.active, "gemm_bnl_next: a BatchNorm-on-load configuration is already pending");
-  BnlPending p{};
-  p.n = (int)n;
-  p.rpg = (int)rpg;
-  p.mom = (float)momentum;
-  p.eps = (float)eps;
-  for (size_t j = 0; j < n; ++j) {
-    fedtgan::GemmArgs::BnLoad& r = p.r[j];
-    const int64_t w = gamma[j].numel();
-    TORCH_CHECK(w >= 4 && w <= 256 && w % 4 == 0 && k0[j] >= 0 && k0[j] % 4 == 0, "gemm_bnl_next: width 4..256, multiple of 4; k0 % 4 == 0");
-    for (const Tensor* t : {&mean[j], &invstd[j]})
-      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() >= 2 * w,
-                  "gemm_bnl_next: mean / invstd [2, width] fp32");
-    for (const Tensor* t : {&gamma[j], &beta[j], &rm[j], &rv[j]})
-      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == w,
-                  "gemm_bnl_next: gamma / beta / running stats [width] fp32");
-    r.part = nullptr;
-    p.part_numel[j] = 0;
-    if (part[j].has_value() && part[j]->defined()) {
-      TORCH_CHECK(part[j]->is_cuda() && part[j]->scalar_type() == at::kFloat && part[j]->is_contiguous() && ptm[j] >= 1,
-                  "gemm_bnl_next: partials");
-      r.part = part[j]->data_ptr<float>();
-      p.part_numel[j] = part[j]->numel();
-    }
-    r.mean = mean[j].data_ptr<float>();
-    r.invstd = invstd[j].data_ptr<float>();
-    r.gamma = gamma[j].data_ptr<float>();
-    r.beta = beta[j].data_ptr<float>();
-    r.rm = rm[j].data_ptr<float>();
-    r.rv = rv[j].data_ptr<float>();
-    r.k0 = (int)k0[j];
-    r.width = (int)w;
-    r.ptm = (int)ptm[j];
-    r.nhat = nullptr;
-    p.nhat_rows[j] = 0;
-    if (nhat[j].has_value() && nhat[j]->defined()) {
-      check_f32_2d(*nhat[j], "nhat");
-      TORCH_CHECK(nhat[j]->size(1) == w && ld_of(*nhat[j]) % 4 == 0 &&
-                      (reinterpret_cast<uintptr_t>(nhat[j]->data_ptr()) & 15) == 0,
-                  "gemm_bnl_next: nhat [M, width], 16-B aligned rows");
-      r.nhat = nhat[j]->data_ptr<float>();
-      r.ldn = ld_of(*nhat[j]);
-      p.nhat_rows[j] = nhat[j]->size(0);
-    }
-  }
-  p.out = nullptr;
-  if (out.has_value() && out->defined()) {
-    check_f32_2d(*out, "out");
-    TORCH_CHECK(ld_of(*out) % 4 == 0 && (reinterpret_cast<uintptr_t>(out->data_ptr()) & 15) == 0,
-                "gemm_bnl_next: out rows 16-B aligned");
-    for (size_t j = 0; j < n; ++j) TORCH_CHECK(p.r[j].nhat, "gemm_bnl_next: materialising needs nhat for every range");
-    p.out = out->data_ptr<float>();
-    p.ldo = ld_of(*out);
-    p.out_rows = out->size(0);
-    p.out_cols = out->size(1);
-  }
-  p.active = true;
-  g_bnl = p;
 }
 
 void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, double alpha, double beta,
@@ -430,45 +320,6 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
     TORCH_CHECK(bn_rpg >= 1 && bn_rpg <= M, "gemm: bn_rpg");
     g.bn_part = fp(*bn_part);
     g.bn_rpg = (int)bn_rpg;
-    if (g_bnpub.active) {
-      BnPubPending& q = g_bnpub;
-      q.active = false;
-      TORCH_CHECK(q.width == N && q.cnt_numel >= (N + tile - 1) / tile && fedtgan::client_batch().k == 1,
-                  "gemm: published BatchNorm statistics need [2, N] mean / invstd, one counter per column tile, one client");
-      g.bnf_mean = q.mean;
-      g.bnf_invstd = q.invstd;
-      g.bnf_rm = q.rm;
-      g.bnf_rv = q.rv;
-      g.bnf_cnt = q.cnt;
-      g.bnf_mom = q.mom;
-      g.bnf_eps = q.eps;
-    }
-  }
-  TORCH_CHECK(!g_bnpub.active, "gemm: gemm_bnpub_next is pending but this GEMM writes no BatchNorm partials");
-  if (g_bnl.active) {
-    BnlPending& p = g_bnl;
-    p.active = false;      // consumed by this call whatever happens below
-    TORCH_CHECK(!ta && !bin && !cbf && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && g.splitk == 1 &&
-                    (tile == 32 || tile == 64) && group == 0 && !chain && g.vec && fedtgan::client_batch().k == 1,
-                "gemm: BatchNorm on load needs a plain unsplit C = A op(B) + bias (row-major fp32 A, 32/64 tiles, 16-B "
-                "operands, one client, unpaired)");
-    TORCH_CHECK(p.rpg >= 1 && p.rpg <= M && (!g.bn_part || g.bn_rpg == p.rpg), "gemm: BatchNorm on load rows per batch");
-    for (int j = 0; j < p.n; ++j) {
-      const fedtgan::GemmArgs::BnLoad& r = p.r[j];
-      TORCH_CHECK(r.k0 + r.width <= K, "gemm: BatchNorm-on-load range beyond K");
-      if (r.part) TORCH_CHECK(p.part_numel[j] >= ((M + r.ptm - 1) / r.ptm) * 6 * r.width, "gemm: partials too small");
-      if (p.out) TORCH_CHECK(p.nhat_rows[j] >= M, "gemm: nhat rows");
-      g.bnl[j] = r;
-    }
-    if (p.n == 2) TORCH_CHECK(p.r[0].k0 + p.r[0].width <= p.r[1].k0 || p.r[1].k0 + p.r[1].width <= p.r[0].k0,
-                              "gemm: BatchNorm-on-load ranges overlap");
-    if (p.out) TORCH_CHECK(p.out_rows >= M && p.out_cols >= K, "gemm: materialised rows [M, K]");
-    g.nbnl = p.n;
-    g.bn_rpg = p.rpg;
-    g.bnl_mom = p.mom;
-    g.bnl_eps = p.eps;
-    g.bnl_out = p.out;
-    g.bnl_ldo = p.ldo;
   }
   if (tile_cnt.has_value() && tile_cnt->defined() && g.splitk > 1) {
     // one arrival counter per output tile, all zero (the reducing workgroup re-zeroes its tile's)
@@ -518,6 +369,16 @@ void gemm(const Tensor& a, const Tensor& b, const Tensor& c, bool ta, bool tb, d
   // adam_cs launch on this stream (a weight gradient inside that optimizer's gradient buffer: the
   // two become one launch, gemm_adam_kernel); group 0: launch now
   const hipStream_t hs = cur_stream();
+  if (group == 6 || group == 7) {
+    // group 7: the same, with the gradient itself stored too (GemmArgs::adam_grad)
+    TORCH_CHECK(!g_adam_pre.active, "gemm: a short-K GEMM is already held for the Adam launch");
+    g.adam_grad = group == 7 ? 1 : 0;
+    TORCH_CHECK(ta && !tb && epi == fedtgan::EPI_NONE && alpha == 1.0 && beta == 0.0 && !g.bias && !g.oh_w && !g.head_a &&
+                    !g.bn_part && !cbf && !bin && !chain && fedtgan::client_batch().k == 1,
+                "gemm: group 6 holds a plain C = A^T B weight gradient of one client (short-K Adam)");
+    g_adam_pre = AdamHeld{g, hs, c.data_ptr<float>(), (int64_t)M, (int64_t)N, (int64_t)g.ldc, true};
+    return;
+  }
   if (group == 3) {
     TORCH_CHECK(!g_adam_held.active, "gemm: a GEMM is already held for the Adam launch");
     TORCH_CHECK(epi == fedtgan::EPI_NONE && beta == 0.0 && !g.bias && !g.oh_w && !g.head_a && !g.bn_part && !cbf && !bin,
@@ -962,7 +823,8 @@ void bn_relu_bwd(const Tensor& dr, const Tensor& r, const Tensor& nhat, const Te
 
 void adam(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v, const Tensor& step, double lr, double b1,
           double b2, double eps, double wd, const optional<Tensor>& rng_bump) {
-  TORCH_CHECK(!g_adam_held.active, "adam: a GEMM held for the Adam launch needs adam_cs (the column-sum form)");
+  TORCH_CHECK(!g_adam_held.active && !g_adam_pre.active,
+              "adam: a GEMM held for the Adam launch needs adam_cs (the column-sum form)");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous() && m.is_contiguous() && v.is_contiguous(), "adam: contiguous");
   TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: sizes");
   TORCH_CHECK((reinterpret_cast<uintptr_t>(p.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0,
@@ -1020,6 +882,34 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
   uint64_t* bump = nullptr;
   if (rng_bump.has_value() && rng_bump->defined()) bump = reinterpret_cast<uint64_t*>(rng_bump->data_ptr<int64_t>());
   const hipStream_t hs = cur_stream();
+  if (g_adam_pre.active) {
+    // the held short-K weight gradient applies Adam to its own block now (it reads only A, B and the step
+    // counter, and writes only its block of p / m / v: independent of this launch's other elements)
+    AdamHeld h = g_adam_pre;
+    g_adam_pre.active = false;
+    TORCH_CHECK(h.stream == hs, "adam_cs: the short-K GEMM held for it was issued on another stream");
+    const int64_t off = h.c - g0;
+    TORCH_CHECK(h.c >= g0 && off % 4 == 0 && h.ldc % 4 == 0 && off + h.M * h.ldc <= n,
+                "adam_cs: the held short-K GEMM's output must be a 4-aligned block inside the gradient buffer");
+    for (int k = 0; k < cs.n_jobs; ++k)
+      TORCH_CHECK(off >= cs.own_hi[k] || off + h.M * h.ldc <= cs.own_lo[k], "adam_cs: the short-K GEMM overlaps a job");
+    fedtgan::GemmArgs q = h.g;
+    q.adam_p = fp(p) + off;
+    q.adam_m = fp(m) + off;
+    q.adam_v = fp(v) + off;
+    q.adam_step = cfp(step);
+    q.adam_lr = (float)lr;
+    q.adam_b1 = (float)b1;
+    q.adam_b2 = (float)b2;
+    q.adam_eps = (float)eps;
+    q.adam_wd = (float)wd;
+    if (fedtgan::launch_gemm_shortk_adam(q, hs)) {
+      cs.skip2_lo = off;
+      cs.skip2_hi = off + h.M * h.ldc;
+    } else {
+      fedtgan::launch_gemm(h.g, hs);     // (a shape the short-K kernel does not take: the plain GEMM, Adam below)
+    }
+  }
   if (g_adam_held.active) {
     // the held weight-gradient GEMM (gemm(..., group=3)) writes rows [0, M) x [0, N) at stride ldc of a
     // block inside g: Adam over that whole block is left to the GEMM's tiles (elements of the block
@@ -1032,12 +922,23 @@ void adam_cs(const Tensor& p, const Tensor& g, const Tensor& m, const Tensor& v,
                 "adam_cs: the held GEMM's output must be a 4-aligned block inside the gradient buffer");
     for (int k = 0; k < cs.n_jobs; ++k)
       TORCH_CHECK(off >= cs.own_hi[k] || off + h.M * h.ldc <= cs.own_lo[k], "adam_cs: the held GEMM overlaps a job output");
+    TORCH_CHECK(cs.skip2_hi <= off || off + h.M * h.ldc <= cs.skip2_lo, "adam_cs: the two held GEMMs overlap");
     cs.skip_lo = off;
     cs.skip_hi = off + h.M * h.ldc;
+    if (cs.skip2_hi > cs.skip2_lo && cs.skip2_lo < cs.skip_lo) {   // (adam_cs_body: the lower range first)
+      std::swap(cs.skip_lo, cs.skip2_lo);
+      std::swap(cs.skip_hi, cs.skip2_hi);
+    }
     if (fedtgan::launch_gemm_adam(h.g, fp(p), cfp(g), fp(m), fp(v), cfp(step), n, (float)lr, (float)b1, (float)b2,
                                   (float)eps, (float)wd, bump, cs, hs))
       return;
-    cs.skip_lo = cs.skip_hi = 0;      // shape not instantiated: the GEMM, then the plain launch
+    // shape not instantiated: the GEMM, then the plain launch (keeping the short-K range cut out, if any)
+    if (cs.skip_lo == off) cs.skip_lo = cs.skip_hi = 0;
+    else cs.skip2_lo = cs.skip2_hi = 0;
+    if (cs.skip_hi <= cs.skip_lo && cs.skip2_hi > cs.skip2_lo) {
+      std::swap(cs.skip_lo, cs.skip2_lo);
+      std::swap(cs.skip_hi, cs.skip2_hi);
+    }
     fedtgan::launch_gemm(h.g, hs);
   }
   fedtgan::launch_adam_colsum(fp(p), cfp(g), fp(m), fp(v), cfp(step), p.numel(), (float)lr, (float)b1, (float)b2,
@@ -1455,6 +1356,23 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gemm_store_wt = value ? 1 : 0;
     return prev;
   }
+  if (key == "gemm_shortk") {
+    const int64_t prev = fedtgan::g_gemm_shortk;
+    fedtgan::g_gemm_shortk = value ? 1 : 0;
+    return prev;
+  }
+  if (key == "gemm_shortk_store") {
+    TORCH_CHECK(value >= 0 && value <= 2, "gemm_shortk_store: 0 plain, 1 non-temporal, 2 write-through");
+    const int64_t prev = fedtgan::g_gemm_shortk_store;
+    fedtgan::g_gemm_shortk_store = (int)value;
+    return prev;
+  }
+  if (key == "gemm_shortk_min_n") {
+    TORCH_CHECK(value >= 4, "gemm_shortk_min_n: >= 4");
+    const int64_t prev = fedtgan::g_gemm_shortk_min_n;
+    fedtgan::g_gemm_shortk_min_n = (int)value;
+    return prev;
+  }
   if (key == "gemm_splitk_inlaunch") {
     const int64_t prev = fedtgan::g_gemm_splitk_inlaunch;
     fedtgan::g_gemm_splitk_inlaunch = value ? 1 : 0;
@@ -1567,11 +1485,6 @@ TORCH_LIBRARY(fedtgan, m) {
   m.def("csr_rows(Tensor opt, Tensor width, int maxw, Tensor(a!) part, Tensor(b!) count, Tensor(c!) offset, "
         "Tensor(d!) rows, int chunk) -> ()");
   m.def("gemm_achain_next(Tensor out, Tensor ws, Tensor cnt) -> ()", &gemm_achain_next);
-  m.def("gemm_bnpub_next(Tensor cnt, Tensor mean, Tensor invstd, Tensor rm, Tensor rv, float momentum, float eps) -> ()",
-        &gemm_bnpub_next);
-  m.def("gemm_bnl_next(Tensor?[] part, Tensor[] mean, Tensor[] invstd, Tensor[] gamma, Tensor[] beta, Tensor[] rm, "
-        "Tensor[] rv, Tensor?[] nhat, int[] k0, int[] ptm, int rpg, float momentum, float eps, Tensor? out) -> ()",
-        &gemm_bnl_next);
   m.def("set_client_batch(int k, int stride, int seed_step, int base) -> int", &set_client_batch);
   m.def("check_status() -> int", &check_status);
   m.def("is_checked() -> bool", &is_checked);

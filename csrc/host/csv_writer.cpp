@@ -26,6 +26,7 @@
 #include <cstring>
 #include <exception>
 #include <future>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -197,9 +198,10 @@ char* put_date(char* p, const DateFields& f, int style) {
 // Rows [r0, r1) into one string.  Every vocabulary entry is quoted once up front and each row is
 // written through a raw pointer into a buffer sized for its worst case (26 bytes per number), so the
 // hot loop does no allocation, no searching and no growing appends.
-std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, int64_t r1,
-                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style,
-                               const double* aux, int64_t aux_cols) {
+// rows [r0, r1) formatted into buf (grown as needed, never shrunk or zero-filled again); returns the length
+static size_t format_csv_into(std::vector<char>& buf, const double* values, int64_t cols, int64_t r0, int64_t r1,
+                              const std::vector<CsvColumn>& out, const std::vector<int>& date_style,
+                              const double* aux, int64_t aux_cols) {
   std::vector<std::vector<std::string>> qv(out.size());
   size_t row_max = 1;
   for (size_t j = 0; j < out.size(); ++j) {
@@ -220,9 +222,10 @@ std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, i
     }
     row_max += w + 1;
   }
-  std::string s;
-  s.resize((size_t)(r1 - r0) * row_max);
-  char* p = &s[0];
+  const size_t need = (size_t)(r1 - r0) * row_max;
+  if (buf.size() < need) buf.resize(need);
+  char* const b0 = buf.data();
+  char* p = b0;
   for (int64_t r = r0; r < r1; ++r) {
     const double* row = values + r * cols;
     const double* arow = aux ? aux + r * aux_cols : nullptr;   // column src >= cols is arow[src - cols]
@@ -258,9 +261,23 @@ std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, i
     }
     *p++ = '\n';
   }
-  s.resize((size_t)(p - s.data()));
-  return s;
+  return (size_t)(p - b0);
 }
+
+std::string format_csv_columns(const double* values, int64_t cols, int64_t r0, int64_t r1,
+                               const std::vector<CsvColumn>& out, const std::vector<int>& date_style,
+                               const double* aux, int64_t aux_cols) {
+  std::vector<char> buf;
+  const size_t n = format_csv_into(buf, values, cols, r0, r1, out, date_style, aux, aux_cols);
+  return std::string(buf.data(), n);
+}
+
+// Chunk buffers kept across tables (write_csv_columns runs once per epoch, on the runtime's writer thread): a
+// fresh zero-filled string per chunk cost a page fault per 4 KB of text on every table -- ~45 MB of first
+// touches per 40k-row Intrusion table, most of the formatter's time, and page-table contention with the
+// training thread.  One table at a time (the mutex); the buffers are reused as they are.
+std::mutex g_csv_mu;
+std::vector<std::vector<char>> g_csv_bufs;
 
 std::vector<int> resolve_date_styles(const double* values, int64_t rows, int64_t cols, const std::vector<CsvColumn>& out) {
   // pandas writes the re-joined column by its dtype, which depends on the whole column: with any "empty"
@@ -323,7 +340,9 @@ void write_csv_columns(const std::string& path, const double* values, int64_t ro
   // the formatting time, and the write of chunk c overlaps the formatting of chunks > c
   const int64_t chunk = std::max<int64_t>(512, (rows + 4 * threads - 1) / (4 * threads));
   const int nchunks = (int)std::max<int64_t>(1, (rows + chunk - 1) / chunk);
-  std::vector<std::string> parts((size_t)nchunks);
+  std::lock_guard<std::mutex> lock(g_csv_mu);
+  if (g_csv_bufs.size() < (size_t)nchunks) g_csv_bufs.resize((size_t)nchunks);
+  std::vector<size_t> lens((size_t)nchunks, 0);
   std::vector<std::promise<void>> ready((size_t)nchunks);
   std::vector<std::future<void>> done;
   done.reserve((size_t)nchunks);
@@ -335,7 +354,7 @@ void write_csv_columns(const std::string& path, const double* values, int64_t ro
       for (int c = next.fetch_add(1); c < nchunks; c = next.fetch_add(1)) {
         try {
           const int64_t r0 = (int64_t)c * chunk, r1 = std::min(rows, r0 + chunk);
-          parts[(size_t)c] = format_csv_columns(values, cols, r0, r1, out, style, aux, aux_cols);
+          lens[(size_t)c] = format_csv_into(g_csv_bufs[(size_t)c], values, cols, r0, r1, out, style, aux, aux_cols);
           ready[(size_t)c].set_value();
         } catch (...) {
           ready[(size_t)c].set_exception(std::current_exception());
@@ -353,20 +372,19 @@ void write_csv_columns(const std::string& path, const double* values, int64_t ro
   std::exception_ptr err;
   // a short write (full disk, I/O error) or a failed close is an error like a formatting failure: the
   // caller must not record a truncated table as written
-  auto put = [&](const std::string& b) {
-    if (f && !err && std::fwrite(b.data(), 1, b.size(), f) != b.size())
+  auto put = [&](const char* b, size_t n) {
+    if (f && !err && std::fwrite(b, 1, n, f) != n)
       err = std::make_exception_ptr(std::runtime_error("csv: short write to " + path));
   };
   if (!f) err = std::make_exception_ptr(std::runtime_error("csv: cannot open " + path));
-  else put(header);
+  else put(header.data(), header.size());
   for (int c = 0; c < nchunks; ++c) {
     try {
       done[(size_t)c].get();
     } catch (...) {
       if (!err) err = std::current_exception();
     }
-    put(parts[(size_t)c]);
-    std::string().swap(parts[(size_t)c]);
+    put(g_csv_bufs[(size_t)c].data(), lens[(size_t)c]);
   }
   for (auto& th : pool) th.join();
   if (f && std::fclose(f) != 0 && !err) err = std::make_exception_ptr(std::runtime_error("csv: close failed for " + path));

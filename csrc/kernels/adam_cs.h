@@ -188,15 +188,18 @@ __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restric
     // for every workgroup -- 2 per CU -- which left the one-float4-per-thread loop HBM-starved on the wide
     // table's 35 M-parameter D).  The fused GEMM's range [skip_lo, skip_hi) is cut out of the index space
     // (no wasted loads); the column-sum jobs' few elements are loaded and left to the jobs.
+    // (and a second range, [skip2_lo, skip2_hi) above the first: a short-K weight gradient's, updated ahead)
     const int64_t lo4 = cs.skip_lo >> 2, hi4 = max(cs.skip_hi >> 2, lo4);
-    const int64_t nn = n4 - (hi4 - lo4);
+    const int64_t lo4b = cs.skip2_lo >> 2, hi4b = max(cs.skip2_hi >> 2, lo4b);
+    const int64_t nn = n4 - (hi4 - lo4) - (hi4b - lo4b);
     for (int64_t i0 = (int64_t)(bid - nb) * blockDim.x + threadIdx.x; i0 < nn; i0 += U * stride) {
       float4 pp[U], gg[U], mm[U], vv[U];
       int64_t ix[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t j = min(i0 + u * stride, nn - 1);
-        ix[u] = j < lo4 ? j : j + (hi4 - lo4);
+        const int64_t j1 = j < lo4 ? j : j + (hi4 - lo4);
+        ix[u] = j1 < lo4b ? j1 : j1 + (hi4b - lo4b);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -230,6 +233,7 @@ __device__ __forceinline__ void adam_cs_body(int bid, int nblk, float* __restric
     bool owned = false;
     for (int k = 0; k < cs.n_jobs; ++k) owned |= e >= cs.own_lo[k] && e < cs.own_hi[k];
     owned |= e >= cs.skip_lo && e < cs.skip_hi;     // updated by a fused GEMM's epilogue (gemm_adam_kernel)
+    owned |= e >= cs.skip2_lo && e < cs.skip2_hi;   // by a short-K weight gradient's, ahead of this launch
     if (owned) continue;
     float4 pp = p4[i], gg = g4[i], mm = m4[i], vv = v4[i];
     float* pf = reinterpret_cast<float*>(&pp);

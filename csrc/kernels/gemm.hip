@@ -157,63 +157,6 @@ __device__ __forceinline__ int lds_swz(int row) {
   return (3 * (row >> 4)) & (KC / 8 - 1);
 }
 
-// ----------------------------------------------------------------------------- BatchNorm on load (EK 5 / 6)
-// A generator layer's BatchNorm(train) + ReLU folded into its consumers (GemmArgs::bnl): the producing GEMM
-// stores the layer's pre-BN output a plus per-tile partial statistics (EK 4 / 5, bn_tile_partials), and every
-// GEMM that reads the layer's output stages relu(BN(a)) from a into LDS.  The per-column (mean, invstd, gamma,
-// beta) of both batches sit in an LDS table behind the stage buffers.  No BatchNorm launch and no extra pass
-// over the activations remain in the forward (the bn_relu_train launches were 2 x 7.7 us of the one-client step).
-constexpr int BNL_W = 256;                                    // widest range (host-checked)
-constexpr size_t BNL_TAB_BYTES = 2 * 2 * BNL_W * sizeof(float) * 4;   // [range][batch][column] float4
-
-struct BnlCtx {
-  const f32x4* tab;   // [(j * 2 + b) * BNL_W + c] = (mean, invstd, gamma, beta)
-  int nr, rpg;
-  int k0[2], w[2];
-  float* out;         // materialise this burst (nullptr: not this workgroup's burst)
-  int ldo;
-  float* nhat[2];
-  int ldn[2];
-};
-
-// 4 consecutive k of row m (k % 4 == 0; a range never splits a float4: k0 and width are multiples of 4).
-// ok[e]: element in range (others stay 0 and are not materialised).
-__device__ __forceinline__ void bnl_apply4(const BnlCtx& c, int m, int k, float (&x)[4], const bool (&ok)[4]) {
-  // range selection by selects, not by indexing the context's arrays with a run-time index (that put the
-  // context in scratch: 80 B per lane, every staged float4 paying scratch loads)
-  const bool in0 = k >= c.k0[0] && k < c.k0[0] + c.w[0];
-  const bool in1 = !in0 && c.nr > 1 && k >= c.k0[1] && k < c.k0[1] + c.w[1];
-  const int kk = k - (in0 ? c.k0[0] : c.k0[1]);
-  const int b = m >= c.rpg ? 1 : 0;
-  if (in0 || in1) {
-    const f32x4* t4 = c.tab + ((in0 ? 0 : 2) + b) * BNL_W + kk;
-    float n[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x4 t = t4[e];
-      n[e] = (x[e] - t[0]) * t[1];            // the bn_relu_train expressions
-      const float y = n[e] * t[2] + t[3];
-      x[e] = ok[e] ? (y > 0.f ? y : 0.f) : 0.f;
-    }
-    if (c.out && ok[0]) {
-      float* dst = (in0 ? c.nhat[0] : c.nhat[1]) + (size_t)m * (in0 ? c.ldn[0] : c.ldn[1]) + kk;
-      if (ok[3]) *reinterpret_cast<f32x4*>(dst) = f32x4{n[0], n[1], n[2], n[3]};
-      else
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (ok[e]) dst[e] = n[e];
-    }
-  }
-  if (c.out && ok[0]) {
-    float* dst = c.out + (size_t)m * c.ldo + k;
-    if (ok[3]) *reinterpret_cast<f32x4*>(dst) = f32x4{x[0], x[1], x[2], x[3]};
-    else
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (ok[e]) dst[e] = x[e];
-  }
-}
-
 template <int KC, bool ROWMAJ, int R>
 struct Chunk {
   static constexpr int NV = R * KC / (4 * NT);   // float4 per thread
@@ -312,33 +255,6 @@ struct Chunk {
           *reinterpret_cast<uint32_t*>(&s[row * (KC + 8) + pk]) =
               pack_bf16x2(ok_cm(i, 0, e) ? v[2 * i][e] : 0.f, ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f);
         }
-      }
-    }
-  }
-
-  // BatchNorm on load (row-major operand only): relu(BN(a)) of the ranges in bc, staged as bf16 / fp32
-  template <bool BF16>
-  __device__ __forceinline__ void store_bnl(void* s_, const BnlCtx& bc) const {
-    static_assert(ROWMAJ, "BatchNorm on load stages a row-major A");
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
-      float x[4];
-      bool ok[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        ok[e] = ok_rm(i, e);
-        x[e] = ok[e] ? v[i][e] : 0.f;
-      }
-      bnl_apply4(bc, r0 + r, k0 + 4 * q, x, ok);
-      if constexpr (BF16) {
-        uint16_t* s = reinterpret_cast<uint16_t*>(s_);
-        *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
-      } else {
-        float* s = reinterpret_cast<float*>(s_);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) s[r * (KC + 1) + 4 * q + e] = x[e];
       }
     }
   }
@@ -514,251 +430,12 @@ __device__ __forceinline__ void bn_tile_partials(const GemmArgs& g, const f32x4 
       for (int b = 0; b < 2; ++b) {
         float* o = g.bn_part + ((size_t)(by * 2 + b) * 3) * g.N + n;
         const float q = red[col * 2 + b] + red[(TN + col) * 2 + b];
-        if (g.bnf_cnt) {   // read back inside this launch by the column tile's last workgroup (bn_publish)
-          __hip_atomic_store(o, tot[j][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(o + g.N, mean[j][b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(o + 2 * (size_t)g.N, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          o[0] = tot[j][b];
-          o[g.N] = mean[j][b];
-          o[2 * (size_t)g.N] = q;
-        }
+        o[0] = tot[j][b];
+        o[g.N] = mean[j][b];
+        o[2 * (size_t)g.N] = q;
       }
     }
   }
-}
-
-__device__ __forceinline__ void bnl_merge(float& n, float& mu, float& m2, float nb, float mub, float m2b) {
-  const float nt = n + nb;
-  if (nt > 0.f) {
-    const float d = mub - mu;
-    mu += d * (nb / nt);
-    m2 += m2b + d * d * (n * nb / nt);
-    n = nt;
-  }
-}
-
-// GemmArgs::bnf_*: after its partials, a workgroup arrives on its column tile's counter; the last arrival merges
-// the column block's partials of every row tile in tile order (the order bnl_prologue merges them: the same bits)
-// and publishes mean / invstd [2][N] plus the running statistics, batch after batch.  The partials are stored
-// and read back with agent-scope (sc1) accesses and every wave's stores are complete (vmcnt) before the relaxed
-// arrival -- the split-K hand-off's protocol.  (Agent-scope release / acquire fences instead -- an L2 write-back
-// per workgroup -- measured the folded step 221.6 us against 205.0 us without publishing.)
-template <int TM, int TN>
-__device__ __forceinline__ void bn_publish(const GemmArgs& g, int n0, int bx, int ntiles_m) {
-  __shared__ unsigned is_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add(&g.bnf_cnt[bx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = t == (unsigned)(ntiles_m - 1) ? 1u : 0u;
-    if (last) __hip_atomic_store(&g.bnf_cnt[bx], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = last;
-  }
-  __syncthreads();
-  if (is_last == 0u) return;
-  const int c = threadIdx.x, n = n0 + c;
-  if (c >= TN || n >= g.N) return;
-  const int rpg = g.bn_rpg, M = g.M, ng = M > rpg ? 2 : 1;
-  float mu[2] = {0.f, 0.f}, var[2] = {0.f, 0.f};
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    if (b >= ng) continue;
-    const int t0 = b ? rpg / TM : 0, t1 = b ? (M - 1) / TM : (min(rpg, M) - 1) / TM;
-    float nn = 0.f, mean = 0.f, m2 = 0.f;
-    for (int tb = t0; tb <= t1; tb += 8) {   // 8 tiles' triples in flight, then merged in order
-      float pc[8], pm[8], pq[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float* p = g.bn_part + ((size_t)(min(tb + u, t1) * 2 + b) * 3) * g.N + n;
-        pc[u] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pm[u] = __hip_atomic_load(p + g.N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        pq[u] = __hip_atomic_load(p + 2 * (size_t)g.N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (tb + u <= t1) bnl_merge(nn, mean, m2, pc[u], pm[u], pq[u]);
-    }
-    mu[b] = mean;
-    var[b] = nn > 0.f ? m2 / nn : 0.f;
-    g.bnf_mean[(size_t)b * g.N + n] = mean;
-    g.bnf_invstd[(size_t)b * g.N + n] = rsqrtf(var[b] + g.bnf_eps);
-  }
-  const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnf_mom;
-  float rm = g.bnf_rm[n], rv = g.bnf_rv[n];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    if (b >= ng) continue;
-    rm = (1.f - mom) * rm + mom * mu[b];
-    rv = (1.f - mom) * rv + mom * var[b] * unb;
-  }
-  g.bnf_rm[n] = rm;
-  g.bnf_rv[n] = rv;
-}
-
-// Prologue of a BatchNorm-on-load GEMM (EK 5 / 6): the (mean, invstd, gamma, beta) table of every range for the
-// batches of this tile's rows.  From partials: merged in producer-tile order (every workgroup gets the same
-// bits); tile (0, 0, 0) merges both batches, publishes mean / invstd and advances the running statistics
-// batch after batch, as bn_relu_train does (biased batch variance; running variance unbiased).
-template <int TM>
-__device__ __forceinline__ void bnl_prologue(const GemmArgs& g, int m0, bool fin, f32x4* tab) {
-  const int rpg = g.bn_rpg, M = g.M;
-  const int ng = M > rpg ? 2 : 1;
-  const int blo = m0 >= rpg ? 1 : 0, bhi = (min(m0 + TM, M) - 1) >= rpg ? 1 : 0;
-  // Fast path (the generator's step: one range from partials, <= BNL_CH producer tiles per batch, one column per
-  // thread): every load of the prologue -- the partial triples of both batches, gamma / beta and the final
-  // statistics of the other range -- is issued before any is used, so the prologue costs one memory round trip.
-  // (Loads behind the merges / table stores of an earlier batch or range serialise: measured 3-4 round trips,
-  // the output GEMM 10.4 -> 28.9 us.)
-  constexpr int BNL_CH = 18;
-  int jp = -1, maxw = 0;
-  for (int j = 0; j < g.nbnl; ++j) {
-    if (g.bnl[j].part) jp = jp < 0 ? j : 99;
-    maxw = max(maxw, g.bnl[j].width);
-  }
-  int tlo[2] = {0, 0}, thi[2] = {-1, -1};
-  bool need[2] = {false, false};
-  if (jp >= 0 && jp < 99) {
-    const int ptm = g.bnl[jp].ptm;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (b >= ng) continue;
-      need[b] = fin || (b >= blo && b <= bhi);
-      tlo[b] = b ? rpg / ptm : 0;
-      thi[b] = b ? (M - 1) / ptm : (min(rpg, M) - 1) / ptm;
-    }
-  }
-  const bool fast = jp < 99 && maxw <= NT && thi[0] - tlo[0] < BNL_CH && thi[1] - tlo[1] < BNL_CH;
-  if (fast) {
-    const int c = threadIdx.x;
-    float gm[2] = {0.f, 0.f}, bt[2] = {0.f, 0.f}, fm[2][2] = {}, fi[2][2] = {};
-    float pc[2][BNL_CH], pm[2][BNL_CH], pq[2][BNL_CH];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j >= g.nbnl || c >= g.bnl[j].width) continue;
-      const GemmArgs::BnLoad& L = g.bnl[j];
-      gm[j] = L.gamma[c];
-      bt[j] = L.beta[c];
-      if (!L.part)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          if (b >= blo && b <= bhi) {
-            fm[j][b] = L.mean[(size_t)b * L.width + c];
-            fi[j][b] = L.invstd[(size_t)b * L.width + c];
-          }
-    }
-    if (jp >= 0 && c < g.bnl[jp].width) {
-      const GemmArgs::BnLoad& L = g.bnl[jp];
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        if (need[b])
-#pragma unroll
-          for (int u = 0; u < BNL_CH; ++u) {
-            const float* p = L.part + ((size_t)(min(tlo[b] + u, thi[b]) * 2 + b) * 3) * L.width + c;
-            pc[b][u] = p[0];
-            pm[b][u] = p[L.width];
-            pq[b][u] = p[2 * (size_t)L.width];
-          }
-    }
-    // every load is in flight: now the statistics, the table and (tile (0, 0, 0)) the published ones
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j >= g.nbnl || c >= g.bnl[j].width) continue;
-      const GemmArgs::BnLoad& L = g.bnl[j];
-      if (j != jp) {
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          if (b >= blo && b <= bhi) tab[(j * 2 + b) * BNL_W + c] = f32x4{fm[j][b], fi[j][b], gm[j], bt[j]};
-        continue;
-      }
-      float mu[2] = {0.f, 0.f}, var[2] = {0.f, 0.f};
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if (!need[b]) continue;
-        float n = 0.f, mean = 0.f, m2 = 0.f;
-#pragma unroll
-        for (int u = 0; u < BNL_CH; ++u)
-          if (tlo[b] + u <= thi[b]) bnl_merge(n, mean, m2, pc[b][u], pm[b][u], pq[b][u]);
-        mu[b] = mean;
-        var[b] = n > 0.f ? m2 / n : 0.f;
-        const float is = rsqrtf(var[b] + g.bnl_eps);
-        tab[(j * 2 + b) * BNL_W + c] = f32x4{mean, is, gm[j], bt[j]};
-        if (fin) {
-          L.mean[(size_t)b * L.width + c] = mean;
-          L.invstd[(size_t)b * L.width + c] = is;
-        }
-      }
-      if (fin) {
-        const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnl_mom;
-        float rm = L.rm[c], rv = L.rv[c];
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if (b >= ng) continue;
-          rm = (1.f - mom) * rm + mom * mu[b];
-          rv = (1.f - mom) * rv + mom * var[b] * unb;
-        }
-        L.rm[c] = rm;
-        L.rv[c] = rv;
-      }
-    }
-    __syncthreads();
-    return;
-  }
-  for (int j = 0; j < g.nbnl; ++j) {
-    const GemmArgs::BnLoad& L = g.bnl[j];
-    for (int c = threadIdx.x; c < L.width; c += NT) {
-      const float gm = L.gamma[c], bt = L.beta[c];
-      if (L.part) {
-        float mu[2] = {0.f, 0.f}, var[2] = {0.f, 0.f};
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          if (b >= ng || (!fin && (b < blo || b > bhi))) continue;
-          const int t0 = b ? rpg / L.ptm : 0, t1 = b ? (M - 1) / L.ptm : (min(rpg, M) - 1) / L.ptm;
-          float n = 0.f, mean = 0.f, m2 = 0.f;
-          // 16 tiles' triples requested together (clamped, always-valid addresses), then merged
-          for (int tb = t0; tb <= t1; tb += 16) {
-            float pc[16], pm[16], pq[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const float* p = L.part + ((size_t)(min(tb + u, t1) * 2 + b) * 3) * L.width + c;
-              pc[u] = p[0];
-              pm[u] = p[L.width];
-              pq[u] = p[2 * (size_t)L.width];
-            }
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-              if (tb + u <= t1) bnl_merge(n, mean, m2, pc[u], pm[u], pq[u]);
-          }
-          mu[b] = mean;
-          var[b] = n > 0.f ? m2 / n : 0.f;
-          const float is = rsqrtf(var[b] + g.bnl_eps);
-          tab[(j * 2 + b) * BNL_W + c] = f32x4{mean, is, gm, bt};
-          if (fin) {
-            L.mean[(size_t)b * L.width + c] = mean;
-            L.invstd[(size_t)b * L.width + c] = is;
-          }
-        }
-        if (fin) {
-          const float unb = (float)rpg / (float)max(rpg - 1, 1), mom = g.bnl_mom;
-          float rm = L.rm[c], rv = L.rv[c];
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            if (b >= ng) continue;
-            rm = (1.f - mom) * rm + mom * mu[b];
-            rv = (1.f - mom) * rv + mom * var[b] * unb;
-          }
-          L.rm[c] = rm;
-          L.rv[c] = rv;
-        }
-      } else {
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-          if (b >= blo && b <= bhi)
-            tab[(j * 2 + b) * BNL_W + c] = f32x4{L.mean[(size_t)b * L.width + c], L.invstd[(size_t)b * L.width + c], gm, bt};
-      }
-    }
-  }
-  __syncthreads();
 }
 
 template <bool F32, int TM, int TN, bool BIN = false>
@@ -916,32 +593,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       b_.template load<VEC>(g.b, g.ldb, n0, g.N, k0, ke);
     }
   };
-  // BatchNorm on load (EK 5 / 6): the stats table behind the two stage buffers; burst i of A is materialised
-  // (GemmArgs::bnl_out) by the workgroups of N tile i % gx
-  constexpr bool BNL = (EK == 5 || EK == 6);
-  BnlCtx bc{};
-  if constexpr (BNL) {
-    static_assert(!TA && !BIN, "BatchNorm on load: row-major fp32 A");
-    bc.tab = reinterpret_cast<const f32x4*>(smem + 2 * C::STAGE);
-    bc.nr = g.nbnl;
-    bc.rpg = g.bn_rpg;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bc.k0[j] = g.bnl[j].k0;
-      bc.w[j] = j < g.nbnl ? g.bnl[j].width : 0;
-      bc.nhat[j] = g.bnl[j].nhat;
-      bc.ldn[j] = g.bnl[j].ldn;
-    }
-    bc.ldo = g.bnl_ldo;
-  }
   auto stage_ab = [&](const CA& a_, const CB& b_, int st) {
     unsigned char* base = smem + st * C::STAGE;
-    if constexpr (BNL) {
-      bc.out = (g.bnl_out && ((a_.k0 - kb) / KC) % gx == bx) ? g.bnl_out : nullptr;
-      a_.template store_bnl<!F32>(base, bc);
-      if constexpr (F32) b_.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
-      else b_.store_bf16(reinterpret_cast<uint16_t*>(base) + TM * C::LD);
-    } else if constexpr (F32) {
+    if constexpr (F32) {
       a_.store_f32(reinterpret_cast<float*>(base));
       b_.store_f32(reinterpret_cast<float*>(base) + TM * C::LD);
     } else if constexpr (BIN) {
@@ -1013,7 +667,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     auto stage2 = [&](int s) { stage_ab(ca2, cb2, s); };
     issue(kb);
     if (kb + KC < ke) issue2(kb + KC);
-    if constexpr (BNL) bnl_prologue<TM>(g, m0, bx == 0 && by == 0 && bz == 0, reinterpret_cast<f32x4*>(smem + 2 * C::STAGE));
     for (int k0 = kb; k0 < ke; k0 += 2 * KC) {
       stage(st);
       __syncthreads();
@@ -1030,7 +683,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
     }
   } else {
     issue(kb);
-    if constexpr (BNL) bnl_prologue<TM>(g, m0, bx == 0 && by == 0 && bz == 0, reinterpret_cast<f32x4*>(smem + 2 * C::STAGE));
     for (int k0 = kb; k0 < ke; k0 += KC) {
       stage(st);
       __syncthreads();
@@ -1082,7 +734,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
       }
   }
   // weight-gradient instantiations (op(A) = A^T) have a plain epilogue (host-checked): no epilogue code at all
-  constexpr bool PLAIN = TA || EK == 1 || EK >= 4;   // (EK 4-6: BatchNorm producers / consumers, plain C + bias)
+  constexpr bool PLAIN = TA || EK == 1 || EK == 4;   // (EK 4: BatchNorm partials, plain C + bias)
   constexpr bool MASKED = !TA && EK == 3;
   const uint64_t step = (!PLAIN && g.epi == EPI_LRELU_DROPOUT && g.rng_ctr) ? *g.rng_ctr : 0ull;
   if constexpr (BIN && TM <= 64) if (g.c16) {
@@ -1248,9 +900,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
                PLAIN ? v : (MASKED ? v * g.ms[(size_t)m * g.ldms + n] : apply_epi(g, v, m, n, step, (uint64_t)m * g.N + n)),
                g.wt);
       }
-  if constexpr (EK == 4 || EK == 5) {   // (host: BN partials need a plain unsplit C = A op(B) + bias)
+  if constexpr (EK == 4) {   // (host: BN partials need a plain unsplit C = A op(B) + bias)
     bn_tile_partials<MI, NJ, TN>(g, acc, m0, n0, by, lane, wm, wn, smem);
-    if (g.bnf_cnt) bn_publish<TM, TN>(g, n0, bx, gy);
   }
 }
 
@@ -1333,7 +984,6 @@ static size_t gemm_smem_bytes(const GemmArgs& g) {
   else stage = T == 32 ? Cfg<false, 32, 32>::STAGE : (T == 128 ? Cfg<false, 128, 128>::STAGE : Cfg<false, 64, 64>::STAGE);
   const int KC = g.f32 ? Cfg<true, 64, 64>::KC / (T >= 128 ? 2 : 1) : Cfg<false, 64, 64>::KC / (T >= 128 ? 2 : 1);
   const bool one_burst = g.kchunk <= KC;
-  if (g.nbnl > 0) return 2 * stage + BNL_TAB_BYTES;   // the BatchNorm-on-load table sits behind two stages
   return (one_burst && T <= 64) ? stage : 2 * stage;
 }
 
@@ -1701,7 +1351,6 @@ static dim3 gemm_prepare(GemmArgs& g) {
 
 // epilogue kind of a launch (gemm_tile's EK): a split-K slice reduced by its own launch, a plain epilogue, or any
 static int gemm_ek(const GemmArgs& g) {
-  if (g.nbnl > 0) return g.bn_part ? 5 : 6;    // BatchNorm on load (+ partials of this GEMM's own output)
   if (g.bn_part) return 4;                     // BatchNorm partials of the output
   if (g.splitk > 1 && !g.red_inl) return 2;
   if (g.splitk > 1) return 0;   // (in-launch reduction: the generic body)
@@ -1720,24 +1369,15 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
   const bool vec = g.vec != 0;   // both operands qualify for 16-B loads (decided by the caller)
   if constexpr (!BATCH) {
     const int ek = gemm_ek(g);
-    if (ek >= 4) {   // BatchNorm producers / consumers: row-major A, 32 / 64 tiles, 16-B operands (host-checked)
-#define FEDTGAN_GEMM_BN(F, TT, EKV)                                                                              \
-  if (g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, true, TT, TT, false, false, EKV>), grid, block, lds, stream, g); \
-  else hipLaunchKernelGGL((gemm_kernel<false, false, F, true, TT, TT, false, false, EKV>), grid, block, lds, stream, g);
-#define FEDTGAN_GEMM_BN_EK(F, TT) \
-  if (ek == 4) {                  \
-    FEDTGAN_GEMM_BN(F, TT, 4)     \
-  } else if (ek == 5) {           \
-    FEDTGAN_GEMM_BN(F, TT, 5)     \
-  } else {                        \
-    FEDTGAN_GEMM_BN(F, TT, 6)     \
-  }
+    if (ek == 4) {   // BatchNorm partials of the output: row-major A, 32 / 64 tiles, 16-B operands (host-checked)
+#define FEDTGAN_GEMM_BN(F, TT)                                                                                    \
+  if (g.tb) hipLaunchKernelGGL((gemm_kernel<false, true, F, true, TT, TT, false, false, 4>), grid, block, lds, stream, g); \
+  else hipLaunchKernelGGL((gemm_kernel<false, false, F, true, TT, TT, false, false, 4>), grid, block, lds, stream, g);
       if (g.f32) {
-        if (T == 32) { FEDTGAN_GEMM_BN_EK(true, 32) } else { FEDTGAN_GEMM_BN_EK(true, 64) }
+        if (T == 32) { FEDTGAN_GEMM_BN(true, 32) } else { FEDTGAN_GEMM_BN(true, 64) }
       } else {
-        if (T == 32) { FEDTGAN_GEMM_BN_EK(false, 32) } else { FEDTGAN_GEMM_BN_EK(false, 64) }
+        if (T == 32) { FEDTGAN_GEMM_BN(false, 32) } else { FEDTGAN_GEMM_BN(false, 64) }
       }
-#undef FEDTGAN_GEMM_BN_EK
 #undef FEDTGAN_GEMM_BN
       return;
     }
@@ -1789,7 +1429,293 @@ static void gemm_dispatch_t(const GemmArgs& g, dim3 grid, dim3 block, size_t lds
 #undef FEDTGAN_GEMM_DISPATCH
 }
 
+// ------------------------------------------------------------------------ short-K weight gradient
+// C [M <= 256, N] = A^T B with A [K, M], B [K, N] both row-major fp32 and K <= 160: the discriminator's
+// first-layer weight gradient dW0 = A0^T X of the wide table (256 x 137,800 over the 150 stacked rows).  As a
+// tile GEMM that is 2,154 workgroups of 128 x 128 each staging two transposed K = 150 operands and writing a
+// 64 KB tile, one round of loads, MFMAs and stores after the other (profiles/wide_r6.md: 100-108 us against
+// a 141 MB-write + 83 MB-read bound of ~35 us).  Here one persistent workgroup per CU keeps the whole A^T
+// operand resident in LDS (bf16, 80 KB) and walks 64-column strips of B: strip s + 1's loads are in flight
+// (registers) while strip s is multiplied and stored.  Both LDS images are row-major [k][column] -- written
+// from coalesced float4 loads with 8-B stores -- and read as MFMA operands with gfx950's transposing LDS read
+// (ds_read_b64_tr_b16: a 16-lane group gets 16 columns x 4 consecutive k), so neither operand is transposed
+// in registers.  The 16-B chunks of a row are XOR-swizzled by the row so that a 32-lane half's two 4-row
+// blocks (k rows 8 apart) hit 64 distinct banks.
+constexpr int SK_THREADS = 512, SK_NS = 64, SK_KMAX = 160, SK_MMAX = 256;
+int g_gemm_shortk = 1;            // 0: the tile GEMM path for every shape
+int g_gemm_shortk_min_n = 16384;  // narrower products keep the tile GEMM (and its pairing)
+
+typedef short sk_v4s __attribute__((ext_vector_type(4)));
+
+// byte offset of halfs [c, c + 4) of row r in a row-major bf16 image of W halfs per row (W = 64 or 256):
+// chunk (8 halfs) index XOR a per-row slot pattern that separates rows {0..3, 8..11} (mod 16) into 8 bank groups
+template <int W>
+__device__ __forceinline__ int sk_off(int r, int c) {
+  const int sw = W == 32 ? 2 * ((r >> 3) & 1)                                 // 64-B rows: 4 per 64 banks
+               : W == 64 ? 2 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1))      // 128-B rows: odd rows sit 32 banks over
+                         : 2 * ((r & 3) | (((r >> 3) & 1) << 2));             // 512-B rows: every row on bank 0
+  return (r * W + (((c >> 3) ^ sw) << 3) + (c & 7)) * 2;
+}
+
+// 8 consecutive k (from k0) of column c0 + (lane & 15), k0 = 8 * (lane >> 4) + kstep: two transposed 4-row reads
+template <int W>
+__device__ __forceinline__ bf16x8 sk_frag(const unsigned char* img, int kbase, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int r = kbase + 8 * g + q;
+  typedef __attribute__((address_space(3))) sk_v4s lds_v4s;
+  const sk_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + sk_off<W>(r, c0 + 4 * p)));
+  const sk_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + sk_off<W>(r + 4, c0 + 4 * p)));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ __launch_bounds__(SK_THREADS) void gemm_shortk_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sk_smem[];
+  unsigned char* As = sk_smem;                                  // [SK_KMAX][SK_MMAX] bf16
+  unsigned char* Bs = sk_smem + SK_KMAX * SK_MMAX * 2;          // [2][SK_KMAX][SK_NS] bf16
+  constexpr int BSZ = SK_KMAX * SK_NS * 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int K = g.K, M = g.M, N = g.N;
+  const int KP = (K + 31) & ~31;                                // MFMA k steps of 32 (rows [K, KP) zero)
+  // A image: row k, columns 4 (t % 64) ... ; 8 rows per pass
+  for (int k = t >> 6; k < KP; k += SK_THREADS / 64) {
+    const int m = 4 * (t & 63);
+    f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (k < K && m < M) x = *reinterpret_cast<const f32x4*>(g.a + (size_t)k * g.lda + m);
+    *reinterpret_cast<uint2*>(As + sk_off<SK_MMAX>(k, m)) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+  }
+  // B strip rows: thread -> column quad t % 16, rows t / 16 + 32 i
+  constexpr int NB = SK_KMAX / (SK_THREADS / 16);               // 5 row passes
+  const int cq = 4 * (t & 15), r0 = t >> 4;
+  f32x4 pf[NB];
+  auto load_strip = [&](int s) {
+    const int n = s * SK_NS + cq;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = r0 + 32 * i;
+      pf[i] = (k < K && n < N) ? *reinterpret_cast<const f32x4*>(g.b + (size_t)k * g.ldb + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage_strip = [&](unsigned char* img) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = r0 + 32 * i;
+      if (k < KP)
+        *reinterpret_cast<uint2*>(img + sk_off<SK_NS>(k, cq)) = uint2{pack_bf16x2(pf[i][0], pf[i][1]),
+                                                                      pack_bf16x2(pf[i][2], pf[i][3])};
+    }
+  };
+  const int nstrips = (N + SK_NS - 1) / SK_NS;
+  // output store policy (g_gemm_shortk_store, host-checked 32-bit offsets): 0 plain, 1 non-temporal, 2 write-through
+  const int pol = g.wt;
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(g.c, 0, 0x7FFFFFFF, 0x00020000);
+  int s = blockIdx.x;
+  if (s < nstrips) load_strip(s);
+  for (int it = 0; s < nstrips; s += gridDim.x, ++it) {
+    unsigned char* img = Bs + (it & 1) * BSZ;    // last read two strips ago, before the previous barrier
+    stage_strip(img);
+    __syncthreads();
+    if (s + (int)gridDim.x < nstrips) load_strip(s + gridDim.x);   // in flight through the MFMAs and stores
+    // wave w: rows [32 w, 32 w + 32) x the strip's 64 columns
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < KP; kb += 32) {
+      bf16x8 af[2], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = sk_frag<SK_MMAX>(As, kb, 32 * w + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = sk_frag<SK_NS>(img, kb, 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = s * SK_NS + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 32 * w + 16 * i + 4 * (lane >> 4) + r;
+          if (m < M && n < N) {
+            if (pol == 0) g.c[(size_t)m * g.ldc + n] = acc[i][j][r];
+            else if (pol == 1) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), crs,
+                                                                     (int)(((size_t)m * g.ldc + n) * 4), 0, 2);
+            else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), crs,
+                                                       (int)(((size_t)m * g.ldc + n) * 4), 0, 16);
+          }
+        }
+      }
+  }
+}
+
+// The same product with Adam applied to the outputs (a weight gradient inside an optimizer's flat gradient buffer,
+// g.adam_* at the same offset as for gemm_adam_kernel), launched right before that optimizer's launch, which skips
+// the block: the 141 MB dW0 of the wide table is neither written (unless g.adam_grad) nor re-read.  Per strip the
+// kernel now moves 3 x 2 x 32 KB of parameters / moments per 256 x 32 block against 19 KB of B, so it is built for
+// bytes in flight: 32-column strips, the accumulators as C^T blocks (operands swapped, so a lane's 4 values are 4
+// consecutive columns of one row: float4 parameters / moments), and the NEXT strip's parameters, moments and B
+// rows requested before this strip's MFMAs -- two register sets, alternating strip by strip.
+constexpr int SKA_NS = 32;
+__global__ __launch_bounds__(SK_THREADS) void gemm_shortk_adam_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ska_smem[];
+  unsigned char* As = ska_smem;                                 // [SK_KMAX][SK_MMAX] bf16
+  unsigned char* Bs = ska_smem + SK_KMAX * SK_MMAX * 2;         // [2][SK_KMAX][SKA_NS] bf16
+  constexpr int BSZ = SK_KMAX * SKA_NS * 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int K = g.K, M = g.M, N = g.N;
+  const int KP = (K + 31) & ~31;
+  for (int k = t >> 6; k < KP; k += SK_THREADS / 64) {
+    const int m = 4 * (t & 63);
+    f32x4 x = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (k < K && m < M) x = *reinterpret_cast<const f32x4*>(g.a + (size_t)k * g.lda + m);
+    *reinterpret_cast<uint2*>(As + sk_off<SK_MMAX>(k, m)) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
+  }
+  const float tt = g.adam_step[0];   // adam_cs_body's bias corrections, from the same step counter
+  const float sz = g.adam_lr / (1.f - powf(g.adam_b1, tt));
+  const float bc2s = sqrtf(1.f - powf(g.adam_b2, tt));
+  // B strip rows: thread -> column quad t % 8, rows t / 8 + 64 i
+  constexpr int RPP = SK_THREADS / (SKA_NS / 4), NB = (SK_KMAX + RPP - 1) / RPP;
+  const int cq = 4 * (t & (SKA_NS / 4 - 1)), r0 = t / (SKA_NS / 4);
+  // wave w: rows [32 w, 32 w + 32) x 32 columns = 2 x 2 blocks; element (i, j) of a lane: row 32 w + 16 i + lane % 16,
+  // columns 16 j + 4 (lane / 16) ... + 3
+  struct Set {
+    f32x4 x[NB];          // B strip rows
+    f32x4 p[2][2], m[2][2], v[2][2];
+  };
+  auto fetch = [&](Set& st, int s) {
+    const int nb = s * SKA_NS;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = r0 + RPP * i;
+      st.x[i] = (k < K && nb + cq < N) ? *reinterpret_cast<const f32x4*>(g.b + (size_t)k * g.ldb + nb + cq)
+                                       : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = min(32 * w + 16 * i + (lane & 15), M - 1);
+        const int n = min(nb + 16 * j + 4 * (lane >> 4), N - 4);
+        const size_t e = (size_t)m * g.ldc + n;
+        st.p[i][j] = *reinterpret_cast<const f32x4*>(g.adam_p + e);
+        st.m[i][j] = *reinterpret_cast<const f32x4*>(g.adam_m + e);
+        st.v[i][j] = *reinterpret_cast<const f32x4*>(g.adam_v + e);
+      }
+  };
+  // one strip: stage its B rows, request the next strip into the other set, multiply, update, store
+  auto strip = [&](Set& cur, Set& nxt, int s, int it, int nstrips) {
+    unsigned char* img = Bs + (it & 1) * BSZ;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int k = r0 + RPP * i;
+      if (k < KP)
+        *reinterpret_cast<uint2*>(img + sk_off<SKA_NS>(k, cq)) = uint2{pack_bf16x2(cur.x[i][0], cur.x[i][1]),
+                                                                        pack_bf16x2(cur.x[i][2], cur.x[i][3])};
+    }
+    __syncthreads();
+    if (s + (int)gridDim.x < nstrips) fetch(nxt, s + gridDim.x);
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < KP; kb += 32) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = sk_frag<SK_MMAX>(As, kb, 32 * w + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = sk_frag<SKA_NS>(img, kb, 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = 32 * w + 16 * i + (lane & 15);
+        const int n = s * SKA_NS + 16 * j + 4 * (lane >> 4);
+        if (m >= M || n >= N) continue;      // (N % 4 == 0: a float4 is all in or all out)
+        const size_t e = (size_t)m * g.ldc + n;
+        f32x4 p4 = cur.p[i][j], m4 = cur.m[i][j], v4 = cur.v[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pe = p4[r], me = m4[r], ve = v4[r];
+          adam_elem(acc[i][j][r], pe, me, ve, g.adam_b1, g.adam_b2, g.adam_eps, g.adam_wd, sz, bc2s);
+          p4[r] = pe;
+          m4[r] = me;
+          v4[r] = ve;
+        }
+        *reinterpret_cast<f32x4*>(g.adam_p + e) = p4;
+        *reinterpret_cast<f32x4*>(g.adam_m + e) = m4;
+        *reinterpret_cast<f32x4*>(g.adam_v + e) = v4;
+        if (g.adam_grad) *reinterpret_cast<f32x4*>(g.c + e) = acc[i][j];
+      }
+  };
+  const int nstrips = (N + SKA_NS - 1) / SKA_NS;
+  Set sa, sb;
+  int s = blockIdx.x, it = 0;
+  if (s < nstrips) fetch(sa, s);
+  while (s < nstrips) {     // two strips per trip: the register sets keep static names
+    strip(sa, sb, s, it++, nstrips);
+    s += gridDim.x;
+    if (s >= nstrips) break;
+    strip(sb, sa, s, it++, nstrips);
+    s += gridDim.x;
+  }
+}
+
+// the shapes gemm_shortk_kernel takes (everything else: the tile GEMM)
+static bool gemm_shortk_ok(const GemmArgs& g) {
+  const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return g_gemm_shortk && g.ta && !g.tb && !g.f32 && !g.bin && !g.c16 && g.nclient <= 1 && g.splitk <= 1 &&
+         g.epi == EPI_NONE && g.alpha == 1.f && g.beta == 0.f && !g.bias && !g.oh_w && !g.bn_part && !g.chain &&
+         !g.head_a && !g.adam_p && g.M <= SK_MMAX && g.M % 4 == 0 && g.K >= 1 && g.K <= SK_KMAX && g.N % 4 == 0 &&
+         g.N >= g_gemm_shortk_min_n && g.lda % 4 == 0 && g.ldb % 4 == 0 && al16(g.a) && al16(g.b) && g.N <= g.ldb &&
+         g.M <= g.lda && g.N <= g.ldc;
+}
+
+int g_gemm_shortk_store = 2;   // write-through: measured best of plain / nt / sc1 (profiles/wide_r6.md)
+
+static void launch_gemm_shortk(GemmArgs g, hipStream_t stream) {
+  g.wt = ((int64_t)g.M * g.ldc * 4 < (int64_t)INT32_MAX) ? g_gemm_shortk_store : 0;   // (buffer stores: 32-bit offsets)
+  static const size_t lds = (size_t)SK_KMAX * (SK_MMAX + 2 * SK_NS) * 2;   // 120 KB: one workgroup per CU
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_shortk_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_shortk_adam_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int nstrips = (g.N + (g.adam_p ? SKA_NS : SK_NS) - 1) / (g.adam_p ? SKA_NS : SK_NS);
+  const dim3 grid(std::min(nstrips, std::max(cus, 1)));
+  if (g.adam_p) hipLaunchKernelGGL(gemm_shortk_adam_kernel, grid, dim3(SK_THREADS), lds, stream, g);
+  else hipLaunchKernelGGL(gemm_shortk_kernel, grid, dim3(SK_THREADS), lds, stream, g);
+}
+
+bool launch_gemm_shortk_adam(GemmArgs g, hipStream_t stream) {
+  check_slab(g);
+  (void)gemm_prepare(g);
+  if (!g.adam_p || !g.adam_m || !g.adam_v || !g.adam_step) return false;
+  GemmArgs q = g;
+  q.adam_p = nullptr;           // (the shape check excludes Adam GEMMs taken by the generic dispatch)
+  if (!gemm_shortk_ok(q)) return false;
+  launch_gemm_shortk(g, stream);
+  return true;
+}
+
 static void gemm_dispatch(const GemmArgs& g, dim3 grid_, hipStream_t stream) {
+  if (gemm_shortk_ok(g)) return launch_gemm_shortk(g, stream);
   const dim3 grid(grid_.x, grid_.y, grid_.z * g.nclient);   // split-K slices x clients
   if (g.nclient > 1) gemm_dispatch_t<true>(g, grid, dim3(NT), gemm_smem_bytes(g), stream);
   else gemm_dispatch_t<false>(g, grid, dim3(NT), gemm_smem_bytes(g), stream);
@@ -1950,7 +1876,7 @@ __global__ __launch_bounds__(NT) void gemm_bnbwd_kernel(GemmArgs g, Grid3 gd, Bn
 
 bool launch_gemm_bnbwd(GemmArgs g, const BnBwdArgs& b, hipStream_t stream) {
   if (g.M <= 0 || g.N <= 0 || b.rows <= 0 || b.cols <= 0) return false;
-  if (client_batch().k > 1 || g.f32 || g.bin || g.c16 || !g.ta || g.tb || g.chain || g.nbnl > 0 || g.bn_part) return false;
+  if (client_batch().k > 1 || g.f32 || g.bin || g.c16 || !g.ta || g.tb || g.chain || g.bn_part) return false;
   const int cols = g_bnb_cols == 8 ? 8 : 4;
   const int groups = NT / cols;
   const int maxr = (b.rows + groups - 1) / groups;

@@ -85,41 +85,7 @@ struct GemmArgs {
   // and sum of squared deviations: bn_part[((m_tile * 2 + batch) * 3 + {0,1,2}) * N + n]
   float* bn_part;
   int bn_rpg;
-  // Published statistics (nullable; with bn_part): the last workgroup of each column tile to write its partials
-  // (arrival counter bnf_cnt[column tile], zero between launches, re-zeroed by that workgroup) merges the column
-  // block's partials in tile order, writes mean / invstd [2][N] and advances the running statistics batch after
-  // batch -- the consumers then load final statistics instead of merging every tile's partials.
-  float* bnf_mean;
-  float* bnf_invstd;
-  float* bnf_rm;
-  float* bnf_rv;
-  unsigned* bnf_cnt;
-  float bnf_mom, bnf_eps;
   int oh_c;       // width of the one-hot block (checked build: gather index bound)
-  // BatchNorm(train) + ReLU of earlier generator layers applied to op(A) while it is staged (gemm_tile EK 5 / 6;
-  // nbnl = 0: none).  op(A) = A row-major, unsplit, C = A op(B) + bias.  Range j covers A's columns
-  // [k0, k0 + width) -- a layer's PRE-BatchNorm output a -- and the GEMM multiplies relu(BN(a)) instead:
-  //   nhat = (a - mean_b) * invstd_b,  y = relu(nhat * gamma + beta)      (b: the row's batch, bn_rpg rows each)
-  // With `part` (the producing GEMM's per-tile partials, bn_part layout, ptiles row tiles of ptm rows) every
-  // workgroup merges the batch statistics itself (Chan, tile order) and tile (0, 0) writes mean / invstd
-  // [2][width] and updates the running statistics (batch after batch); without it mean / invstd are final.
-  // bnl_out (nullable): the workgroups materialise relu(BN(a)) (and the raw columns outside the ranges) at
-  // bnl_out[m * bnl_ldo + k] and nhat at nhat[m * ldn + c] -- burst i by the workgroups of N tile i % gx.
-  struct BnLoad {
-    const float* part;
-    float* mean;
-    float* invstd;
-    const float* gamma;
-    const float* beta;
-    float* rm;
-    float* rv;
-    float* nhat;
-    int ldn, k0, width, ptiles, ptm;
-  } bnl[2];
-  int nbnl;
-  float bnl_mom, bnl_eps;
-  float* bnl_out;
-  int bnl_ldo;
   // Split-K reduced inside the GEMM launch (nullable): one arrival counter per output tile, zero
   // between launches.  Every K-slice workgroup publishes its slab write-through and takes a ticket;
   // the one that completes a tile sums the tile's slabs and applies the epilogue (no
@@ -143,6 +109,7 @@ struct GemmArgs {
   float* adam_v;
   const float* adam_step;
   float adam_lr, adam_b1, adam_b2, adam_eps, adam_wd;
+  int adam_grad;   // gemm_shortk_kernel<ADAM>: also store the gradient (gemm_adam_kernel always does)
   // chained GEMM (host-side pointer, nullable; chain_epilogue_kernel): once this GEMM's output C [M, N]
   // is final, the tail C2 = epi2(C B2^T + bias2) (the tail's own GemmArgs: op(A2) = this C, row-local,
   // K2 = N <= 1024) is computed in this GEMM's reduction launch, as fp32 dot products
@@ -310,7 +277,12 @@ struct AdamColsum {
   int64_t own_lo[8], own_hi[8];
   int dot_self[8];    // dot_v is this job's own output's parameters: use the pre-update values
   int64_t skip_lo, skip_hi;   // elements updated by a fused GEMM's Adam epilogue (gemm_adam_kernel)
+  int64_t skip2_lo, skip2_hi; // and by a short-K weight gradient that applied Adam ahead of this launch
+                              // (launch_gemm_shortk_adam); both ranges 4-aligned, disjoint, skip_lo <= skip2_lo
 };
+// C = A^T B by gemm_shortk_kernel with Adam applied to the outputs in its epilogue (g.adam_* set as for
+// gemm_adam_kernel; the gradient itself is stored only with g.adam_grad); false: shape not taken
+bool launch_gemm_shortk_adam(GemmArgs g, hipStream_t stream);
 void launch_adam_colsum(float* p, const float* g, float* m, float* v, const float* step, int64_t n, float lr, float b1,
                         float b2, float eps, float wd, uint64_t* rng_ctr_bump, const AdamColsum& cs,
                         hipStream_t stream);
@@ -326,6 +298,9 @@ extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int64_t g_adam_u_min;   // Adam launches over >= this many float4 (x clients) load ADAM_U float4 per thread
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
+extern int g_gemm_shortk;          // 1: C = A^T B with K <= 160, M <= 256 and wide N by gemm_shortk_kernel
+extern int g_gemm_shortk_min_n;    // narrowest N that takes it
+extern int g_gemm_shortk_store;    // its output stores: 0 plain, 1 non-temporal, 2 write-through (sc1)
 extern int g_gemm_splitk_inlaunch;   // split-K reduced inside the GEMM launch where a tile counter is given (1)
 extern int g_act_row_mode;   // activation kernels on rows wider than 512: one workgroup per row (1) or per 1-4 rows
 extern int g_decode_rows;   // generation decode: one wave per row (1) or one thread per (row, column) (0)

@@ -387,6 +387,8 @@ class FedRuntime:
                 self.engine.set_training_data(self.train_matrix)
         if getattr(self, "thread_local_capture", False):
             self.engine.capture_mode = "thread_local"
+        if self.gradflow is not None:     # the diagnostics read every parameter gradient after the epoch
+            self.engine.keep_grads = True
         self.engine.set_generation_tables(self.gen_cond, self.transformer)
         self._initial_weights()
         if cfg.resume:

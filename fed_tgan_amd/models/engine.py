@@ -133,6 +133,18 @@ class EngineConfig:
     # Adam epilogue's per-element p / m / v traffic and R0 losing its pair partner cost more than the
     # 51 MB gradient round trip saves; profiles/batched_r3.md)
     fuse_d0_adam: bool = False
+    # HIP, one client: D0's weight gradient, when it is a short-K product the persistent strip kernel takes
+    # (ops.shortk_ok: <= 256 x wide N over <= 160 rows -- the wide table's 256 x 137,800 over 150), applies Adam in
+    # that kernel's epilogue right before the optimizer launch, which skips its range: the 141 MB gradient is
+    # neither written nor re-read.  A/B knob, default off: bitwise the same training, but measured slower (wide
+    # 0.2334-0.241 s/epoch against 0.2275-0.2286 on one box): the kernel's parameter / moment traffic comes as
+    # 256 rows x 128 B per strip (rows 551 KB apart) instead of the float4 Adam's contiguous stream, and runs at
+    # ~3.7 TB/s where the Adam launch runs at ~6 (profiles/wide_r6.md)
+    fuse_d0_shortk: bool = False
+    # every launch stores the step's parameter gradients in the flat gradient buffers (gradient tests, grad-flow
+    # diagnostics -- FedRuntime sets CTGANEngine.keep_grads for those); off, a fused optimizer epilogue may skip a
+    # gradient nothing reads (fuse_d0_shortk)
+    keep_grads: bool = False
     # HIP, bf16: each generator layer's Linear -> BatchNorm(train) -> ReLU as ONE launch, a workgroup
     # owning 16 output columns of one batch (kernels/bn_fused.hip) instead of a tile GEMM + BN launch
     bn_colown: bool = False
@@ -145,21 +157,8 @@ class EngineConfig:
     # zero between steps).  The wide table's G.out gradient: 7,018 x 7,402 dense (228 us) -> 7,018 x 640 + 500
     # scattered rows.  0 = always dense.
     onehot_wgrad_min: int = 1 << 20
-    # HIP, paired step, one-hot conditions, <= 2 hidden generator layers of <= 256 units: each generator layer's
-    # BatchNorm(train) + ReLU is folded into the GEMMs around it instead of a launch of its own (K6).  The layer's
-    # GEMM stores its pre-BN output plus per-tile partial statistics; the next layer's GEMM and the output GEMM
-    # merge those statistics in their prologue and stage relu(BN(a)) from the pre-BN values as they load them;
-    # the output GEMM also writes relu(BN(a)) and nhat back for the backward.  Removes both bn_relu_train launches.
-    # Off by default: measured slower (Intrusion step +11.5 us, profiles/bn_fold_r5.txt): every consumer
-    # workgroup re-merges all producer tiles' partials (+6-13 us per consumer GEMM) against 2 x 7.7 us of BN
-    # launches removed.
-    bn_fold: bool = False
-    # With bn_fold: each layer GEMM's last workgroup per column tile merges the partials once and publishes
-    # mean / invstd and the running statistics (GemmArgs::bnf_*), so the consumers' prologues load final
-    # statistics instead of re-merging every producer tile's partials (backends with bn_publish_capable).
-    # Off: the folded step measured 214 us with it against 205 us without (no fold: 194 us) -- the producer's
-    # serialised last-arrival merge costs more than the consumers' merges (profiles/bn_fold_r5.txt).
-    bn_fold_publish: bool = False
+    # (BatchNorm(train) + ReLU folded into the generator GEMMs around it -- round 5's bn_fold / bn_fold_publish --
+    # measured slower in every variant, +11.5 / +20 us per step (profiles/bn_fold_r5.txt), and was removed.)
     # HIP step graphs (paired step, one client): ONE sampler launch at the head of each graph replay draws the
     # batches of all graph_unroll steps (step k keyed on RNG step ctr + k, into batch-buffer set k) instead of a
     # sampler launch heading every step -- bitwise the same draws; the launch is off the per-step serial path
@@ -468,27 +467,7 @@ class CTGANEngine:
         # generator forward buffers hold two batches: rows [0, B) the D phase, [B, 2B) the G phase.
         # The paired prepare runs both through ONE M = 2B GEMM chain (BN statistics per batch);
         # the per-phase paths use the G-phase rows, which are also what the G backward reads.
-        # BatchNorm folded into the generator GEMMs (EngineConfig.bn_fold): the layers' pre-BN outputs and z live
-        # in Hp = [a_{L-1} | ... | a_0 | z], columns [Hw, Hw + c0) of the same rows as H (one row stride, so the
-        # sampler writes z there and the condition block into H in one launch); the output GEMM materialises
-        # relu(BN(a)) and z into H for the backward
-        c0 = self.c_cols[0]
-        self._fold_static = (getattr(self.ops, "bn_fold_capable", False) and self.use_onehot and bool(self.cfg.bn_fold) and
-                             not self.cfg.bn_colown and
-                             1 <= len(self.gdims) <= 2 and all(g <= 256 and g % 4 == 0 for g in self.gdims) and
-                             all(o % 4 == 0 for o in self.off) and c0 % 4 == 0)
-        if self._fold_static:
-            self._multi = False
-            # rows [Hp | H]: the sampler gets both as one row ([z in Hp] ... [c block in H], the c block last, as
-            # its width is read off the row's end)
-            big = _padded_rows(2 * B, c0 + self.Hw, dev)
-            self.Hp2 = big[:, :c0]
-            self.H2 = big[:, c0:c0 + self.Hw]
-            self._Hbig = big
-            self._bn_part = [z(-(-2 * B // 32) * 6 * g) for g in self.gdims]   # 32-row tiles at most
-            # arrival counters of the statistics-publishing GEMMs (one per column tile, re-zeroed by the kernel)
-            self._bn_cnt = torch.zeros(len(self.gdims), 64, dtype=torch.int32, device=self.device)
-        elif self._multi:
+        if self._multi:
             # one set of the sampler's outputs per step of a graph replay: H2 (z | c behind the activations), the D
             # input block and the draws' col / opt; set 0 is also what the per-step path uses
             self._h2_sets = _padded_rows(self._U * 2 * B, self.Hw, dev)
@@ -701,9 +680,6 @@ class CTGANEngine:
         cond: the rows' (col, opt) int32 condition indices -- the conditional block of H is then
         applied as a one-hot gather instead of a dense K range (``EngineConfig.onehot``)."""
         o = self.ops
-        if training and paired and cond is not None and self._fold_on():
-            self._g_forward_fold(logits, act_out, stream_id, slerp, cond)
-            return
         for i, g in enumerate(self.gdims):
             a, b_ = self.off[i], self.off[i + 1]
             x, W, oh = self._g_in(H, a, self.p[f"G.{i}.W"], cond)
@@ -720,56 +696,6 @@ class CTGANEngine:
         else:
             o.linear_activate(x, W, self.p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
                               slerp=slerp, onehot=oh)
-
-    def _fold_on(self) -> bool:
-        """EngineConfig.bn_fold applies to this launch sequence (one client, one stream, paired step)."""
-        return self._fold_static and self.lanes is None and self.batch is None and \
-            getattr(self.ops, "batch_k", 1) == 1 and bool(self.cfg.paired)
-
-    def _g_forward_fold(self, logits, act_out, stream_id, slerp, cond):
-        """The paired training forward with every BatchNorm folded into the generator GEMMs (EngineConfig.bn_fold):
-        layer i's GEMM reads Hp[:, off[i]:c0] -- layer i-1's pre-BN output staged as relu(BN(.)) from the partial
-        statistics its GEMM wrote -- and stores its own pre-BN output and partials; the output GEMM stages every
-        layer through its BatchNorm (the last from partials, the others from the statistics their first consumer
-        published) and materialises relu(BN(a)), z and nhat into H / nhat for the backward.  Same math as
-        linear_bn_relu + bn_relu_train (batch statistics per batch, running statistics batch after batch)."""
-        o, p = self.ops, self.p
-        Hp, c0, L = self.Hp2, self.c_cols[0], len(self.gdims)
-        rpg, mom, eps = self.B, self.cfg.bn_momentum, self.cfg.bn_eps
-        ptm = []
-
-        pub = bool(self.cfg.bn_fold_publish) and getattr(o, "bn_publish_capable", False)
-
-        def bn_args(j, from_part):
-            return (self._bn_part[j] if from_part and not pub else None, self.bn_mean2[j], self.bn_invstd2[j],
-                    p[f"G.{j}.gamma"], p[f"G.{j}.beta"], p[f"G.{j}.rm"], p[f"G.{j}.rv"])
-
-        for i in range(L):
-            a, b_ = self.off[i], self.off[i + 1]
-            x, W, oh = self._g_in(Hp, a, p[f"G.{i}.W"], cond)
-            tile, _ = o.gemm_plan(x.shape[0], W.shape[0], x.shape[1])
-            tile = min(tile, 64)
-            if i > 0:       # layer i-1's BatchNorm, applied while this GEMM stages its output (its first consumer)
-                part, mean, istd, gm, bt, rm, rv = bn_args(i - 1, True)
-                o.gemm_bnl_next([part], [mean], [istd], [gm], [bt], [rm], [rv], [None], [0], [ptm[i - 1]], rpg, mom, eps)
-            if pub:         # this GEMM's last workgroup per column tile publishes the layer's statistics
-                o.gemm_bnpub_next(self._bn_cnt[i], self.bn_mean2[i], self.bn_invstd2[i], p[f"G.{i}.rm"],
-                                  p[f"G.{i}.rv"], mom, eps)
-            o.gemm(x, W, Hp[:, b_:a], tb=True, bias=p[f"G.{i}.b"], onehot=oh, bn_part=self._bn_part[i], bn_rpg=rpg,
-                   tile=tile, splitk=1)
-            ptm.append(tile)
-        x, W, oh = self._g_in(Hp, 0, p["G.out.W"], cond)
-        cols = [bn_args(j, j == L - 1) for j in range(L)]
-        tile, _ = o.gemm_plan(x.shape[0], W.shape[0], x.shape[1])
-        o.gemm_bnl_next([c[0] for c in cols], [c[1] for c in cols], [c[2] for c in cols], [c[3] for c in cols],
-                        [c[4] for c in cols], [c[5] for c in cols], [c[6] for c in cols],
-                        [self.nhat2[j] for j in range(L)], [self.off[j + 1] for j in range(L)], ptm, rpg, mom, eps,
-                        out=self.H2[:, :c0])
-        if act_out is None:
-            o.gemm(x, W, logits, tb=True, bias=p["G.out.b"], onehot=oh, tile=min(tile, 64), splitk=1)
-        else:
-            o.linear_activate(x, W, p["G.out.b"], logits, act_out, self.spans, self.cfg.tau, stream_id=stream_id,
-                              slerp=slerp, onehot=oh, tile=min(tile, 64), splitk=1)
 
     def _d_forward(self, rows: slice, stream_base: int, X=None, coef=None) -> bool:
         """D's hidden layers on the packed rows.  With ``coef`` the last layer's epilogue also
@@ -875,9 +801,6 @@ class CTGANEngine:
         doubles their workgroups (M = 1000 fills the chip better than M = 500)."""
         o, B = self.ops, self.B
         h, cc = self.H2, self.c_cols
-        if self._fold_on():     # z goes to the pre-BN rows Hp, the condition block to H: one sampler launch
-            c0 = self.c_cols[0]
-            h, cc = self._Hbig, (c0 + self.c_cols[0], c0 + self.c_cols[1])
         if draw:                # (else drawn ahead by the graph's multi-step sampler launch, _draw_all)
             o.sample_train(self.tables, h, self.z_cols, cc, self.Xall[2 * B:4 * B], self.X_real, self.Dd,
                            self.col2, self.opt2, step_counter=(self.stepD, self.stepG), metrics=self.metrics,
@@ -911,6 +834,10 @@ class CTGANEngine:
         # otherwise D0's weight gradient may be the GEMM held for the Adam launch (its operands, A0 and X, are
         # final here: the R chain below writes only dl[*][I])
         d0_fused = pair and not fuse_d and self.cfg.fuse_d0_adam and getattr(o, "gemm_adam", False)
+        # a short-K D0 weight gradient (the wide table's 256 x 137,800 over 150 rows) applies Adam itself, launched
+        # just before the optimizer launch (gemm(..., group=6)): R0 -- which reads W0 -- is then no pair partner
+        d0_pre = pair and not d0_fused and self.cfg.fuse_d0_shortk and \
+            getattr(o, "shortk_ok", lambda *a: False)(self.ddims[0], self.K1, 3 * nP)
         for i in range(L):
             last_fused = fuse_d and i == L - 1
             with self._lane(1 + i % 2):
@@ -918,6 +845,9 @@ class CTGANEngine:
                 if i == 0 and d0_fused:
                     kw = {"tile": 64 if self.cfg.dw0_tile not in (32, 64) else self.cfg.dw0_tile}   # gemm_adam tiles
                     grp = 3
+                elif i == 0 and d0_pre:
+                    kw = {"splitk": 1}
+                    grp = 7 if (self.cfg.keep_grads or getattr(self, "keep_grads", False)) else 6
                 else:
                     grp = 3 if last_fused else (1 if pair else 0)
                 o.gemm(self.A[i], prev, self.g[f"D.{i}.W"], ta=True, group=grp, **kw)
@@ -929,7 +859,7 @@ class CTGANEngine:
                        ms=self.ms[i + 1][I], group=4)
                 rk = {"chain": True}
             o.gemm(inp, self.p[f"D.{i}.W"], self.dl[i][I], tb=True, epi=EPI_MASK, ms=self.ms[i][I],
-                   group=2 if (pair and not (i == 0 and d0_fused)) else 0, **rk)
+                   group=2 if (pair and not (i == 0 and (d0_fused or d0_pre))) else 0, **rk)
             inp = self.dl[i][I]
             prev = self.dl[i]
         # (the column sums are folded into the Adam launch: those workgroups update the bias / head

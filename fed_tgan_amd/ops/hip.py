@@ -110,11 +110,10 @@ def _effective_splits(K: int, sk: int, kc: int) -> int:
 
 class HipOps:
     name = "hip"
-    bn_fold_capable = True       # EngineConfig.bn_fold (gemm_bnl_next + BN partials)
-    bn_publish_capable = True    # EngineConfig.bn_fold_publish (gemm_bnpub_next)
     adam_counts_steps = False    # step counters are bumped by the sampler launch of each phase
     gemm_adam = True             # gemm(..., group=3) + adam(jobs=...) run as one launch
     achain_capable = True        # EngineConfig.fuse_achain (gemm_achain_next)
+    shortk_min_n = 16384         # mirrors the native gemm_shortk_min_n (set both to route narrower products)
 
     def __init__(self, device: torch.device, seed: int = 0, precision: str = "bf16", mem=None):
         self.L = native.require()
@@ -325,22 +324,16 @@ class HipOps:
         tile, sk = _plan(M, N, K, kc, self._plan_clients())
         return self.tile_override or tile, _effective_splits(K, self.split_override or sk, kc)
 
-    def gemm_bnpub_next(self, cnt, mean, invstd, rm, rv, momentum, eps):
-        """The next gemm() with bn_part also publishes the final BatchNorm statistics from its last workgroup per
-        column tile (csrc/kernels/launch.h GemmArgs::bnf_*, EngineConfig.bn_fold_publish)."""
-        self.L.gemm_bnpub_next(cnt, mean, invstd, rm, rv, float(momentum), float(eps))
+    def shortk_ok(self, M: int, N: int, K: int) -> bool:
+        """Does C [M, N] = A^T B over K rows run as the short-K strip kernel (csrc gemm_shortk_kernel; the shape
+        contract of gemm_shortk_ok for 16-B aligned row-major operands, default gemm_shortk_min_n)?"""
+        return (not self.f32 and getattr(self, "batch_k", 1) == 1 and M <= 256 and M % 4 == 0 and 1 <= K <= 160
+                and N % 4 == 0 and N >= self.shortk_min_n)
 
     def gemm_achain_next(self, out, ws, cnt):
         """The next chain tail (gemm(..., group=4) with a head seed) also forms the head's backward link
         out = (A1 W1) . MS0 in the chain launch (csrc/kernels/launch.h GemmArgs::ach_*, EngineConfig.fuse_achain)."""
         self.L.gemm_achain_next(out, ws, cnt)
-
-    def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
-        """The next gemm() stages relu(BatchNorm(a)) for the given column ranges of its A operand (see
-        csrc/kernels/launch.h GemmArgs::bnl and EngineConfig.bn_fold)."""
-        self.L.gemm_bnl_next(list(part), list(mean), list(invstd), list(gamma), list(beta), list(rm), list(rv),
-                             list(nhat), [int(k) for k in k0], [int(t) for t in ptm], int(rpg), float(momentum),
-                             float(eps), out)
 
     def linear_bn_relu(self, x, W, b, gamma, beta, out, abuf, nhat, mean, invstd, rmean, rvar, training=True,
                        momentum=0.1, eps=1e-5, groups=1, onehot=None):

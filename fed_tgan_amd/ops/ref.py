@@ -26,24 +26,10 @@ EPI_RELU = 3
 class TorchOps:
     adam_counts_steps = True     # eager Adam bumps its step counter (the HIP sampler does it there)
     name = "torch"
-    # EngineConfig.bn_fold on this backend (the GEMM-folded BatchNorm stated in torch: the oracle of the HIP
-    # path's partials / BN-on-load / materialisation; off by default -- the eager path runs BN as its own op)
-    bn_fold_capable = False
-    _bnl = None                  # pending gemm_bnl_next configuration (class default: subclasses need no __init__)
-
-    def __init__(self):
-        self._bnl = None
 
     # ------------------------------------------------------------------ GEMM
     def gemm_plan(self, M: int, N: int, K: int):
         return 32, 1
-
-    def gemm_bnl_next(self, part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm, rpg, momentum, eps, out=None):
-        """The next gemm() multiplies relu(BatchNorm(a)) for these column ranges of its A (see HipOps)."""
-        if self._bnl is not None:
-            raise RuntimeError("gemm_bnl_next: a configuration is already pending")
-        self._bnl = (list(zip(part, mean, invstd, gamma, beta, rm, rv, nhat, k0, ptm)), int(rpg), float(momentum),
-                     float(eps), out)
 
     @staticmethod
     def _bn_partials(v: torch.Tensor, part: torch.Tensor, rpg: int, tile: int):
@@ -62,49 +48,6 @@ class TorchOps:
                 pv[t, b, 1] = mu
                 pv[t, b, 2] = ((x - mu) ** 2).sum(0)
 
-    def _bn_on_load(self, A: torch.Tensor) -> torch.Tensor:
-        ranges, rpg, mom, eps, out = self._bnl
-        self._bnl = None
-        M = A.shape[0]
-        ng = 2 if M > rpg else 1
-        A = A.clone()
-        for part, mean, istd, gm, bt, rm, rv, nh, k0, ptm in ranges:
-            w = gm.numel()
-            x = A[:, k0:k0 + w]
-            if part is not None:        # merge the producer's tiles (Chan), publish, advance the running stats
-                pv = part.view(-1, 2, 3, w)
-                for b in range(ng):
-                    n = torch.zeros(w, dtype=A.dtype, device=A.device)
-                    mu = torch.zeros_like(n)
-                    m2 = torch.zeros_like(n)
-                    t0, t1 = (rpg // ptm, (M - 1) // ptm) if b else (0, (min(rpg, M) - 1) // ptm)
-                    for t in range(t0, t1 + 1):
-                        nb, mb, m2b = pv[t, b, 0], pv[t, b, 1], pv[t, b, 2]
-                        nt = n + nb
-                        d = mb - mu
-                        f = torch.where(nt > 0, nb / nt.clamp_min(1), torch.zeros_like(nt))
-                        mu = mu + d * f
-                        m2 = m2 + m2b + d * d * torch.where(nt > 0, n * nb / nt.clamp_min(1), torch.zeros_like(nt))
-                        n = nt
-                    var = torch.where(n > 0, m2 / n.clamp_min(1), torch.zeros_like(n))
-                    mean.view(-1, w)[b].copy_(mu)
-                    istd.view(-1, w)[b].copy_(torch.rsqrt(var + eps))
-                    unb = rpg / max(rpg - 1, 1)
-                    with torch.no_grad():
-                        rm.mul_(1 - mom).add_(mom * mu)
-                        rv.mul_(1 - mom).add_(mom * var * unb)
-            rows_b = (torch.arange(M, device=A.device) >= rpg).long()
-            mu_r = mean.view(-1, w)[rows_b]
-            is_r = istd.view(-1, w)[rows_b]
-            nhat_v = (x - mu_r) * is_r
-            y = torch.relu(nhat_v * gm + bt)
-            A[:, k0:k0 + w] = y
-            if out is not None:
-                nh.copy_(nhat_v)
-        if out is not None:
-            out[:, :A.shape[1]].copy_(A)
-        return A
-
     def gemm(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, epi=EPI_NONE, ms=None,
              slope=0.2, p_drop=0.5, stream_id=0, head=None, group=0, onehot=None, bn_part=None, bn_rpg=0, tile=None,
              splitk=None, **_):
@@ -115,8 +58,6 @@ class TorchOps:
         bn_part (with bn_rpg, tile): also the per-tile BatchNorm partials of the stored output."""
         A = a.t() if ta else a
         B = b.t() if tb else b
-        if self._bnl is not None:
-            A = self._bn_on_load(A)
         acc = torch.matmul(A, B)
         if alpha != 1.0:
             acc = acc * alpha

@@ -19,9 +19,8 @@ DEV = torch.device("cuda:0")
 def _twin_cfg(cfg):
     """A single-client engine issuing the batched engine's launch sequence: the batched step never chains
     D1 into D0's reduction launch nor fuses D1's weight gradient into the D Adam (models/engine.py,
-    batch_k > 1) -- fp32 epilogue paths that are close to, not bitwise equal to, the bf16-operand GEMMs -- and runs
-    the generator's BatchNorm as its own launches (EngineConfig.bn_fold is a one-client launch sequence)."""
-    return dataclasses.replace(cfg, chain_d1=False, fuse_d_adam=False, bn_fold=False)
+    batch_k > 1) -- fp32 epilogue paths that are close to, not bitwise equal to, the bf16-operand GEMMs."""
+    return dataclasses.replace(cfg, chain_d1=False, fuse_d_adam=False)
 
 
 def _client_tables(X, k):
@@ -194,7 +193,7 @@ def test_batched_ragged_clients_bit_identical_to_single_engines():
     rows = [9000, 5000, 1000]
     data = [X[rng.integers(0, len(X), n)] for n in rows]
     # no D1 chain / fused D Adam: the launch sequence of one client alone (k = 1) is then the batched one
-    cfg = EngineConfig(batch_size=500, chain_d1=False, fuse_d_adam=False, bn_fold=False)
+    cfg = EngineConfig(batch_size=500, chain_d1=False, fuse_d_adam=False)
     seeds = [3000 + c for c in range(3)]
     bc = BatchedClients(tr.layout, cfg, DEV, seeds, n_rows=max(rows))
     bc.engines[0].ops.batch_plan = False

@@ -31,7 +31,7 @@ def _engine(precision="bf16", g_wt=False, wide=False):
     else:
         _, _, _, _, _, _, tr, X = small_table()
     torch.manual_seed(0)
-    cfg = EngineConfig(batch_size=500, precision=precision, g_wt=g_wt or wide)
+    cfg = EngineConfig(batch_size=500, precision=precision, g_wt=g_wt or wide, keep_grads=True)
     if wide:
         cfg.onehot_wgrad_min = 1
     eng = CTGANEngine(tr.layout, cfg, DEV, backend="hip", seed=11)
@@ -209,8 +209,7 @@ def test_large_batches_train(batch):
     eng._prepare_paired()
     torch.cuda.synchronize()
     B, g0 = eng.B, eng.gdims[0]
-    # the layer's pre-BN output: the GEMM's scratch, or (EngineConfig.bn_fold) the pre-BN rows beside H
-    a = eng.Hp2[:, eng.off[1]:eng.off[0]] if eng._fold_on() else eng.abuf2[0]
+    a = eng.abuf2[0]          # the layer's pre-BN output (the GEMM's scratch)
     out = eng.H2[:, eng.off[1]:eng.off[0]]
     for h in (slice(0, B), slice(B, 2 * B)):
         ref = torch.relu(F.batch_norm(a[h], None, None, eng.p["G.0.gamma"], eng.p["G.0.beta"], True, 0.1, 1e-5))
@@ -495,66 +494,19 @@ def test_chain_tail_prefetch_matches_plain(batch):
         assert torch.equal(f, f0), float((f - f0).abs().max())
 
 
-@pytest.mark.parametrize("publish", [True, False])
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_bn_fold_matches_bn_launches(precision, publish):
-    """EngineConfig.bn_fold: the generator's BatchNorm folded into its GEMMs (partials from the producing GEMM,
-    relu(BN(a)) staged by the consumers, materialised by the output GEMM) gives the forward of the GEMM +
-    bn_relu_train launches -- activations, nhat, batch and running statistics, logits -- up to the statistics'
-    summation order (and bf16 rounding of the staged operands), and trains the same.  publish: the producing
-    GEMM's last workgroup per column tile merges the partials and publishes the statistics
-    (EngineConfig.bn_fold_publish); otherwise every consumer workgroup merges them."""
-    from fed_tgan_amd.ops import native
-    native.require()
-    _, _, _, _, _, _, tr, X = small_table()
-    engs = []
-    for fold in (False, True):
-        torch.manual_seed(0)
-        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, precision=precision, bn_fold=fold,
-                                                  bn_fold_publish=publish), DEV,
-                          backend="hip", seed=21)
-        eng.set_training_data(X)
-        engs.append(eng)
-    a, b = engs
-    b.flat.copy_(a.flat)
-    assert not a._fold_on() and b._fold_on()
-    for e in engs:
-        e._prepare_paired()
-    torch.cuda.synchronize()
-    tol = 2e-5 if precision == "fp32" else 2e-2
-    c0 = a.c_cols[0]
-    for i in range(len(a.gdims)):
-        assert _rel(b.bn_mean2[i], a.bn_mean2[i]) < 1e-5, i
-        assert _rel(b.bn_invstd2[i], a.bn_invstd2[i]) < 1e-4, i
-        assert _rel(b.p[f"G.{i}.rm"], a.p[f"G.{i}.rm"]) < 1e-5 and _rel(b.p[f"G.{i}.rv"], a.p[f"G.{i}.rv"]) < 1e-4
-        assert _rel(b.nhat2[i], a.nhat2[i]) < tol, (i, _rel(b.nhat2[i], a.nhat2[i]))
-    assert _rel(b.H2[:, :c0], a.H2[:, :c0]) < tol, _rel(b.H2[:, :c0], a.H2[:, :c0])
-    assert torch.equal(b.H2[:, c0:], a.H2[:, c0:])          # the condition block, written by the sampler
-    assert _rel(b.logits2, a.logits2) < (1e-4 if precision == "fp32" else 5e-2)
-    # whole steps: the same training up to rounding
-    for e in engs:
-        e.train_steps(3, use_graph=False)
-    torch.cuda.synchronize()
-    assert _rel(b.flat, a.flat) < 1e-3, _rel(b.flat, a.flat)
-    b.train_steps(8)            # graph capture of the folded step
-    ld, lg = b.losses()
-    assert np.isfinite(ld) and np.isfinite(lg)
-
-
-def test_bn_fold_config_is_checked():
-    """gemm_bnl_next refuses ranges the kernel cannot stage, and a pending configuration is consumed (or
-    dropped by reset_held) -- never applied to a later, unrelated GEMM."""
+def test_pending_achain_is_checked_and_dropped():
+    """gemm_achain_next refuses operands the kernel cannot use, and a pending configuration is consumed by the next
+    chain tail or dropped by reset_held -- never applied to a later, unrelated GEMM."""
     from fed_tgan_amd.ops import native
     L = native.require()
     f = lambda *s: torch.zeros(*s, device=DEV)  # noqa: E731
-    w = 64
-    args = lambda width, k0: ([None], [f(2, width)], [f(2, width)], [f(width)], [f(width)], [f(width)], [f(width)],  # noqa: E731
-                              [None], [k0], [32], 100, 0.1, 1e-5, None)
+    cnt = torch.zeros(10, dtype=torch.int32, device=DEV)
     with pytest.raises(RuntimeError):
-        L.gemm_bnl_next(*args(258, 0))        # wider than 256
+        L.gemm_achain_next(f(10, 256), f(4 * 10 * 256), cnt.float())       # counters must be int32
+    L.gemm_achain_next(f(10, 256), f(4 * 10 * 256), cnt)
+    from fed_tgan_amd.ops.hip import HipOps
     with pytest.raises(RuntimeError):
-        L.gemm_bnl_next(*args(w, 2))          # k0 not a multiple of 4
-    L.gemm_bnl_next(*args(w, 0))
+        HipOps(DEV).gemm(f(10, 8), f(4, 8), f(10, 4), tb=True)    # not a chain tail: refused, still pending
     assert L.reset_held() == 1 and L.reset_held() == 0
 
 

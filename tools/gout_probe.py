@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--N", type=int, default=7018)
     ap.add_argument("--K", type=int, default=640)
     ap.add_argument("--C", type=int, default=6762)
+    ap.add_argument("--k1", type=int, default=137800, help="packed D input width (pac x row width)")
     args = ap.parse_args()
     from fed_tgan_amd.ops.hip import HipOps
     dev = torch.device("cuda:0")
@@ -42,7 +43,8 @@ def main():
     M, N, K, C = args.M, args.N, args.K, args.C
     g = torch.Generator(device="cpu").manual_seed(0)
     x = torch.randn(M, K, generator=g).to(dev)
-    Wst = (torch.randn(K + C, N, generator=g) * 0.02).to(dev)      # input-major storage [in, out]
+    Np = -(-N // 4) * 4                                              # rows padded to 16 B, as the engine's flat buffer
+    Wst = (torch.randn(K + C, Np, generator=g) * 0.02).to(dev)[:, :N]   # input-major storage [in, out]
     W = Wst.t()                                                      # logical [out, in] (transposed view)
     Wd = Wst[:K].t().contiguous()                                    # dense part as [out, K] rows (TB = true)
     b = torch.randn(N, generator=g).to(dev)
@@ -64,8 +66,35 @@ def main():
     ob = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     res["torch_mm_bf16"] = timed(lambda: torch.mm(xb, wb, out=ob), args.reps)
     res["copy_out_28MB"] = timed(lambda: out.fill_(1.0), args.reps)
+    del Wst, W, Wd, xb, wb, ob, out
+    # the two long-K / short-K discriminator GEMMs of the same step: dW0 = A0^T X (K = 150 rows) and the D-phase
+    # D0 forward X W0^T (150 x 256, K = 137,800)
+    K1, R, H = args.k1, 150, 256
+    X = torch.randn(R, K1, generator=g).to(dev)
+    A0 = torch.randn(R, H, generator=g).to(dev)
+    W0 = (torch.randn(H, K1, generator=g) * 0.01).to(dev)
+    dW = torch.empty(H, K1, device=dev)
+    res["dW0_shortk"] = timed(lambda: o.gemm(A0, X, dW, ta=True), args.reps)
+    ref = dW.clone()
+    prev = torch.ops.fedtgan.set_tuning("gemm_shortk", 0)
+    for tile in (None, 64, 128):
+        tag = f"tile{tile or 'auto'}"
+        res[f"dW0_{tag}"] = timed(lambda: o.gemm(A0, X, dW, ta=True, tile=tile), args.reps)
+    torch.ops.fedtgan.set_tuning("gemm_shortk", prev)
+    res["dW0_shortk_vs_tile_maxdiff"] = float((dW - ref).abs().max())
+    res["dW0_torch_fp32"] = timed(lambda: torch.mm(A0.t(), X, out=dW), args.reps)
+    res["dW0_torch_bf16"] = timed(lambda: torch.mm(A0.t().bfloat16(), X.bfloat16()), args.reps)
+    res["fill_141MB"] = timed(lambda: dW.fill_(1.0), args.reps)
+    d0 = torch.empty(R, H, device=dev)
+    res["D0fwd_auto"] = timed(lambda: o.gemm(X, W0, d0, tb=True), args.reps)
+    for sk in (8, 16, 32, 64):
+        res[f"D0fwd_sk{sk}"] = timed(lambda: o.gemm(X, W0, d0, tb=True, splitk=sk), args.reps)
+    for t, sk in ((128, 32), (128, 64), (64, 48), (64, 64)):
+        res[f"D0fwd_t{t}_sk{sk}"] = timed(lambda: o.gemm(X, W0, d0, tb=True, tile=t, splitk=sk), args.reps)
+    res["D0fwd_torch_fp32"] = timed(lambda: torch.mm(X, W0.t(), out=d0), args.reps)
+    res["read_W0_X"] = timed(lambda: (W0.sum(), X.sum()), args.reps)
     for k, v in res.items():
-        print(f"{k:36s} {v:8.2f} us", flush=True)
+        print(f"{k:36s} {v:10.4f}", flush=True)
     print(json.dumps({k: round(v, 2) for k, v in res.items()}))
 
 

@@ -9,7 +9,7 @@ mkdir -p $OUT
 cd $R
 W="python tools/run_config.py --spec wide --rows 100000 --clients 1 --epochs 2 --n-sample 10000"
 for i in 1 2; do
-  for v in "" "--engine fuse_d_adam=0 --engine fuse_d0_adam=1" "--plan WAVE_FILL_64=1" "--engine bn_fold=1"; do
+  for v in "" "--engine fuse_d_adam=0 --engine fuse_d0_adam=1" "--plan WAVE_FILL_64=1"; do
     timeout -k 10 200 $W $v 2>&1 | grep '"mean_sec_per_epoch_after_first"' >> $OUT/wide.jsonl || exit 1
   done
 done

@@ -66,6 +66,7 @@ def main():
             key, val = kv.split("=", 1)
             getattr(hip_ops, key)
             setattr(hip_ops, key, bool(int(val)) if isinstance(getattr(hip_ops, key), bool) else int(val))
+    if args.tuning:     # (before round 6 this loop sat under `if args.plan:` -- tuning alone was silently ignored)
         from fed_tgan_amd.ops import native
         for kv in args.tuning:
             key, val = kv.split("=", 1)
