@@ -91,6 +91,12 @@ class EngineConfig:
     gen_graph: bool = True      # GPU: replay the generation pass (per sample count) as one hipGraph
     precision: str = "bf16"     # GEMM operands on the HIP path: bf16 (fp32 accumulate) or exact fp32
     graph_unroll: int = 8       # GPU: training steps captured per hipGraph (fewer graph launches)
+    # GPU, one client: blocks of graph_unroll steps captured in ONE hipGraph (each block with its own multi-step
+    # sampler launch on the same buffer sets, so nothing but the graph boundary changes); 0 = as many as an epoch
+    # holds.  A/B knob, default 1: the device idles ~8.5 us between consecutive replays (step_breakdown_r6.txt),
+    # but one 80-step graph per epoch measured slower -- bench 15.98-16.41 vs 15.83-16.24 ms, the train phase
+    # 15.27-15.82 vs 15.20-15.24 ms (profiles/graph_blocks_r6.txt), as 40-step graphs did (multi_draw_ab_r6.txt)
+    graph_blocks: int = 1
     streams: bool = False       # GPU: overlap independent launches of a step on side HIP streams
     paired: bool = True         # draw + generate the D- and G-phase batches of a step in one pass
     # generator GEMMs multiply only the dense part of their input [... | z | c]; the one-hot
@@ -1094,9 +1100,16 @@ class CTGANEngine:
         if use_graph is None:
             use_graph = self._graphs_by_default()
         if use_graph:
-            # U steps per graph launch (the per-launch gap between graphs is paid n/U times)
+            # U steps per graph launch (the per-launch gap between graphs is paid n/U times), or a graph of B
+            # blocks of U steps (_graph_blocks) for the bulk of an epoch
             U = max(1, int(self.cfg.graph_unroll))
             left = n
+            big = U * self._graph_blocks()
+            if big > U and left >= big:
+                gb = self.graphs.get(self._graph_key(big)) or self._capture(big)
+                for _ in range(left // big):
+                    gb.replay()
+                left %= big
             if left >= U:
                 g = self.graphs.get(self._graph_key(U)) or self._capture(U)
                 for _ in range(left // U):
@@ -1116,6 +1129,15 @@ class CTGANEngine:
     def train_epoch(self, use_graph: bool | None = None):
         self.train_steps(self.steps_per_epoch, use_graph)
 
+    def _graph_blocks(self) -> int:
+        """U-step blocks per big step graph (EngineConfig.graph_blocks; 0: those of one epoch).  One client only:
+        a batched engine keeps one block per graph."""
+        if self.batch is not None or getattr(self.ops, "batch_k", 1) != 1:
+            return 1
+        U = max(1, int(self.cfg.graph_unroll))
+        b = int(self.cfg.graph_blocks)
+        return max(1, b if b > 0 else self.steps_per_epoch // U)
+
     def _graphs_by_default(self) -> bool:
         """Step graphs unless asked otherwise: on a GPU with the HIP backend.  The eager torch oracle
         (ops/ref.py) runs eagerly: on wide tables its step is tens of thousands of small ATen launches
@@ -1134,9 +1156,15 @@ class CTGANEngine:
         steps = self.steps_per_epoch if steps is None else int(steps)
         if self.tables and steps > 0 and self._graphs_by_default():
             U = max(1, int(self.cfg.graph_unroll))
-            if steps >= U and self._graph_key(U) not in self.graphs:
+            big = U * self._graph_blocks()
+            rest = steps
+            if big > U and steps >= big:
+                if self._graph_key(big) not in self.graphs:
+                    self._capture(big)
+                rest = steps % big
+            if rest >= U and self._graph_key(U) not in self.graphs:
                 self._capture(U)
-            if steps % U and self._graph_key(1) not in self.graphs:
+            if rest % U and self._graph_key(1) not in self.graphs:
                 self._capture(1)
         if self.gen_tables is not None and self.cfg.gen_graph and self.ops.name == "hip":
             for n in gen_rows:
@@ -1182,17 +1210,18 @@ class CTGANEngine:
             for dst, src in zip(state, snap):
                 dst.copy_(src)
         g = torch.cuda.CUDAGraph()
-        multi = self._multi and steps == self._U and self.batch is None
+        multi = self._multi and steps % self._U == 0 and self.batch is None
         try:
             with torch.cuda.graph(g, capture_error_mode=self.capture_mode):
                 if multi:
-                    # one launch draws every step's batch into its own buffer set; step k then runs on set k with
-                    # its own optimizer counters / metrics (written by that launch)
-                    self._bind_set(0, 0)
-                    self._draw_all()
-                    for k in range(steps):
-                        self._bind_set(k, k)
-                        self._one_step(draw=False)
+                    # one launch draws every step's batch of a block into its own buffer set; step k then runs on
+                    # set k with its own optimizer counters / metrics (written by that launch); blocks repeat
+                    for _ in range(steps // self._U):
+                        self._bind_set(0, 0)
+                        self._draw_all()
+                        for k in range(self._U):
+                            self._bind_set(k, k)
+                            self._one_step(draw=False)
                 else:
                     for _ in range(steps):      # every step re-reads the device RNG/step counters
                         self._one_step()

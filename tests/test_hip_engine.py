@@ -580,3 +580,27 @@ def test_fused_achain_matches_gemm_chain():
     for k in range(4):
         torch.testing.assert_close(out[1][k], out[0][k], rtol=1e-4, atol=1e-5 if k == 0 else 1e-6)
         assert torch.equal(out[1][k], out[2][k]), k
+
+
+@pytest.mark.gpu
+def test_multi_block_graph_matches_block_graphs():
+    """EngineConfig.graph_blocks: B blocks of graph_unroll steps captured in ONE hipGraph (each block with its own
+    multi-step sampler launch) train bitwise like one graph per block -- over a 2-block graph, a leftover block and
+    leftover single steps."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    out = []
+    for blocks in (1, 2):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, graph_unroll=4, graph_blocks=blocks), DEV,
+                          backend="hip", seed=7)
+        eng.set_training_data(X)
+        assert eng._graph_blocks() == blocks
+        eng.train_steps(14, use_graph=True)      # 8 (one 2-block graph or two block graphs) + 4 + 2 single
+        torch.cuda.synchronize()
+        assert (8 in eng.graphs) == (blocks == 2)
+        out.append((eng.flat.clone(), eng.mD.clone(), eng.vG.clone(), eng.stepD.clone(), eng.ops.ctr.clone()))
+    for name, a, b in zip(("flat", "mD", "vG", "stepD", "ctr"), *out):
+        assert torch.equal(a, b), name
+    assert float(out[1][3]) == 14.0
