@@ -125,10 +125,11 @@ class FedConfig:
     # stream).  None = on where it applies (one process per GPU, HIP bf16 generation with graphs, FedAvg)
     pipeline_sample: Optional[bool] = None
     # pipelined sampling: issue the table's body / gather / copy / writer hand-off after the next round's training
-    # is queued (their host time then overlaps it).  Off: measured no gain on one GPU (16.12-16.22 vs 16.11-16.25 ms)
-    # and +2 ms over an RCCL communicator, where that work queued beside the epoch stretches its kernels as
-    # train_sync=0 does (profiles/sync_r5.txt)
-    defer_handoff: bool = False
+    # is queued (their host time then overlaps it).  None = on without real process groups (one process per run):
+    # measured on the round-6 tree 15.76-15.81 vs 15.88-15.98 ms per round (profiles/round_sync_r6.txt; round 5:
+    # no gain, 16.12-16.22 vs 16.11-16.25); off over an RCCL communicator, where that work queued beside the epoch
+    # stretched its kernels by ~2 ms as train_sync=0 does (profiles/sync_r5.txt)
+    defer_handoff: Optional[bool] = None
     # HIP stream priority of the pipelined generation stream (torch convention: lower = higher priority; 0 normal).
     # HIP maps streams onto hardware queues round-robin in creation order, so a normal-priority side stream can
     # share the training stream's in-order queue (seen in a kernel trace: both on queue 1)
@@ -741,7 +742,10 @@ class FedRuntime:
         # (pipelined: the rows come from the generation side stream, and the gather / copy are ordered on it, so
         # the round ends without waiting for them -- the next round's training overlaps them)
         pipe = bool(getattr(self, "_pipe", False)) and self.rank in samplers
-        if pipe and async_copy and self.cfg.defer_handoff:
+        defer = self.cfg.defer_handoff
+        if defer is None:
+            defer = not bool(getattr(c, "dist_active", False))
+        if pipe and async_copy and defer:
             # only the prep (snapshot of the model) is issued now; the body, the gather, the copy and the writer
             # hand-off are issued by _complete_handoff once the next round's training is queued, so their host
             # time overlaps that training instead of the GPU idling behind it
