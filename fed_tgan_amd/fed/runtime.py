@@ -125,11 +125,12 @@ class FedConfig:
     # stream).  None = on where it applies (one process per GPU, HIP bf16 generation with graphs, FedAvg)
     pipeline_sample: Optional[bool] = None
     # pipelined sampling: issue the table's body / gather / copy / writer hand-off after the next round's training
-    # is queued (their host time then overlaps it).  None = on without real process groups (one process per run):
-    # measured on the round-6 tree 15.76-15.81 vs 15.88-15.98 ms per round (profiles/round_sync_r6.txt; round 5:
-    # no gain, 16.12-16.22 vs 16.11-16.25); off over an RCCL communicator, where that work queued beside the epoch
-    # stretched its kernels by ~2 ms as train_sync=0 does (profiles/sync_r5.txt)
-    defer_handoff: Optional[bool] = None
+    # is queued (their host time then overlaps it).  None = on without real process groups.  Default off: on the
+    # round-6 tree one box measured 15.76-15.81 vs 15.88-15.98 ms per round, a second box no gain (15.87-15.93 vs
+    # 15.79-15.86 on its settled pairs; profiles/round_sync_r6.txt), round 5 no gain either; over an RCCL
+    # communicator that work queued beside the epoch stretched its kernels by ~2 ms as train_sync=0 does
+    # (profiles/sync_r5.txt)
+    defer_handoff: Optional[bool] = False
     # HIP stream priority of the pipelined generation stream (torch convention: lower = higher priority; 0 normal).
     # HIP maps streams onto hardware queues round-robin in creation order, so a normal-priority side stream can
     # share the training stream's in-order queue (seen in a kernel trace: both on queue 1)
