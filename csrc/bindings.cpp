@@ -1301,11 +1301,6 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gp_split = value ? 1 : 0;
     return prev;
   }
-  if (key == "act_tail_reg") {
-    const int64_t prev = fedtgan::g_act_tail_reg;
-    fedtgan::g_act_tail_reg = value ? 1 : 0;
-    return prev;
-  }
   if (key == "act_row_mode") {
     TORCH_CHECK(value >= 0 && value <= 2, "act_row_mode: 0 per-wave, 1 row (LDS image), 2 row (registers; forward)");
     const int prev = fedtgan::g_act_row_mode;

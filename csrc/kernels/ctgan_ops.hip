@@ -353,7 +353,6 @@ __device__ __forceinline__ void slerp_weights(float saa, float sbb, float sab, f
   }
 }
 
-int g_act_tail_reg = 1;   // wide rows with the fused slerp: the condition-block tail in registers (activate_rowreg_kernel TREG)
 int g_act_row_mode = 2;   // wide rows: one 512-thread workgroup per row, register-resident (2) or LDS row image (1)
 constexpr int ACT_WAVES = 4;   // rows (waves) per workgroup when the LDS image allows it
 constexpr int ACT_PF = 8;      // logits prefetched per lane (rows up to 512 wide)
@@ -712,8 +711,7 @@ __global__ __launch_bounds__(ROW_WAVES * 64) void activate_row_kernel(const floa
 // contiguous column ranges).  Per-element LDS atomics (the LDS-image kernel above) serialise the lanes of a wave
 // that hit one span: on the wide table (7,018 columns, spans ~17 wide) the LDS pipe was busy ~40 us per CU per
 // launch (rocprofv3 SQ_LDS_IDX_ACTIVE, profiles/wide_pmc_r4.txt).
-// TREG: the fused slerp's condition-block tail is read in one round into registers (g_act_tail_reg)
-template <int GPW, int NW = ROW_WAVES, bool BT_ = false, bool TREG = false>
+template <int GPW, int NW = ROW_WAVES, bool BT_ = false>
 __global__ __launch_bounds__(NW * 64) void activate_rowreg_kernel(const float* __restrict__ logits, int ldl,
                                                                          float* __restrict__ out, int ldo, int rows,
                                                                          SpanTables sp, float inv_tau, uint64_t seed,
@@ -829,43 +827,22 @@ __global__ __launch_bounds__(NW * 64) void activate_rowreg_kernel(const float* _
         sab += ar[g][q] * xv[g][q];
       }
     }
-  // the condition-block tail (global: written by the sampler): up to TR columns per thread are requested in ONE
-  // round and kept in registers for the output pass (the wide table's 6,762-column tail was 2 x 4 dependent
-  // rounds of TU loads); longer tails loop TU at a time and re-read for the output pass
-  constexpr int TU = 4, TR = TREG ? 16 : 1;
-  const bool tail_reg = TREG && sl.cols - D <= TR * NTH;
-  float tra[TR], trf[TR];
-  if (tail_reg) {
+  constexpr int TU = 4;   // tail loads in flight per thread
+  for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
+    float ra[TU], fb[TU];
 #pragma unroll
-    for (int u = 0; u < TR; ++u) {
-      const int j = min(D + u * NTH + tid, sl.cols - 1);
-      tra[u] = a[j];
-      trf[u] = y[j];
+    for (int u = 0; u < TU; ++u) {
+      const int j = min(j0 + u * NTH + tid, sl.cols - 1);
+      ra[u] = a[j];
+      fb[u] = y[j];
     }
 #pragma unroll
-    for (int u = 0; u < TR; ++u)
-      if (D + u * NTH + tid < sl.cols) {
-        saa += tra[u] * tra[u];
-        sbb += trf[u] * trf[u];
-        sab += tra[u] * trf[u];
+    for (int u = 0; u < TU; ++u)
+      if (j0 + u * NTH + tid < sl.cols) {
+        saa += ra[u] * ra[u];
+        sbb += fb[u] * fb[u];
+        sab += ra[u] * fb[u];
       }
-  } else {
-    for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
-      float ra[TU], fb[TU];
-#pragma unroll
-      for (int u = 0; u < TU; ++u) {
-        const int j = min(j0 + u * NTH + tid, sl.cols - 1);
-        ra[u] = a[j];
-        fb[u] = y[j];
-      }
-#pragma unroll
-      for (int u = 0; u < TU; ++u)
-        if (j0 + u * NTH + tid < sl.cols) {
-          saa += ra[u] * ra[u];
-          sbb += fb[u] * fb[u];
-          sab += ra[u] * fb[u];
-        }
-    }
   }
   const float3 tot = block_sum3<NW>(saa, sbb, sab, red);
   RngArgs srng{seed, ctr, sl.stream};
@@ -880,14 +857,6 @@ __global__ __launch_bounds__(NW * 64) void activate_rowreg_kernel(const float* _
       const int j = (4 * (wv + NW * g) + q) * 64 + lane;
       if (j < D) o[j] = wa * ar[g][q] + wb * xv[g][q];
     }
-  if (tail_reg) {
-#pragma unroll
-    for (int u = 0; u < TR; ++u) {
-      const int j = D + u * NTH + tid;
-      if (j < sl.cols) o[j] = wa * tra[u] + wb * trf[u];
-    }
-    return;
-  }
   for (int j0 = D; j0 < sl.cols; j0 += TU * NTH) {
     float ra[TU], fb[TU];
 #pragma unroll
@@ -1332,19 +1301,12 @@ void launch_activate(const float* logits, int ldl, float* out, int ldo, int rows
     const size_t lds = (size_t)(sp.dim + 2 * sp.n_span + 3 * ROW_WAVES) * sizeof(float);
     const dim3 grid(rows, 1, cb.k), block(nw * 64);
     const bool xcd = cb.xcd != 0;
-    const bool treg = g_act_tail_reg && sl.real != nullptr && sl.cols - sp.dim <= 16 * (int)block.x;
 #define FEDTGAN_ACT_REG(G, W)                                                                                       \
   do {                                                                                                             \
     allow_big_lds(activate_rowreg_kernel<G, W, false>, lds);                                                       \
     allow_big_lds(activate_rowreg_kernel<G, W, true>, lds);                                                        \
-    allow_big_lds(activate_rowreg_kernel<G, W, false, true>, lds);                                                 \
-    allow_big_lds(activate_rowreg_kernel<G, W, true, true>, lds);                                                  \
-    if (treg)                                                                                                      \
-      hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, W, true, true> : activate_rowreg_kernel<G, W, false, true>), \
-                         grid, block, lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb); \
-    else                                                                                                           \
-      hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, W, true> : activate_rowreg_kernel<G, W, false>), grid, block, \
-                         lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);   \
+    hipLaunchKernelGGL((xcd ? activate_rowreg_kernel<G, W, true> : activate_rowreg_kernel<G, W, false>), grid, block, \
+                       lds, stream, logits, ldl, out, ldo, rows, sp, 1.f / tau, seed, ctr, stream_id, sl, cb);     \
     return;                                                                                                        \
   } while (0)
     if (nw == 2 && gpw <= 1) FEDTGAN_ACT_REG(1, 2);

@@ -298,7 +298,6 @@ extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int64_t g_adam_u_min;   // Adam launches over >= this many float4 (x clients) load ADAM_U float4 per thread
 extern int g_gemm_store_wt;   // GEMM outputs / split-K slabs: plain (0) or write-through sc1 (1)
-extern int g_act_tail_reg;         // activate_rowreg_kernel: fused slerp's condition tail read once into registers
 extern int g_gemm_shortk;          // 1: C = A^T B with K <= 160, M <= 256 and wide N by gemm_shortk_kernel
 extern int g_gemm_shortk_min_n;    // narrowest N that takes it
 extern int g_gemm_shortk_store;    // its output stores: 0 plain, 1 non-temporal, 2 write-through (sc1)
