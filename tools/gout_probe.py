@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--K", type=int, default=640)
     ap.add_argument("--C", type=int, default=6762)
     ap.add_argument("--k1", type=int, default=137800, help="packed D input width (pac x row width)")
+    ap.add_argument("--only-gout", action="store_true", help="just the engine-layout G.out launch (counter runs)")
     args = ap.parse_args()
     from fed_tgan_amd.ops.hip import HipOps
     dev = torch.device("cuda:0")
@@ -54,6 +55,10 @@ def main():
     off = (torch.arange(8, dtype=torch.int32) * (C // 8)).to(dev)
     oh = (W[:, K:], col, opt, off)
     res = {}
+    if args.only_gout:
+        res["gout_engine_layout"] = timed(lambda: o.gemm(x, W[:, :K], out, tb=True, bias=b, onehot=oh), args.reps)
+        print(json.dumps(res))
+        return
     for tile in (None, 64, 128):
         tag = f"tile{tile or 'auto'}"
         res[f"inmajor_onehot_bias_{tag}"] = timed(
