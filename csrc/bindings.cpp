@@ -1389,6 +1389,11 @@ int64_t set_tuning(const std::string& key, int64_t value) {
     fedtgan::g_gemm_pair_max_wg = (int)value;
     return prev;
   }
+  if (key == "gemm_xcd_nmajor") {
+    const int64_t prev = fedtgan::g_gemm_xcd_nmajor;
+    fedtgan::g_gemm_xcd_nmajor = value ? 1 : 0;
+    return prev;
+  }
   if (key == "gemm_xcd_remap") {
     const int64_t prev = fedtgan::g_gemm_xcd_remap;
     TORCH_CHECK(value >= 0 && value <= 2, "gemm_xcd_remap: 0 off, 1 long-K tiles, 2 always");

@@ -556,16 +556,22 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
   // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with
   // its own L2), so consecutive workgroup ids -- the N tiles sharing one A row block -- would land
   // on 8 different L2s.  Remap so each XCD gets a contiguous run of logical tiles.
+  // Order 2 (host: when it touches fewer operand bytes per XCD, e.g. a wide output over a short M) walks the
+  // logical tiles M-fastest, so an XCD's run is a few N column strips over every row block: its L2 then holds a
+  // 1/8 slice of B instead of all of it (the tail past 8 * per decodes the same way, so the map stays a bijection).
   if (g.xcd_remap) {
     const int total = gx * gy * gz;
     const int lin = bx + gx * (by + gy * bz);
     const int per = total / 8;
-    if (lin < 8 * per) {
-      const int logical = (lin % 8) * per + lin / 8;
+    const int logical = lin < 8 * per ? (lin % 8) * per + lin / 8 : lin;
+    if (g.xcd_remap == 2) {
+      by = logical % gy;
+      bx = (logical / gy) % gx;
+    } else {
       bx = logical % gx;
       by = (logical / gx) % gy;
-      bz = logical / (gx * gy);
     }
+    bz = logical / (gx * gy);
   }
   const int n0 = bx * TN, m0 = by * TM;
   const int kb = bz * g.kchunk;
@@ -1031,6 +1037,7 @@ constexpr int GEMM_MAX_SPLITS = 64;
 // even on the short-K step GEMMs (the round-2 measurement that kept it off there predates the pair / chain
 // launches)
 int g_gemm_xcd_remap = 2;
+int g_gemm_xcd_nmajor = 1;
 int g_gemm_store_wt = 0;   // 1: write-through (sc1) output / slab stores
 int g_gemm_pairs = 1;      // 1: independent GEMM pairs share one launch (launch_gemm_pair)
 int g_gemm_pair_max_wg = 0;   // pairs whose two grids together exceed this many workgroups launch separately (0: no limit)
@@ -1346,6 +1353,15 @@ static dim3 gemm_prepare(GemmArgs& g) {
   g.xcd_remap = g_gemm_xcd_remap == 2 ||
                 (g_gemm_xcd_remap == 1 && ((g.splitk > 1 && kchunk >= 512) || (g.splitk == 1 && g.K >= 768) ||
                                            (T == 128 && tm >= 64) || (int64_t)tm * tn * g.splitk >= 1024));
+  // M-fastest order when an XCD's run of per = tiles / 8 logical tiles then spans fewer operand rows (row blocks
+  // x T of A + column tiles x T of B, both K long): the wide table's G out, 8 x 55 tiles, 7,168 -> 1,920 rows per
+  // XCD.  Same tiles, same sums: only which XCD (L2) computes a tile changes.
+  if (g.xcd_remap && g_gemm_xcd_nmajor && g.splitk == 1) {
+    const int64_t per = std::max<int64_t>((int64_t)tm * tn / 8, 1);
+    const int64_t r1 = (per + tn - 1) / tn + 1, c1 = std::min<int64_t>(per, tn);   // N-fastest (order 1)
+    const int64_t r2 = std::min<int64_t>(per, tm), c2 = (per + tm - 1) / tm + 1;   // M-fastest (order 2)
+    if (4 * (r2 + c2) < 3 * (r1 + c1)) g.xcd_remap = 2;
+  }
   return dim3(tn, tm, g.splitk);
 }
 

@@ -67,7 +67,7 @@ struct GemmArgs {
   int vec;     // 1: both operands may be read with 16-B loads (see gemm.hip Chunk::load)
   int tile;    // output tile edge: 64 (default) or 32 (4x the workgroups, for short-K GEMMs)
   int f32;     // 1: exact-fp32 MFMA (v_mfma_f32_16x16x4_f32); 0: bf16 operands, fp32 accumulate
-  int xcd_remap;   // 1: XCD-contiguous tile order (set by launch_gemm)
+  int xcd_remap;   // XCD-contiguous tile order (set by launch_gemm): 1 N-fastest, 2 M-fastest
   int wt;          // 1: write-through (sc1) output stores (set by launch_gemm)
   // One-hot conditional block (nullable): the K columns of op(A) are only the DENSE part of the
   // input; its trailing one-hot block (the conditional vector c, exactly one 1 per row at
@@ -294,6 +294,7 @@ bool launch_gemm_adam(GemmArgs g, float* p, const float* gr, float* m, float* v,
                       hipStream_t stream);
 
 extern int g_gemm_xcd_remap;   // GEMM XCD-contiguous tile order: 0 off, 1 long-K tiles, 2 always
+extern int g_gemm_xcd_nmajor;  // let a GEMM take the M-fastest XCD tile order when it touches fewer bytes
 extern int g_adam_store;       // Adam p/m/v store policy: 0 plain, 2 nt, 16 sc1 write-through
 extern int g_adam_max_blocks;  // Adam grid cap (grid-stride beyond it)
 extern int64_t g_adam_u_min;   // Adam launches over >= this many float4 (x clients) load ADAM_U float4 per thread

@@ -116,6 +116,11 @@ class FedConfig:
     # the generation graph, the pinned D2H copy and the CSV hand-off while the 80-step epoch still runs
     # stretches the epoch's kernels by ~2 ms (profiles/bench_train_sync_r3.txt)
     train_sync: bool = True
+    # train_sync's wait, early: the host waits for the epoch's kernels up to (not including) the last N U-step
+    # graph blocks, so the aggregation / sampling issue and the next round's launches are queued while those
+    # blocks run instead of the device idling behind the host's round boundary (0 = wait for the whole epoch;
+    # used with round_sync=False -- its wait would put the idle back)
+    sync_lead_blocks: int = 0
     # wait on the host for the round's device work (aggregation, generation) before returning: the round time
     # then is device time; without it the next round's launches queue behind the generation and the host
     # returns at once (the epoch CSV's own hand-off waits for the table copy either way)
@@ -902,14 +907,18 @@ class FedRuntime:
                 c.g.wait()
             elif self.is_client and alive[c.client_index]:
                 hw = time.perf_counter()
-                self.engine.train_epoch(self.cfg.use_graph)
+                self.engine.train_epoch(self.cfg.use_graph, lead=max(int(self.cfg.sync_lead_blocks), 0))
                 hi = time.perf_counter()
                 if self.gradflow is not None:
                     self.gradflow.update(self.engine)
             # the previous round's deferred table work, now that this round's training is queued
             self._complete_handoff()
             if self.cfg.train_sync and self.device.type == "cuda":
-                stream_sync(self.device)
+                ev = getattr(self.engine, "lead_event", None) if self.cfg.sync_lead_blocks > 0 else None
+                if ev is not None:
+                    ev.synchronize()
+                else:
+                    stream_sync(self.device)
         # host-side seconds of the train phase: waiting at the entry barrier, issuing the epoch, until its end
         self._host_train = {"h_wait": (hw - h0) if hw else 0.0, "h_issue": (hi - hw) if hi else 0.0,
                             "h_total": time.perf_counter() - h0}

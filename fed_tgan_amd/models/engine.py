@@ -1094,9 +1094,13 @@ class CTGANEngine:
         if hasattr(self.ops, "end_step"):
             self.ops.end_step(self)
 
-    def train_steps(self, n: int, use_graph: bool | None = None):
+    def train_steps(self, n: int, use_graph: bool | None = None, lead: int = 0):
+        """n optimisation steps.  ``lead`` > 0 (graph path): ``lead_event`` is recorded on the stream before the
+        last ``lead`` U-step blocks, so a host that waits on it wakes while those blocks still run (None when the
+        epoch has fewer blocks or runs eagerly -- the caller then waits on the stream)."""
         if not self.tables:
             raise RuntimeError("set_training_data() first")
+        self.lead_event = None
         if use_graph is None:
             use_graph = self._graphs_by_default()
         if use_graph:
@@ -1112,7 +1116,10 @@ class CTGANEngine:
                 left %= big
             if left >= U:
                 g = self.graphs.get(self._graph_key(U)) or self._capture(U)
-                for _ in range(left // U):
+                nb = left // U
+                for i in range(nb):
+                    if lead and i == nb - lead:
+                        self._mark_lead()
                     g.replay()
                 left %= U
             if left:
@@ -1126,8 +1133,14 @@ class CTGANEngine:
         if hasattr(self.ops, "check"):
             self.ops.check()
 
-    def train_epoch(self, use_graph: bool | None = None):
-        self.train_steps(self.steps_per_epoch, use_graph)
+    def train_epoch(self, use_graph: bool | None = None, lead: int = 0):
+        self.train_steps(self.steps_per_epoch, use_graph, lead)
+
+    def _mark_lead(self):
+        if getattr(self, "_lead_ev", None) is None:
+            self._lead_ev = torch.cuda.Event()
+        self._lead_ev.record(torch.cuda.current_stream(self.device))
+        self.lead_event = self._lead_ev
 
     def _graph_blocks(self) -> int:
         """U-step blocks per big step graph (EngineConfig.graph_blocks; 0: those of one epoch).  One client only:

@@ -604,3 +604,23 @@ def test_multi_block_graph_matches_block_graphs():
     for name, a, b in zip(("flat", "mD", "vG", "stepD", "ctr"), *out):
         assert torch.equal(a, b), name
     assert float(out[1][3]) == 14.0
+
+
+def test_lead_event_marks_before_last_blocks():
+    """train_steps(..., lead=N) (FedConfig.sync_lead_blocks): an event recorded before the last N graph blocks;
+    the training itself is bitwise the same as without it."""
+    from fed_tgan_amd.ops import native
+    native.require()
+    _, _, _, _, _, _, tr, X = small_table()
+    out = []
+    for lead in (0, 1):
+        torch.manual_seed(0)
+        eng = CTGANEngine(tr.layout, EngineConfig(batch_size=500, graph_unroll=4), DEV, backend="hip", seed=7)
+        eng.set_training_data(X)
+        eng.train_steps(12, use_graph=True, lead=lead)
+        assert (eng.lead_event is not None) == (lead > 0)
+        if lead:
+            eng.lead_event.synchronize()
+        torch.cuda.synchronize()
+        out.append((eng.flat.clone(), eng.ops.ctr.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

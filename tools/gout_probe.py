@@ -37,8 +37,13 @@ def main():
     ap.add_argument("--C", type=int, default=6762)
     ap.add_argument("--k1", type=int, default=137800, help="packed D input width (pac x row width)")
     ap.add_argument("--only-gout", action="store_true", help="just the engine-layout G.out launch (counter runs)")
+    ap.add_argument("--tuning", action="append", default=[], metavar="KEY=VALUE", help="native set_tuning knob")
     args = ap.parse_args()
     from fed_tgan_amd.ops.hip import HipOps
+    from fed_tgan_amd.ops import native
+    for kv in args.tuning:
+        k, v = kv.split("=", 1)
+        native.require().set_tuning(k, int(v))
     dev = torch.device("cuda:0")
     o = HipOps(dev, seed=1, precision="bf16")
     M, N, K, C = args.M, args.N, args.K, args.C
