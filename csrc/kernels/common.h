@@ -157,14 +157,18 @@ __device__ __forceinline__ float2 box_muller(uint32_t a, uint32_t b) {
 __device__ __forceinline__ float gumbel(uint32_t x) { return -logf(neg_log_u(x)); }
 
 // round-to-nearest-even fp32 -> bf16 bits
+// fp32 -> bf16, round to nearest even: gfx950's v_cvt_pk_bf16_f32 (one VALU op per PAIR; fp32 denormals are kept,
+// amdhsa_float_denorm_mode_32 = 3) -- the same bits as the integer form (u + 0x7FFF + lsb) >> 16 it replaces for
+// every non-NaN input (a NaN now stays a quiet NaN instead of possibly rounding to infinity)
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float f32x2_hw __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  uint32_t r = ((u >> 16) & 1u) + 0x7FFFu;
-  return (uint16_t)((u + r) >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_hw){a, b}, bf16x2_hw));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -232,8 +232,17 @@ struct Chunk {
     return r0 + 4 * (t % RQ) + e < rmax && k0 + 2 * (t / RQ + (NT / RQ) * i) + half < kmax;
   }
 
-  // bf16 image [row][KC + 8]
+  // bf16 image [row][KC + 8].  A burst wholly inside the operand (every burst but an edge tile's) takes the
+  // unchecked body: no per-element bounds selects (counters on the wide G out: VALU instructions ~18x its MFMAs,
+  // most of them staging), same bits.
   __device__ __forceinline__ void store_bf16(uint16_t* s) const {
+    if (r0 + R <= rmax && k0 + KC <= kmax)
+      store_bf16_body<false>(s);
+    else
+      store_bf16_body<true>(s);
+  }
+  template <bool CHK>
+  __device__ __forceinline__ void store_bf16_body(uint16_t* s) const {
     const int t = threadIdx.x;
     if constexpr (ROWMAJ) {
 #pragma unroll
@@ -241,7 +250,7 @@ struct Chunk {
         const int r = t / (KC / 4) + (NT / (KC / 4)) * i, q = t % (KC / 4);
         float x[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[e] = ok_rm(i, e) ? v[i][e] : 0.f;
+        for (int e = 0; e < 4; ++e) x[e] = (!CHK || ok_rm(i, e)) ? v[i][e] : 0.f;
         *reinterpret_cast<uint2*>(&s[r * (KC + 8) + 4 * q]) = uint2{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])};
       }
     } else {
@@ -253,7 +262,7 @@ struct Chunk {
           const int row = 4 * rq + e;
           const int pk = (((2 * kp) >> 3) ^ lds_swz<KC>(row)) * 8 + ((2 * kp) & 7);   // swizzled k position
           *reinterpret_cast<uint32_t*>(&s[row * (KC + 8) + pk]) =
-              pack_bf16x2(ok_cm(i, 0, e) ? v[2 * i][e] : 0.f, ok_cm(i, 1, e) ? v[2 * i + 1][e] : 0.f);
+              pack_bf16x2((!CHK || ok_cm(i, 0, e)) ? v[2 * i][e] : 0.f, (!CHK || ok_cm(i, 1, e)) ? v[2 * i + 1][e] : 0.f);
         }
       }
     }
