@@ -309,7 +309,11 @@ def test_gpu_round_zero_costs_a_steady_round(tmp_path):
     # timestamp_experiment.csv: entry e ends when epoch e's table is on disk; the first one also holds the
     # write of table 0 that no earlier round overlaps
     assert len(stamps) == 4 and all(s > 0 for s in stamps)
-    assert max(stamps) <= 1.5 * steady, (stamps, r, res["metrics"])
+    assert max(stamps[1:]) <= 1.5 * steady, (stamps, r, res["metrics"])
+    # entry 0 = round 0 + table 0's write, which nothing overlaps: bounded by the steady round plus that write as the
+    # writer measured it (round 1's csv_write_prev; ~5-7 ms against a ~15 ms round since the round-6 step speed-up)
+    w0 = res["metrics"][1].get("csv_write_prev", 0.0)
+    assert stamps[0] <= 1.5 * steady + w0, (stamps, r, res["metrics"])
 
 
 def test_gpu_pipelined_sampling_matches_unpipelined(tmp_path):
