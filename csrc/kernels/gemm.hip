@@ -832,6 +832,47 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bx, int by, int
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           cs[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * (TN + 1) + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+    // fp32 output, unsplit, 16-B aligned rows: each thread owns a column quad and writes it as one 16-B store (a
+    // quarter of the store / index instructions of the per-element loop below; same arithmetic per element)
+    if (gz == 1 && !(BIN && g.c16) && (g.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(g.c) & 15) == 0) {
+      static_assert(NT % (TN / 4) == 0, "fixed column quad per thread");
+      const int nq = 4 * (threadIdx.x % (TN / 4));
+      float cb4[4];
+      ColEpi ce4[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int nc = min(n0 + nq + c, g.N - 1);
+        cb4[c] = g.bias ? g.bias[nc] : 0.f;
+        ce4[c] = col_epi(g, nc);
+      }
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(g.c, 0, 0x7FFFFFFF, 0x00020000);
+      for (int ml = threadIdx.x / (TN / 4); ml < TM; ml += NT / (TN / 4)) {
+        const int m = m0 + ml, n = n0 + nq;
+        if (m >= g.M || n >= g.N) continue;
+        float y[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v = g.alpha * cs[ml * (TN + 1) + nq + c];
+          if (g.beta != 0.f && n + c < g.N) v += g.beta * g.c[(size_t)m * g.ldc + n + c];
+          if (g.bias) v += cb4[c];
+          y[c] = PLAIN ? v : apply_epi_c(g, v, m, n + c, step, (uint64_t)m * g.N + n + c, ce4[c]);
+        }
+        const size_t e0 = (size_t)m * g.ldc + n;
+        if (n + 4 <= g.N) {
+          const f32x4 v4 = f32x4{y[0], y[1], y[2], y[3]};
+          if (g.wt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v4), crs, (int)(e0 * 4), 0, 16);
+          else
+            *reinterpret_cast<f32x4*>(g.c + e0) = v4;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (n + c < g.N) st_out(g.c, e0 + c, y[c], g.wt);
+        }
+      }
+      return;
+    }
     // each thread stays on one column (NT is a multiple of TN): its bias / BN parameters load once
     static_assert(NT % TN == 0, "fixed column per thread");
     const int nl = threadIdx.x % TN;
